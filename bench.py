@@ -1,0 +1,235 @@
+"""bench.py — the reference's headline metric on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2]
+
+Metric (BASELINE.json): Mray/s and ms/frame at 1920x1080 depth=3 on 1/2/4/8
+MI355X vs host CPU.  A step renders ONE full frame of the configured workload
+(default C2 = the reference's scene2.dat at 1920x1080, max bounces 3) from a
+scene already resident in HBM into an RGBA8 framebuffer in HBM.  With N ranks
+(one process per GPU, torch.distributed over RCCL) every rank renders its
+contiguous row slab and the slabs are assembled with one RCCL all-gather over
+xGMI inside the timed step (strong scaling: the frame is fixed).
+
+value = primary rays (= pixels) of all ranks / max-over-ranks time, in Mray/s.
+The roofline entry prices the trace kernel against the FP32 vector peak with
+the reference algorithm's operation count; the CPU baseline
+times the reference's own primitive code (oracle/_ref) on host cores over a
+bounded sample of the same frame.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "ray-tracing-gpu_amd"))
+SCENES = os.path.join(REPO, "tests", "golden", "scenes")
+
+# FP32 operations per work item of the reference algorithm.
+OPS_TRI, OPS_PLANE, OPS_QUAD = 52, 12, 103
+OPS_RAY_SETUP, OPS_SHADE_PER_LIT_LIGHT = 34, 75
+PEAK_FP32_TFLOPS = 157.3          # MI355X_MICROARCH.md: FP32 vector (= dense f32 MFMA) peak
+PEAK_NOFMA_TOPS = 78.6            # no FMA allowed by parity: packed v_pk_mul/add, 1 op/lane/clk x2
+
+CONFIGS = {
+    "c1": ("scene1.dat", 512, 512, 1),
+    "c2": ("scene2.dat", 1920, 1080, 3),
+    "c3": ("heightfield", 1920, 1080, 1),
+    "c4": ("scene2.dat", 3840, 2160, 5),
+    "c4s7": ("scene7.dat", 3840, 2160, 5),
+    "c4s9": ("scene9.dat", 3840, 2160, 5),
+    "c5": ("heightfield", 7680, 4320, 3),
+}
+
+
+def scene_path(name: str) -> str:
+    if name == "heightfield":
+        from rt_amd import synth
+
+        return synth.write_heightfield(os.path.join("/tmp", "rt_amd_heightfield.dat"))
+    return os.path.join(SCENES, name)
+
+
+def algorithmic_flops(types, primary, bounce, shadow):
+    import numpy as np
+
+    per_ray = (int(np.sum(types == 0)) * OPS_TRI + int(np.sum(types == 1)) * OPS_PLANE +
+               int(np.sum(types == 2)) * OPS_QUAD)
+    return (primary + bounce + shadow) * per_ray + primary * OPS_RAY_SETUP + shadow * OPS_SHADE_PER_LIT_LIGHT
+
+
+def cpu_baseline(path, w, h, depth, seconds):
+    """Time the reference's own primitive code (oracle/_ref, serial like the
+    reference) on 8x8 windows spread over the frame until `seconds` elapse;
+    fall back to the C restatement (oracle/liboracle.so) when _ref was not built."""
+    import numpy as np
+
+    ref = os.path.join(REPO, "oracle", "_ref", "libref_oracle.so")
+    port = os.path.join(REPO, "oracle", "liboracle.so")
+    VP = ctypes.c_void_p
+    if os.path.exists(ref):
+        L = ctypes.CDLL(ref)
+        kind, load, rend, free = "reference", L.ref_load, L.ref_render_window, L.ref_free
+        rend.argtypes = [VP, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, VP]
+        call = lambda p, r0, r1, c0, c1, buf: rend(p, r0, r1, c0, c1, buf)
+    else:
+        if not os.path.exists(port):
+            import subprocess
+
+            subprocess.run(["make", "-s", "-C", os.path.join(REPO, "oracle")], check=True)
+        L = ctypes.CDLL(port)
+        kind, load, rend, free = "port", L.oracle_load, L.oracle_render_window, L.oracle_free
+        rend.argtypes = [VP, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, VP, ctypes.c_int]
+        call = lambda p, r0, r1, c0, c1, buf: rend(p, r0, r1, c0, c1, buf, 1)
+    load.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(VP)]
+    free.argtypes = [VP]
+    p = VP()
+    assert load(path.encode(), w, h, depth, ctypes.byref(p)) == 0
+    buf = np.zeros((8, 8, 3), np.float32)
+    # 8x8 windows on a coarse grid, visited in a fixed scrambled order
+    wins = [(r, c) for r in range(0, h - 7, max(8, h // 32)) for c in range(0, w - 7, max(8, w // 32))]
+    order = np.random.default_rng(1234).permutation(len(wins))
+    px = 0
+    t0 = time.perf_counter()
+    k = 0
+    while True:
+        r, c = wins[order[k % len(wins)]]
+        call(p, r, r + 8, c, c + 8, buf.ctypes.data)
+        px += 64
+        k += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or (k >= len(wins) and el >= seconds / 4):
+            break
+    free(p)
+    return {"value": round(px / el / 1e6, 4), "unit": "Mray/s", "cores": 1, "kind": kind,
+            "sample": f"{k} 8x8 windows ({px} primary rays) on a {len(wins)}-window grid over the "
+                      f"{w}x{h} depth={depth} frame, {el:.1f} s, serial like the reference loop"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import numpy as np
+    import torch
+
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import rt_amd
+
+    name, W, H, depth = CONFIGS[args.config]
+    path = scene_path(name)
+    scene = rt_amd.Scene(path, W, H, depth)
+    ctx = rt_amd.Context(local)
+    ctx.upload(scene)
+    types = scene.arrays()[0]
+
+    rows = -(-H // world)                      # equal slabs (padded when H % world != 0)
+    r0, r1 = min(H, rank * rows), min(H, (rank + 1) * rows)
+    frame = scene.frame.copy()
+    frame.row_begin, frame.row_end = r0, r1
+    slab = torch.zeros((rows, W, 4), dtype=torch.uint8, device="cuda")
+    full = torch.zeros((world * rows, W, 4), dtype=torch.uint8, device="cuda") if world > 1 else slab
+    stream = torch.cuda.current_stream().cuda_stream
+
+    # one counted render (atomics) for the algorithmic work of this rank's slab
+    sf = frame.copy()
+    sf.flags = rt_amd.FLAG_STATS
+    ctx.render(sf)
+    st = ctx.stats()
+    flops = algorithmic_flops(types, st.primary_rays, st.bounce_rays, st.shadow_rays)
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record()
+        ctx.render_async(frame, slab.data_ptr(), 0, stream)
+        if ev is not None:
+            ev[1].record()
+        if world > 1:
+            dist.all_gather_into_tensor(full, slab)
+
+    for _ in range(args.warmup):
+        step()
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(events[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = sum(a.elapsed_time(b) for a, b in events) / args.steps
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        c = torch.tensor([st.primary_rays, st.bounce_rays, st.shadow_rays], dtype=torch.float64, device="cuda")
+        dist.all_reduce(c)
+        tot_primary, tot_bounce, tot_shadow = (float(x) for x in c.tolist())
+    else:
+        tot_primary, tot_bounce, tot_shadow = float(st.primary_rays), float(st.bounce_rays), float(st.shadow_rays)
+
+    if rank == 0:
+        ms = elapsed * 1e3 / args.steps
+        value = W * H * args.steps / elapsed / 1e6
+        achieved = flops / (kernel_ms * 1e-3) / 1e12
+        traffic = None
+        tfile = os.path.join(REPO, "profiles", "traffic.json")
+        if os.path.exists(tfile):
+            with open(tfile) as f:
+                traffic = json.load(f).get(f"{args.config}_n{world}")
+        out = {
+            "metric": "Mray/s and ms/frame at 1920x1080 depth=3, 1/2/4/8 MI355X vs host CPU",
+            "value": round(value, 3),
+            "unit": "Mray/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": f"reference scene file {name}" if name != "heightfield" else "synthetic 50k-triangle heightfield (rt_amd.synth)",
+            "config": {"workload": f"{name} {W}x{H} max_bounces={depth}", "width": W, "height": H,
+                       "max_bounces": depth, "surfaces": int(types.shape[0]),
+                       "parallelism": f"row-slab x{world}" + (" + RCCL all-gather" if world > 1 else "")},
+            "total_rays_per_s_M": round((tot_primary + tot_bounce + tot_shadow) * args.steps / elapsed / 1e6, 3),
+            "rays_per_frame": {"primary": int(tot_primary), "bounce": int(tot_bounce), "shadow": int(tot_shadow)},
+            "kernel_ms": round(kernel_ms, 4),
+            "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
+                         "frac_vs_nofma_issue_peak": round(achieved / PEAK_NOFMA_TOPS, 4),
+                         "flops_per_launch": int(flops), "kernel": f"rt_trace_kernel<{st.stack_depth}>"},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            cb = cpu_baseline(path, W, H, depth, args.cpu_seconds)
+            cb["gpu_over_cpu"] = round(value / cb["value"], 1) if cb["value"] else None
+            out["cpu_baseline"] = cb
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,142 @@
+/*
+ * rt.h — C ABI of the MI355X-native Whitted ray tracer (librt_amd.so).
+ *
+ * Drop-in boundary for the reference's per-pixel hot path.  The reference
+ * (Rodyll/Ray-Tracing-GPU, /root/reference/Projet-INF8702) exposes that path
+ * through the CScene singleton (Scene.h:41-70) and chooses the CPU loop or the
+ * GL compute shader inside CScene::LancerRayons (Scene.cpp:672) on the global
+ * CVar::g_ComputerShadersON (Var.cpp:11).  This header replaces:
+ *
+ *   rt_scene_*      CScene's host surface: AjusterResolution (Scene.cpp:162),
+ *                   AjusterNbRebondsMax / AjusterEnergieMinimale /
+ *                   AjusterIndiceRefraction (Scene.cpp:180-217),
+ *                   TraiterFichierDeScene (Scene.cpp:231), Initialiser
+ *                   (Scene.cpp:140: InitialiserCamera + Pretraitement) and the
+ *                   LancerRayons prologue (Scene.cpp:676-679).
+ *   rt_create /     CNuanceurCalculProg(path, compile) + activer()
+ *   rt_destroy      (NuanceurCalculProg.cpp:57,146) and the GL context.
+ *   rt_upload_scene the std140 UBO marshal "General"/"SceneData"
+ *                   (Scene.cpp:697-1269) — but file-ordered, unbounded, and
+ *                   without the ≤10-per-type cap.
+ *   rt_render*      glDispatchCompute(W/16,H/16,1) + glMemoryBarrier
+ *                   (Scene.cpp:1307-1310) and, for parity, the CPU loop
+ *                   (Scene.cpp:1538-1561) whose float RGB went to
+ *                   glTexImage2D(GL_RGBA8, GL_RGB, GL_FLOAT) (Scene.cpp:1562).
+ *
+ * Conventions: every call returns 0 on success, a negative RT_E* code on
+ * failure (the library never exits; see rt_last_error / rt_scene_error).
+ * Images are row-major, memory row y = pixel row PixY, row 0 = BOTTOM
+ * scanline (GL texture origin, Scene.cpp:1545-1546).  Thread-safe across
+ * contexts, not within one.
+ */
+#ifndef RT_AMD_RT_H
+#define RT_AMD_RT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+enum {
+    RT_OK = 0,
+    RT_E_ARG = -1,       /* bad argument / null pointer                 */
+    RT_E_IO = -2,        /* scene file cannot be opened                 */
+    RT_E_PARSE = -3,     /* scene file rejected (see rt_scene_error)    */
+    RT_E_STATE = -4,     /* call order violated (e.g. render before upload) */
+    RT_E_HIP = -5,       /* HIP runtime error (see rt_last_error)       */
+    RT_E_UNSUPPORTED = -6/* e.g. bounce depth beyond the compiled stack */
+};
+
+/* Surface kinds, file order is preserved in every array below. */
+enum { RT_TRIANGLE = 0, RT_PLANE = 1, RT_QUADRIC = 2 };
+
+/* Post-Pretraitement scene, FILE ORDER (the order of CScene::m_Surfaces).
+ * geom[i*12 + …]:
+ *   triangle: p0 p1 p2 (9)  normal (3)      — Triangle.h m_Pts / m_Normale
+ *   plane   : normal (3) cst (1) 0…         — Plan.h m_Normale / m_Cst
+ *   quadric : quad (3) lin (3) mix (3) cst  — Quadrique.h m_Quadratique /
+ *                                             m_Lineaire / m_Mixte / m_Cst
+ * material[i*10 + …]: r g b Ka Kd Ks shininess Kr Kt ior (ISurface.h:25-41)
+ * lights[j*7 + …]   : pos(3) r g b intensity (Lumiere.h:23-27)
+ * Caller owns the memory; rt_upload_scene deep-copies to the device. */
+typedef struct rt_scene_flat {
+    int32_t n_surfaces;
+    int32_t n_lights;
+    const int32_t* type;
+    const float* geom;
+    const float* material;
+    const float* lights;
+} rt_scene_flat;
+
+/* One frame (or one row slab of it, for multi-GPU sharding). */
+typedef struct rt_frame {
+    float cam_pos[3];     /* CameraDeScene::Position                        */
+    float orient[16];     /* CameraDeScene::Orientation, row-major m[4][4]  */
+    float half_w, half_h; /* Scene.cpp:676-677                              */
+    float inv_w, inv_h;   /* Scene.cpp:678-679                              */
+    float background[3];  /* m_CouleurArrierePlan                           */
+    int32_t width, height;
+    int32_t row_begin, row_end; /* slab [row_begin,row_end) of PixY         */
+    int32_t max_bounces;  /* m_NbRebondsMax (0 = the shipped executable)    */
+    float min_energy;     /* m_EnergieMinRayon (0.01)                       */
+    float scene_ior;      /* m_IndiceRefractionScene (1.0)                  */
+    int32_t flags;        /* RT_FLAG_*                                      */
+} rt_frame;
+
+#define RT_FLAG_STATS 1   /* count rays / tests into rt_stats (small cost)  */
+
+typedef struct rt_stats {
+    uint64_t primary_rays;
+    uint64_t bounce_rays;  /* reflected + refracted rays traced            */
+    uint64_t shadow_rays;  /* rays sent to ObtenirFiltreDeSurface           */
+    uint64_t shadow_tests_skipped; /* shadow tests elided by the exact
+                                      all-lanes-opaque early exit           */
+    float kernel_ms;       /* last render's kernel time (hipEvent)          */
+    int32_t stack_depth;   /* compiled bounce-stack depth that ran          */
+    int32_t reserved;
+} rt_stats;
+
+/* ------------------------------------------------------------ host scene */
+typedef struct rt_scene rt_scene;
+
+int rt_scene_create(rt_scene** out);                          /* CScene::CScene, Scene.cpp:61 */
+int rt_scene_set_resolution(rt_scene*, int32_t w, int32_t h);  /* AjusterResolution, Scene.cpp:162 */
+int rt_scene_set_max_bounces(rt_scene*, int32_t n);            /* AjusterNbRebondsMax, Scene.cpp:180 */
+int rt_scene_set_min_energy(rt_scene*, float e);               /* AjusterEnergieMinimale, Scene.cpp:197 */
+int rt_scene_set_scene_ior(rt_scene*, float ior);              /* AjusterIndiceRefraction, Scene.cpp:214 */
+int rt_scene_load_file(rt_scene*, const char* path);           /* TraiterFichierDeScene, Scene.cpp:231 */
+int rt_scene_prepare(rt_scene*);            /* Initialiser, Scene.cpp:140 (ONCE; not per frame) */
+int rt_scene_get_flat(const rt_scene*, rt_scene_flat* out);    /* views into scene-owned arrays */
+int rt_scene_get_frame(const rt_scene*, rt_frame* out);        /* full-frame rt_frame */
+const char* rt_scene_error(const rt_scene*);
+void rt_scene_destroy(rt_scene*);
+
+/* --------------------------------------------------------------- device */
+typedef struct rt_ctx rt_ctx;
+
+int rt_create(int32_t hip_device, rt_ctx** out);
+int rt_upload_scene(rt_ctx*, const rt_scene_flat*);
+/* Synchronous.  rgba8_out: host or device pointer to
+ * (row_end-row_begin)*width*4 bytes, RGBA8 = GL float->unorm8 of the RGB
+ * (clamp to [0,1], round to nearest, alpha 255). */
+int rt_render(rt_ctx*, const rt_frame*, uint8_t* rgba8_out);
+/* Parity/debug: float RGB exactly as m_InfoPixel (unclamped), 3 floats/px. */
+int rt_render_float(rt_ctx*, const rt_frame*, float* rgb_out);
+/* Asynchronous, device pointers only, on `hip_stream` (hipStream_t; NULL =
+ * the context's own stream).  Either output may be NULL.  No host sync, no
+ * allocation: safe to capture in a hipGraph or to enqueue behind RCCL. */
+int rt_render_async(rt_ctx*, const rt_frame*, uint8_t* rgba8_dev, float* rgb_dev, void* hip_stream);
+int rt_last_stats(rt_ctx*, rt_stats* out);
+const char* rt_last_error(rt_ctx*);
+void rt_destroy(rt_ctx*);
+
+int rt_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RT_AMD_RT_H */

@@ -1,0 +1,747 @@
+// rt_kernels.hip — the hot path on gfx950 (MI355X) and the device half of the
+// C ABI (include/rt.h).
+//
+// What runs here replaces, per pixel, the reference's CPU loop
+// (Scene.cpp:1538-1561) -> ObtenirCouleur (:1705) -> ObtenirCouleurSurIntersection
+// (:1740, plus the commented reflect/refract block :1779-1823 when
+// max_bounces > 0) -> ObtenirFiltreDeSurface (:1842), and the primitive tests
+// CTriangle/CPlan/CQuadrique::Intersection (Triangle.cpp:127, Plan.cpp:128,
+// Quadrique.cpp:160).  It is NOT a translation of shaders/rayTracing.glsl.
+//
+// Execution model:
+//  * one wave64 = one 8x8 pixel tile, lane l -> (l&7, l>>3); a 256-thread
+//    workgroup covers 16x16 pixels (4 tiles);
+//  * the surface list is walked in FILE ORDER by every lane of the wave in
+//    lockstep, so the surface index, its type switch and its 64-byte record are
+//    wave-uniform: records arrive through the scalar data cache (s_load) into
+//    SGPRs and feed the VALU directly — no per-lane gather, no LDS round trip;
+//  * closest hit keeps (t, index) only; the hit normal is rebuilt once for the
+//    winner (bit-identical: same expressions, same inputs);
+//  * shadow rays multiply the transmittance filter in file order and leave the
+//    surface loop as soon as every active lane's filter is exactly +0 (only
+//    when the host proved all filter factors are non-negative and finite, so
+//    the skipped factors could not have changed a single bit);
+//  * bounces (depth > 0) run as an explicit per-lane DFS with a compile-time
+//    sized frame stack instead of recursion, folding each node's colour
+//    bottom-up in the reference's order: ((local + C_refl*Kr) + C_refr*Kt);
+//  * no FMA contraction, IEEE f32 division and sqrt.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/rt.h"
+#include "rt_math.h"
+
+#pragma clang fp contract(off)
+
+namespace rt {
+
+// ------------------------------------------------------------ device layout
+// 64-byte surface record, FILE ORDER (4 x float4):
+//   word 0         : kind (int bits)
+//   triangle       : p0 [1..3]  e1=p1-p0 [4..6]  e2=p2-p0 [7..9]  n [10..12]
+//   plane          : n [1..3]   cst [4]
+//   quadric        : quad [1..3] mix [4..6] lin [7..9] cst [10]
+//   words 13..15   : shadow filter factor  colour * Kt  (Scene.cpp:1857-1858)
+// Edges are the reference's own per-test subtractions (Triangle.cpp:135-136)
+// hoisted to upload time: same operands, same IEEE subtraction, same bits.
+// Material (3 x float4): [r g b Ka] [Kd Ks shin Kr] [Kt ior 0 0]
+// Light    (2 x float4): [x y z I]  [r g b 0]
+struct SceneDev {
+    const float4* __restrict__ geom;
+    const float4* __restrict__ mat;
+    const float4* __restrict__ lights;
+    int n_surf;
+    int n_lights;
+    int opaque_exit;  // filter factors all finite and >= +0
+    int pad;
+};
+
+struct FrameDev {
+    float cam[3];
+    float orient[16];
+    float half_w, half_h, inv_w, inv_h;
+    float bg[3];
+    int width, height, row_begin, row_end;
+    int max_bounces;
+    float min_energy, scene_ior;
+    int flags;
+};
+
+struct StatsDev {
+    unsigned long long primary, bounce, shadow, skipped;
+};
+
+// --------------------------------------------------------- primitive tests
+// Each returns whether the reference's Intersection() would set a surface,
+// and the distance it would report.
+
+// Triangle.cpp:127-172 (Moller-Trumbore).  Early outs become predicates.
+__device__ __forceinline__ bool hit_triangle(const float4 a, const float4 b, const float4 c,
+                                             const Vec3 O, const Vec3 D, float& t)
+{
+    const Vec3 p0 = make3(a.y, a.z, a.w);
+    const Vec3 e1 = make3(b.x, b.y, b.z);
+    const Vec3 e2 = make3(b.w, c.x, c.y);
+    const Vec3 P = cross(D, e2);
+    const float det = dot(e1, P);
+    const float inv = 1.0f / det;
+    const Vec3 S = O - p0;
+    const float u = dot(S, P) * inv;
+    const Vec3 Q = cross(S, e1);
+    const float v = dot(D, Q) * inv;
+    t = dot(e2, Q) * inv;
+    return !(fabsf(det) < kEps) && !(u < 0 || u > 1) && !(v < 0 || u + v > 1);
+}
+
+// Plan.cpp:128-144
+__device__ __forceinline__ bool hit_plane(const float4 a, const float4 b, const Vec3 O, const Vec3 D,
+                                          float& t)
+{
+    const Vec3 n = make3(a.y, a.z, a.w);
+    const float vd = dot(n, D);
+    t = -(dot(n, O) + b.x) / vd;
+    return fabsf(vd) > kEps;
+}
+
+// Quadrique.cpp:171-194 — the three coefficients, expression trees verbatim.
+struct QuadCoef {
+    float A, B, C;
+};
+__device__ __forceinline__ QuadCoef quad_coef(const float4 a, const float4 b, const float4 c,
+                                              const Vec3 o, const Vec3 d)
+{
+    const Vec3 q = make3(a.y, a.z, a.w);
+    const Vec3 m = make3(b.x, b.y, b.z);
+    const Vec3 l = make3(b.w, c.x, c.y);
+    const float cst = c.z;
+    QuadCoef k;
+    k.A = d.x * (q.x * d.x + m.z * d.y + m.y * d.z) + d.y * (q.y * d.y + m.x * d.z) + d.z * (q.z * d.z);
+    k.B = d.x * (q.x * o.x + 0.5f * (m.z * o.y + m.y * o.z + l.x)) +
+          d.y * (q.y * o.y + 0.5f * (m.z * o.x + m.x * o.z + l.y)) +
+          d.z * (q.z * o.z + 0.5f * (m.y * o.x + m.x * o.y + l.z));
+    k.C = o.x * (q.x * o.x + m.z * o.y + m.y * o.z + l.x) + o.y * (q.y * o.y + m.x * o.z + l.y) +
+          o.z * (q.z * o.z + l.z) + cst;
+    return k;
+}
+// Quadrique.cpp:196-248 (root choice: min, else max if min < EPS, accept if !(t<0);
+// degenerate A == 0 branch always reports -0.5*(C/B)).
+__device__ __forceinline__ bool hit_quadric(const float4 a, const float4 b, const float4 c,
+                                            const Vec3 O, const Vec3 D, float& t)
+{
+    const QuadCoef k = quad_coef(a, b, c, O, D);
+    if (k.A != 0.0f) {
+        const float Ka = -k.B / k.A;
+        const float Kb = k.C / k.A;
+        float delta = Ka * Ka - Kb;
+        const bool pos = delta > 0;
+        delta = sqrtf(delta);
+        const float t0 = Ka - delta;
+        const float t1 = Ka + delta;
+        float dist = t0 < t1 ? t0 : t1;
+        if (dist < kEps) dist = t0 > t1 ? t0 : t1;
+        t = dist;
+        return pos && !(dist < 0);
+    }
+    t = -0.5f * (k.C / k.B);
+    return true;
+}
+
+// Quadrique.cpp:214-237 / :243-246 — rebuilt only for the winning quadric.
+__device__ __forceinline__ Vec3 quadric_normal(const float4 a, const float4 b, const float4 c,
+                                               const Vec3 O, const Vec3 D, float t)
+{
+    const QuadCoef k = quad_coef(a, b, c, O, D);
+    const Vec3 q = make3(a.y, a.z, a.w);
+    const Vec3 m = make3(b.x, b.y, b.z);
+    const Vec3 l = make3(b.w, c.x, c.y);
+    if (k.A != 0.0f) {
+        const Vec3 hp = O + t * D;
+        Vec3 n;
+        n.x = 2.0f * q.x * hp.x + m.y * hp.z + m.z * hp.y + l.x;
+        n.y = 2.0f * q.y * hp.y + m.x * hp.z + m.z * hp.x + l.y;
+        n.z = 2.0f * q.z * hp.z + m.x * hp.y + m.y * hp.x + l.z;
+        return normalize(n);
+    }
+    return normalize(l);
+}
+
+__device__ __forceinline__ int kind_of(const float4 a) { return __float_as_int(a.x); }
+
+// Scene.cpp:1705-1715: closest hit in file order; strict '<' keeps the first
+// of equal distances.  Returns the winning index (-1 = miss).
+__device__ __forceinline__ int closest_hit(const SceneDev& S, const Vec3 O, const Vec3 D, float& best_t)
+{
+    float bt = -1.0f;
+    int bi = -1;
+    for (int i = 0; i < S.n_surf; ++i) {
+        const float4* rec = S.geom + 4 * i;
+        const float4 a = rec[0], b = rec[1], c = rec[2];
+        float t;
+        bool ok;
+        const int kind = kind_of(a);
+        if (kind == RT_TRIANGLE) ok = hit_triangle(a, b, c, O, D, t);
+        else if (kind == RT_PLANE) ok = hit_plane(a, b, O, D, t);
+        else ok = hit_quadric(a, b, c, O, D, t);
+        if (ok && t > kEps && (t < bt || bt < 0)) {
+            bt = t;
+            bi = i;
+        }
+    }
+    best_t = bt;
+    return bi;
+}
+
+__device__ __forceinline__ Vec3 hit_normal(const SceneDev& S, int idx, const Vec3 O, const Vec3 D, float t)
+{
+    const float4* rec = S.geom + 4 * idx;
+    const float4 a = rec[0], b = rec[1], c = rec[2], d = rec[3];
+    const int kind = kind_of(a);
+    if (kind == RT_TRIANGLE) return make3(c.z, c.w, d.x);
+    if (kind == RT_PLANE) return make3(a.y, a.z, a.w);
+    return quadric_normal(a, b, c, O, D, t);
+}
+
+struct Mat {
+    Color color;
+    float ka, kd, ks, shin, kr, kt, ior;
+};
+__device__ __forceinline__ Mat load_mat(const SceneDev& S, int idx)
+{
+    const float4 m0 = S.mat[3 * idx], m1 = S.mat[3 * idx + 1], m2 = S.mat[3 * idx + 2];
+    return Mat{{m0.x, m0.y, m0.z}, m0.w, m1.x, m1.y, m1.z, m1.w, m2.x, m2.y};
+}
+
+// Scene.cpp:1842-1861 ObtenirFiltreDeSurface.  L is the UNNORMALISED light
+// vector; it is normalised here exactly like the reference (in place).
+__device__ __forceinline__ Color shadow_filter(const SceneDev& S, const Vec3 P, Vec3& L,
+                                               unsigned& skipped)
+{
+    Color F{1.0f, 1.0f, 1.0f};
+    const float dist = norm(L);
+    L = div_recip(L, dist);
+    bool lit = true;
+    for (int i = 0; i < S.n_surf; ++i) {
+        const float4* rec = S.geom + 4 * i;
+        const float4 a = rec[0], b = rec[1], c = rec[2], d = rec[3];
+        float t;
+        bool ok;
+        const int kind = kind_of(a);
+        if (kind == RT_TRIANGLE) ok = hit_triangle(a, b, c, P, L, t);
+        else if (kind == RT_PLANE) ok = hit_plane(a, b, P, L, t);
+        else ok = hit_quadric(a, b, c, P, L, t);
+        if (ok && t > kEps && t < dist) {
+            F *= Color{d.y, d.z, d.w};
+            lit = (F.r != 0.0f) | (F.g != 0.0f) | (F.b != 0.0f);
+        }
+        if (S.opaque_exit && !__any(lit)) {
+            skipped += (unsigned)(S.n_surf - 1 - i);
+            break;
+        }
+    }
+    return F;
+}
+
+struct Counters {
+    unsigned primary = 0, bounce = 0, shadow = 0, skipped = 0;
+};
+
+// Scene.cpp:1742-1777: ambient + every light (N.L gate on the unnormalised
+// light vector, filter, Lambert "Gouraud" term, Phong term).
+__device__ __forceinline__ Color shade_local(const SceneDev& S, const Mat& m, const Vec3 P, const Vec3 N,
+                                             const Vec3 D, Counters& cnt)
+{
+    Color res = m.color * m.ka;
+    for (int li = 0; li < S.n_lights; ++li) {
+        const float4 l0 = S.lights[2 * li], l1 = S.lights[2 * li + 1];
+        Vec3 L = make3(l0.x, l0.y, l0.z) - P;
+        if (dot(L, N) > 0) {
+            ++cnt.shadow;
+            const Color F = shadow_filter(S, P, L, cnt.skipped);
+            const Color LC = Color{l1.x, l1.y, l1.z} * F;
+            const float g = l0.w * m.kd * dot(N, L);
+            res += (m.color * g) * LC;
+            const Vec3 rf = reflect(L, N);
+            const float ps = dot(rf, D);
+            if (ps > 0) {
+                const float pf = l0.w * m.ks * powf(ps, m.shin);
+                res += LC * pf;
+            }
+        }
+    }
+    return res;
+}
+
+// One pixel's colour.  MAXD = compile-time bounce-stack capacity (0 = no
+// bounces: the reference as shipped).
+struct Frame {
+    Color acc;
+    Vec3 P, N, D;
+    float rior, energy;
+    int surf, stage;
+};
+
+template <int MAXD>
+__device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, Counters& cnt)
+{
+    const Color bg{F.bg[0], F.bg[1], F.bg[2]};
+    if constexpr (MAXD == 0) {
+        float t;
+        const int idx = closest_hit(S, O, D, t);
+        if (idx < 0) return bg;
+        const Vec3 N = hit_normal(S, idx, O, D, t);
+        const Mat m = load_mat(S, idx);
+        const Vec3 P = O + t * D;
+        return shade_local(S, m, P, N, D, cnt);
+    } else {
+        Frame stk[MAXD];
+        int sp = 0;
+        float rior = 1.0f, energy = 1.0f;
+        Color ret{0.f, 0.f, 0.f};
+        bool trace = true;
+        for (;;) {
+            if (trace) {
+                float t;
+                const int idx = closest_hit(S, O, D, t);
+                ret = bg;
+                if (idx >= 0) {
+                    const Vec3 N = hit_normal(S, idx, O, D, t);
+                    const Mat m = load_mat(S, idx);
+                    const Vec3 P = O + t * D;
+                    const Color acc = shade_local(S, m, P, N, D, cnt);
+                    // Scene.cpp:1779-1781 / :1790-1792 gates; bounces == sp
+                    const float er = m.kr * energy;
+                    const float et = m.kt * energy;
+                    const bool can = sp < F.max_bounces && sp < MAXD;
+                    const bool doR = er > F.min_energy && can;
+                    const bool doT = et > F.min_energy && can;
+                    if (doR || doT) {
+                        Frame& fr = stk[sp++];
+                        fr.acc = acc;
+                        fr.P = P;
+                        fr.N = N;
+                        fr.D = D;
+                        fr.rior = rior;
+                        fr.energy = energy;
+                        fr.surf = idx;
+                        ++cnt.bounce;
+                        O = P;
+                        if (doR) {  // Scene.cpp:1782-1788: IOR left at CRayon's default 0
+                            fr.stage = 0;
+                            D = reflect(D, N);
+                            rior = 0.0f;
+                            energy = er;
+                        } else {
+                            fr.stage = 1;
+                            Vec3 n = N;
+                            float ratio;
+                            if (rior == m.ior) {  // Scene.cpp:1797-1803 inside -> out
+                                rior = F.scene_ior;
+                                ratio = m.ior / F.scene_ior;
+                                n = -n;
+                            } else {
+                                rior = m.ior;
+                                ratio = F.scene_ior / m.ior;
+                            }
+                            D = refract(D, n, ratio);
+                            energy = et;
+                        }
+                        continue;
+                    }
+                    ret = acc;
+                }
+                trace = false;
+            }
+            if (sp == 0) return ret;
+            Frame& fr = stk[sp - 1];
+            const Mat m = load_mat(S, fr.surf);
+            if (fr.stage == 0) {
+                fr.acc += ret * m.kr;  // Scene.cpp:1787
+                const float et = m.kt * fr.energy;
+                if (et > F.min_energy && (sp - 1) < F.max_bounces) {
+                    fr.stage = 1;
+                    ++cnt.bounce;
+                    Vec3 n = fr.N;
+                    float ratio;
+                    if (fr.rior == m.ior) {
+                        rior = F.scene_ior;
+                        ratio = m.ior / F.scene_ior;
+                        n = -n;
+                    } else {
+                        rior = m.ior;
+                        ratio = F.scene_ior / m.ior;
+                    }
+                    O = fr.P;
+                    D = refract(fr.D, n, ratio);
+                    energy = et;
+                    trace = true;
+                    continue;
+                }
+                ret = fr.acc;
+                --sp;
+            } else {
+                fr.acc += ret * m.kt;  // Scene.cpp:1822
+                ret = fr.acc;
+                --sp;
+            }
+        }
+    }
+}
+
+template <int MAXD>
+__global__ __launch_bounds__(256) void rt_trace_kernel(const SceneDev S, const FrameDev F, unsigned* __restrict__ rgba,
+                                                       float* __restrict__ rgbf, StatsDev* __restrict__ stats)
+{
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int px = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
+    const int ly = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+    const int py = F.row_begin + ly;
+    const bool valid = px < F.width && py < F.row_end;
+
+    Counters cnt;
+    Color c{0.f, 0.f, 0.f};
+    if (valid) {
+        // Scene.cpp:1543-1552: (float)(2*PixX) * InvW - 1, then * HalfW
+        const Vec3 d0 = make3((2 * px * F.inv_w - 1) * F.half_w, (2 * py * F.inv_h - 1) * F.half_h, -1.0f);
+        Mat4 M;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) M.m[i >> 2][i & 3] = F.orient[i];
+        const Vec3 D = normalize(d0 * M);
+        const Vec3 O = make3(F.cam[0], F.cam[1], F.cam[2]);
+        cnt.primary = 1;
+        c = radiance<MAXD>(S, F, O, D, cnt);
+        const size_t o = (size_t)ly * F.width + px;
+        if (rgbf) {
+            rgbf[3 * o] = c.r;
+            rgbf[3 * o + 1] = c.g;
+            rgbf[3 * o + 2] = c.b;
+        }
+        if (rgba) rgba[o] = unorm8(c.r) | (unorm8(c.g) << 8) | (unorm8(c.b) << 16) | 0xFF000000u;
+    }
+    if (F.flags & RT_FLAG_STATS) {
+        atomicAdd(&stats->primary, (unsigned long long)cnt.primary);
+        atomicAdd(&stats->bounce, (unsigned long long)cnt.bounce);
+        atomicAdd(&stats->shadow, (unsigned long long)cnt.shadow);
+        atomicAdd(&stats->skipped, (unsigned long long)cnt.skipped * 1ull);
+    }
+}
+
+// Compiled bounce-stack capacities.  The host picks the smallest one that
+// covers the bounce depth the scene can actually reach.
+#define RT_STACK_DEPTHS(X) X(0) X(1) X(2) X(3) X(4) X(5) X(8) X(12) X(16) X(20) X(32)
+
+}  // namespace rt
+
+// ===================================================================== host
+using namespace rt;
+
+struct rt_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    float4* d_geom = nullptr;
+    float4* d_mat = nullptr;
+    float4* d_lights = nullptr;
+    StatsDev* d_stats = nullptr;
+    void* d_scratch = nullptr;  // staging for host outputs
+    size_t scratch_bytes = 0;
+    int n_surf = 0, n_lights = 0;
+    int opaque_exit = 0;
+    float k_max = 0.0f;         // max(Kr, Kt) over surfaces (NaN ignored)
+    bool uploaded = false;
+    rt_stats last{};
+    std::string err;
+};
+
+#define RT_EXPORT extern "C" __attribute__((visibility("default")))
+
+static int hip_fail(rt_ctx* c, hipError_t e, const char* what)
+{
+    c->err = std::string(what) + ": " + hipGetErrorString(e);
+    return RT_E_HIP;
+}
+#define HIP_TRY(c, call)                                   \
+    do {                                                   \
+        hipError_t e_ = (call);                            \
+        if (e_ != hipSuccess) return hip_fail(c, e_, #call); \
+    } while (0)
+
+RT_EXPORT const char* rt_last_error(rt_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+RT_EXPORT int rt_create(int32_t dev, rt_ctx** out)
+{
+    if (!out) return RT_E_ARG;
+    *out = nullptr;
+    rt_ctx* c = new rt_ctx();
+    c->device = dev;
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev <= 0 || dev < 0 || dev >= ndev) {
+        *out = c;
+        c->err = "no usable HIP device";
+        return RT_E_HIP;
+    }
+    *out = c;
+    HIP_TRY(c, hipSetDevice(dev));
+    HIP_TRY(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIP_TRY(c, hipEventCreate(&c->ev0));
+    HIP_TRY(c, hipEventCreate(&c->ev1));
+    HIP_TRY(c, hipMalloc(&c->d_stats, sizeof(StatsDev)));
+    return RT_OK;
+}
+
+RT_EXPORT void rt_destroy(rt_ctx* c)
+{
+    if (!c) return;
+    if (c->stream) {
+        (void)hipSetDevice(c->device);
+        (void)hipStreamSynchronize(c->stream);
+    }
+    hipFree(c->d_geom);
+    hipFree(c->d_mat);
+    hipFree(c->d_lights);
+    hipFree(c->d_stats);
+    hipFree(c->d_scratch);
+    if (c->ev0) hipEventDestroy(c->ev0);
+    if (c->ev1) hipEventDestroy(c->ev1);
+    if (c->stream) hipStreamDestroy(c->stream);
+    delete c;
+}
+
+static bool nonneg_finite(float v) { return std::isfinite(v) && !std::signbit(v); }
+
+RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
+{
+    if (!c || !s || s->n_surfaces < 0 || s->n_lights < 0) return RT_E_ARG;
+    if (s->n_surfaces > 0 && (!s->type || !s->geom || !s->material)) return RT_E_ARG;
+    if (s->n_lights > 0 && !s->lights) return RT_E_ARG;
+    if (!c->stream) return RT_E_STATE;
+    HIP_TRY(c, hipSetDevice(c->device));
+    const int n = s->n_surfaces, nl = s->n_lights;
+    std::vector<float> geom((size_t)std::max(n, 1) * 16, 0.0f), mat((size_t)std::max(n, 1) * 12, 0.0f),
+        lig((size_t)std::max(nl, 1) * 8, 0.0f);
+    bool opaque = true;
+    float kmax = 0.0f;
+    for (int i = 0; i < n; ++i) {
+        const float* g = s->geom + 12 * (size_t)i;
+        const float* m = s->material + 10 * (size_t)i;
+        float* o = &geom[16 * (size_t)i];
+        int kind = s->type[i];
+        if (kind < RT_TRIANGLE || kind > RT_QUADRIC) {
+            c->err = "unknown surface type";
+            return RT_E_ARG;
+        }
+        std::memcpy(&o[0], &kind, sizeof(int));
+        if (kind == RT_TRIANGLE) {
+            const Vec3 p0 = make3(g[0], g[1], g[2]), p1 = make3(g[3], g[4], g[5]), p2 = make3(g[6], g[7], g[8]);
+            const Vec3 e1 = p1 - p0, e2 = p2 - p0;  // Triangle.cpp:135-136
+            o[1] = p0.x; o[2] = p0.y; o[3] = p0.z;
+            o[4] = e1.x; o[5] = e1.y; o[6] = e1.z;
+            o[7] = e2.x; o[8] = e2.y; o[9] = e2.z;
+            o[10] = g[9]; o[11] = g[10]; o[12] = g[11];
+        } else if (kind == RT_PLANE) {
+            o[1] = g[0]; o[2] = g[1]; o[3] = g[2]; o[4] = g[3];
+        } else {
+            o[1] = g[0]; o[2] = g[1]; o[3] = g[2];  // quad
+            o[4] = g[6]; o[5] = g[7]; o[6] = g[8];  // mix
+            o[7] = g[3]; o[8] = g[4]; o[9] = g[5];  // lin
+            o[10] = g[9];
+        }
+        const Color fc = Color{m[0], m[1], m[2]} * m[8];  // colour * Kt
+        o[13] = fc.r; o[14] = fc.g; o[15] = fc.b;
+        opaque = opaque && nonneg_finite(fc.r) && nonneg_finite(fc.g) && nonneg_finite(fc.b);
+        float* q = &mat[12 * (size_t)i];
+        for (int k = 0; k < 10; ++k) q[k] = m[k];
+        if (m[7] > kmax) kmax = m[7];
+        if (m[8] > kmax) kmax = m[8];
+    }
+    for (int j = 0; j < nl; ++j) {
+        const float* l = s->lights + 7 * (size_t)j;
+        float* o = &lig[8 * (size_t)j];
+        o[0] = l[0]; o[1] = l[1]; o[2] = l[2]; o[3] = l[6];
+        o[4] = l[3]; o[5] = l[4]; o[6] = l[5]; o[7] = 0.0f;
+    }
+    hipFree(c->d_geom);
+    hipFree(c->d_mat);
+    hipFree(c->d_lights);
+    c->d_geom = c->d_mat = c->d_lights = nullptr;
+    HIP_TRY(c, hipMalloc(&c->d_geom, geom.size() * sizeof(float)));
+    HIP_TRY(c, hipMalloc(&c->d_mat, mat.size() * sizeof(float)));
+    HIP_TRY(c, hipMalloc(&c->d_lights, lig.size() * sizeof(float)));
+    HIP_TRY(c, hipMemcpy(c->d_geom, geom.data(), geom.size() * sizeof(float), hipMemcpyHostToDevice));
+    HIP_TRY(c, hipMemcpy(c->d_mat, mat.data(), mat.size() * sizeof(float), hipMemcpyHostToDevice));
+    HIP_TRY(c, hipMemcpy(c->d_lights, lig.data(), lig.size() * sizeof(float), hipMemcpyHostToDevice));
+    c->n_surf = n;
+    c->n_lights = nl;
+    c->opaque_exit = opaque ? 1 : 0;
+    c->k_max = kmax;
+    c->uploaded = true;
+    return RT_OK;
+}
+
+// Deepest bounce level any pixel can reach: a child exists only while
+// K * energy > min_energy (Scene.cpp:1780,1791); energies are products of
+// factors <= k_max and float rounding is monotone, so iterating with k_max
+// bounds every path.
+static int reachable_depth(const rt_ctx* c, const rt_frame* f)
+{
+    // With a negative threshold the energy argument below does not hold.
+    if (!(f->min_energy >= 0.0f)) return f->max_bounces;
+    int levels = 0;
+    float e = 1.0f;
+    while (levels < f->max_bounces) {
+        const float child = c->k_max * e;
+        if (!(child > f->min_energy)) break;
+        e = child;
+        ++levels;
+        if (levels > 4096) break;
+    }
+    return levels;
+}
+
+typedef void (*kernel_fn)(const SceneDev, const FrameDev, unsigned*, float*, StatsDev*);
+
+static kernel_fn pick_kernel(int depth, int& cap)
+{
+#define RT_PICK(N)                                 \
+    if (depth <= N) {                              \
+        cap = N;                                   \
+        return (kernel_fn)&rt_trace_kernel<N>;     \
+    }
+    RT_STACK_DEPTHS(RT_PICK)
+#undef RT_PICK
+    cap = -1;
+    return nullptr;
+}
+
+static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_dev, hipStream_t st, bool timed)
+{
+    if (!c || !f) return RT_E_ARG;
+    if (!c->uploaded) {
+        c->err = "render before rt_upload_scene";
+        return RT_E_STATE;
+    }
+    if (f->width <= 0 || f->height <= 0 || f->row_begin < 0 || f->row_end > f->height ||
+        f->row_begin > f->row_end || f->max_bounces < 0) {
+        c->err = "bad rt_frame geometry";
+        return RT_E_ARG;
+    }
+    const int depth = reachable_depth(c, f);
+    int cap = 0;
+    kernel_fn k = pick_kernel(depth, cap);
+    if (!k) {
+        c->err = "reachable bounce depth " + std::to_string(depth) + " exceeds the compiled stack (32)";
+        return RT_E_UNSUPPORTED;
+    }
+    SceneDev S{c->d_geom, c->d_mat, c->d_lights, c->n_surf, c->n_lights, c->opaque_exit, 0};
+    FrameDev F;
+    std::memcpy(F.cam, f->cam_pos, sizeof F.cam);
+    std::memcpy(F.orient, f->orient, sizeof F.orient);
+    F.half_w = f->half_w;
+    F.half_h = f->half_h;
+    F.inv_w = f->inv_w;
+    F.inv_h = f->inv_h;
+    std::memcpy(F.bg, f->background, sizeof F.bg);
+    F.width = f->width;
+    F.height = f->height;
+    F.row_begin = f->row_begin;
+    F.row_end = f->row_end;
+    F.max_bounces = f->max_bounces;
+    F.min_energy = f->min_energy;
+    F.scene_ior = f->scene_ior;
+    F.flags = f->flags;
+    const int rows = f->row_end - f->row_begin;
+    c->last = rt_stats{};
+    c->last.stack_depth = cap;
+    if (rows == 0) return RT_OK;
+    if (f->flags & RT_FLAG_STATS) HIP_TRY(c, hipMemsetAsync(c->d_stats, 0, sizeof(StatsDev), st));
+    dim3 grid((f->width + 15) / 16, (rows + 15) / 16);
+    if (timed) HIP_TRY(c, hipEventRecord(c->ev0, st));
+    StatsDev* stats = c->d_stats;
+    void* args[] = {&S, &F, &rgba_dev, &rgb_dev, &stats};
+    HIP_TRY(c, hipLaunchKernel((const void*)k, grid, dim3(256), args, 0, st));
+    if (timed) HIP_TRY(c, hipEventRecord(c->ev1, st));
+    return RT_OK;
+}
+
+static int finish_sync(rt_ctx* c, const rt_frame* f, hipStream_t st, bool timed)
+{
+    HIP_TRY(c, hipStreamSynchronize(st));
+    if (timed) {
+        float ms = 0.f;
+        HIP_TRY(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+        c->last.kernel_ms = ms;
+    }
+    if (f->flags & RT_FLAG_STATS) {
+        StatsDev h{};
+        HIP_TRY(c, hipMemcpy(&h, c->d_stats, sizeof h, hipMemcpyDeviceToHost));
+        c->last.primary_rays = h.primary;
+        c->last.bounce_rays = h.bounce;
+        c->last.shadow_rays = h.shadow;
+        c->last.shadow_tests_skipped = h.skipped;
+    }
+    return RT_OK;
+}
+
+static bool is_device_ptr(const void* p)
+{
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
+}
+
+static int ensure_scratch(rt_ctx* c, size_t bytes)
+{
+    if (c->scratch_bytes >= bytes) return RT_OK;
+    hipFree(c->d_scratch);
+    c->d_scratch = nullptr;
+    c->scratch_bytes = 0;
+    HIP_TRY(c, hipMalloc(&c->d_scratch, bytes));
+    c->scratch_bytes = bytes;
+    return RT_OK;
+}
+
+static int render_sync(rt_ctx* c, const rt_frame* f, void* out, bool as_float)
+{
+    if (!c || !f || !out) return RT_E_ARG;
+    HIP_TRY(c, hipSetDevice(c->device));
+    const size_t px = (size_t)f->width * (size_t)std::max(0, f->row_end - f->row_begin);
+    const size_t bytes = px * (as_float ? 12 : 4);
+    const bool dev = is_device_ptr(out);
+    void* target = out;
+    if (!dev) {
+        int rc = ensure_scratch(c, std::max<size_t>(bytes, 16));
+        if (rc) return rc;
+        target = c->d_scratch;
+    }
+    int rc = launch(c, f, as_float ? nullptr : (unsigned*)target, as_float ? (float*)target : nullptr, c->stream, true);
+    if (rc) return rc;
+    if (!dev && bytes) HIP_TRY(c, hipMemcpyAsync(out, target, bytes, hipMemcpyDeviceToHost, c->stream));
+    return finish_sync(c, f, c->stream, true);
+}
+
+RT_EXPORT int rt_render(rt_ctx* c, const rt_frame* f, uint8_t* rgba8_out) { return render_sync(c, f, rgba8_out, false); }
+
+RT_EXPORT int rt_render_float(rt_ctx* c, const rt_frame* f, float* rgb_out) { return render_sync(c, f, rgb_out, true); }
+
+RT_EXPORT int rt_render_async(rt_ctx* c, const rt_frame* f, uint8_t* rgba8_dev, float* rgb_dev, void* stream)
+{
+    if (!c || !f) return RT_E_ARG;
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    return launch(c, f, (unsigned*)rgba8_dev, rgb_dev, st, false);
+}
+
+RT_EXPORT int rt_last_stats(rt_ctx* c, rt_stats* out)
+{
+    if (!c || !out) return RT_E_ARG;
+    *out = c->last;
+    return RT_OK;
+}

@@ -1,0 +1,275 @@
+"""rt_amd — Python host binding of librt_amd.so (the MI355X ray tracer).
+
+The product is the C ABI in ``include/rt.h``; this module is a thin ctypes
+binding over it, shaped like the reference's ``CScene`` (Scene.h:41-70) so a
+caller of the reference finds the same verbs:
+
+    scene = CScene()
+    scene.AjusterResolution(1920, 1080)        # Scene.cpp:162
+    scene.AjusterNbRebondsMax(3)               # Scene.cpp:180
+    scene.TraiterFichierDeScene("scene2.dat")  # Scene.cpp:231
+    img = scene.LancerRayons()                 # Scene.cpp:672 -> (H, W, 4) uint8, row 0 = bottom
+
+There is no CPU fallback: if ``librt_amd.so`` is missing or no HIP device is
+usable, the render calls raise.  Host-only calls (parsing, Pretraitement,
+flattening) work without a GPU.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import numpy as np
+
+__all__ = [
+    "RtError", "SceneFlat", "Frame", "Stats", "Scene", "Context", "CScene", "lib",
+    "LIB_PATH", "TRIANGLE", "PLANE", "QUADRIC", "FLAG_STATS",
+]
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("RT_AMD_LIB", os.path.join(os.path.dirname(_HERE), "lib", "librt_amd.so"))
+
+TRIANGLE, PLANE, QUADRIC = 0, 1, 2
+FLAG_STATS = 1
+_ERRORS = {-1: "RT_E_ARG", -2: "RT_E_IO", -3: "RT_E_PARSE", -4: "RT_E_STATE", -5: "RT_E_HIP",
+           -6: "RT_E_UNSUPPORTED"}
+
+
+class RtError(RuntimeError):
+    def __init__(self, where: str, code: int, msg: str = ""):
+        super().__init__(f"{where} failed: {_ERRORS.get(code, code)} {msg}".rstrip())
+        self.code = code
+
+
+class SceneFlat(ctypes.Structure):
+    _fields_ = [("n_surfaces", ctypes.c_int32), ("n_lights", ctypes.c_int32),
+                ("type", ctypes.POINTER(ctypes.c_int32)), ("geom", ctypes.POINTER(ctypes.c_float)),
+                ("material", ctypes.POINTER(ctypes.c_float)), ("lights", ctypes.POINTER(ctypes.c_float))]
+
+
+class Frame(ctypes.Structure):
+    _fields_ = [("cam_pos", ctypes.c_float * 3), ("orient", ctypes.c_float * 16),
+                ("half_w", ctypes.c_float), ("half_h", ctypes.c_float),
+                ("inv_w", ctypes.c_float), ("inv_h", ctypes.c_float),
+                ("background", ctypes.c_float * 3),
+                ("width", ctypes.c_int32), ("height", ctypes.c_int32),
+                ("row_begin", ctypes.c_int32), ("row_end", ctypes.c_int32),
+                ("max_bounces", ctypes.c_int32), ("min_energy", ctypes.c_float),
+                ("scene_ior", ctypes.c_float), ("flags", ctypes.c_int32)]
+
+    def copy(self) -> "Frame":
+        f = Frame()
+        ctypes.pointer(f)[0] = self
+        return f
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("primary_rays", ctypes.c_uint64), ("bounce_rays", ctypes.c_uint64),
+                ("shadow_rays", ctypes.c_uint64), ("shadow_tests_skipped", ctypes.c_uint64),
+                ("kernel_ms", ctypes.c_float), ("stack_depth", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
+
+
+_lib: Optional[ctypes.CDLL] = None
+
+# Every symbol include/rt.h declares, with its ctypes signature.
+_VP = ctypes.c_void_p
+SIGNATURES = {
+    "rt_abi_version": (ctypes.c_int, []),
+    "rt_scene_create": (ctypes.c_int, [ctypes.POINTER(_VP)]),
+    "rt_scene_set_resolution": (ctypes.c_int, [_VP, ctypes.c_int32, ctypes.c_int32]),
+    "rt_scene_set_max_bounces": (ctypes.c_int, [_VP, ctypes.c_int32]),
+    "rt_scene_set_min_energy": (ctypes.c_int, [_VP, ctypes.c_float]),
+    "rt_scene_set_scene_ior": (ctypes.c_int, [_VP, ctypes.c_float]),
+    "rt_scene_load_file": (ctypes.c_int, [_VP, ctypes.c_char_p]),
+    "rt_scene_prepare": (ctypes.c_int, [_VP]),
+    "rt_scene_get_flat": (ctypes.c_int, [_VP, ctypes.POINTER(SceneFlat)]),
+    "rt_scene_get_frame": (ctypes.c_int, [_VP, ctypes.POINTER(Frame)]),
+    "rt_scene_error": (ctypes.c_char_p, [_VP]),
+    "rt_scene_destroy": (None, [_VP]),
+    "rt_create": (ctypes.c_int, [ctypes.c_int32, ctypes.POINTER(_VP)]),
+    "rt_upload_scene": (ctypes.c_int, [_VP, ctypes.POINTER(SceneFlat)]),
+    "rt_render": (ctypes.c_int, [_VP, ctypes.POINTER(Frame), _VP]),
+    "rt_render_float": (ctypes.c_int, [_VP, ctypes.POINTER(Frame), _VP]),
+    "rt_render_async": (ctypes.c_int, [_VP, ctypes.POINTER(Frame), _VP, _VP, _VP]),
+    "rt_last_stats": (ctypes.c_int, [_VP, ctypes.POINTER(Stats)]),
+    "rt_last_error": (ctypes.c_char_p, [_VP]),
+    "rt_destroy": (None, [_VP]),
+}
+
+
+def lib() -> ctypes.CDLL:
+    """Load librt_amd.so once; raise (never fall back) if it is absent."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RtError("load", -4, f"{LIB_PATH} not built (run __graft_entry__.build())")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _check(where: str, rc: int, msg_fn=None):
+    if rc != 0:
+        raise RtError(where, rc, msg_fn() if msg_fn else "")
+
+
+class Scene:
+    """Host scene: CScene's parser + Initialiser (camera, Pretraitement)."""
+
+    def __init__(self, path: str, width: int, height: int, max_bounces: int = 0,
+                 min_energy: float = 0.01, scene_ior: float = 1.0):
+        L = lib()
+        self._h = _VP()
+        _check("rt_scene_create", L.rt_scene_create(ctypes.byref(self._h)))
+        err = lambda: (L.rt_scene_error(self._h) or b"").decode()
+        _check("rt_scene_set_resolution", L.rt_scene_set_resolution(self._h, width, height), err)
+        _check("rt_scene_set_max_bounces", L.rt_scene_set_max_bounces(self._h, max_bounces), err)
+        L.rt_scene_set_min_energy(self._h, min_energy)
+        L.rt_scene_set_scene_ior(self._h, scene_ior)
+        _check("rt_scene_load_file", L.rt_scene_load_file(self._h, os.fsencode(path)), err)
+        _check("rt_scene_prepare", L.rt_scene_prepare(self._h), err)
+        self.flat = SceneFlat()
+        _check("rt_scene_get_flat", L.rt_scene_get_flat(self._h, ctypes.byref(self.flat)))
+        self.frame = Frame()
+        _check("rt_scene_get_frame", L.rt_scene_get_frame(self._h, ctypes.byref(self.frame)))
+        self.width, self.height = width, height
+
+    @property
+    def n_surfaces(self) -> int:
+        return self.flat.n_surfaces
+
+    def arrays(self):
+        """(type[n], geom[n,12], material[n,10], lights[L,7]) as numpy copies."""
+        n, nl = self.flat.n_surfaces, self.flat.n_lights
+        t = np.ctypeslib.as_array(self.flat.type, (max(n, 1),))[:n].copy() if n else np.zeros(0, np.int32)
+        g = np.ctypeslib.as_array(self.flat.geom, (max(n, 1) * 12,))[: n * 12].reshape(n, 12).copy() if n else np.zeros((0, 12), np.float32)
+        m = np.ctypeslib.as_array(self.flat.material, (max(n, 1) * 10,))[: n * 10].reshape(n, 10).copy() if n else np.zeros((0, 10), np.float32)
+        l = np.ctypeslib.as_array(self.flat.lights, (max(nl, 1) * 7,))[: nl * 7].reshape(nl, 7).copy() if nl else np.zeros((0, 7), np.float32)
+        return t, g, m, l
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().rt_scene_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Context:
+    """One HIP device: uploaded scene + render entry points."""
+
+    def __init__(self, device: int = 0):
+        L = lib()
+        self._h = _VP()
+        rc = L.rt_create(device, ctypes.byref(self._h))
+        if rc != 0:
+            msg = (L.rt_last_error(self._h) or b"").decode() if self._h else ""
+            if self._h:
+                L.rt_destroy(self._h)
+                self._h = None
+            raise RtError("rt_create", rc, msg)
+
+    def _err(self) -> str:
+        return (lib().rt_last_error(self._h) or b"").decode()
+
+    def upload(self, scene: Scene):
+        _check("rt_upload_scene", lib().rt_upload_scene(self._h, ctypes.byref(scene.flat)), self._err)
+
+    def render(self, frame: Frame) -> np.ndarray:
+        """RGBA8 (rows, W, 4), row 0 = frame.row_begin (bottom-up)."""
+        rows = frame.row_end - frame.row_begin
+        out = np.zeros((rows, frame.width, 4), np.uint8)
+        _check("rt_render", lib().rt_render(self._h, ctypes.byref(frame), out.ctypes.data), self._err)
+        return out
+
+    def render_float(self, frame: Frame) -> np.ndarray:
+        rows = frame.row_end - frame.row_begin
+        out = np.zeros((rows, frame.width, 3), np.float32)
+        _check("rt_render_float", lib().rt_render_float(self._h, ctypes.byref(frame), out.ctypes.data), self._err)
+        return out
+
+    def render_async(self, frame: Frame, rgba_dev_ptr: int = 0, rgb_dev_ptr: int = 0, stream: int = 0):
+        _check("rt_render_async", lib().rt_render_async(self._h, ctypes.byref(frame), rgba_dev_ptr or None,
+                                                        rgb_dev_ptr or None, stream or None), self._err)
+
+    def stats(self) -> Stats:
+        s = Stats()
+        _check("rt_last_stats", lib().rt_last_stats(self._h, ctypes.byref(s)))
+        return s
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().rt_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class CScene:
+    """The reference's CScene verbs over the HIP backend (Scene.h:41-70)."""
+
+    def __init__(self, device: int = 0):
+        self._w, self._h = 512, 256          # Var.cpp:4-5
+        self._max_bounces = 20               # Scene.cpp:68
+        self._min_energy = 0.01              # Scene.cpp:69
+        self._scene_ior = 1.0                # Scene.cpp:70
+        self._path: Optional[str] = None
+        self._device = device
+        self._scene: Optional[Scene] = None
+        self._ctx: Optional[Context] = None
+
+    def AjusterResolution(self, w: int, h: int):
+        self._w, self._h = int(w), int(h)
+        self._scene = None
+
+    def AjusterNbRebondsMax(self, n: int):
+        self._max_bounces = int(n)
+
+    def AjusterEnergieMinimale(self, e: float):
+        self._min_energy = float(e)
+
+    def AjusterIndiceRefraction(self, ior: float):
+        self._scene_ior = float(ior)
+
+    def TraiterFichierDeScene(self, path: str):
+        self._path = path
+        self._scene = None
+
+    def _prepared(self) -> Scene:
+        if self._path is None:
+            raise RtError("LancerRayons", -4, "no scene file (TraiterFichierDeScene)")
+        if self._scene is None:
+            self._scene = Scene(self._path, self._w, self._h, self._max_bounces, self._min_energy, self._scene_ior)
+            if self._ctx is None:
+                self._ctx = Context(self._device)
+            self._ctx.upload(self._scene)
+        return self._scene
+
+    def _frame(self) -> Frame:
+        f = self._prepared().frame.copy()
+        f.max_bounces, f.min_energy, f.scene_ior = self._max_bounces, self._min_energy, self._scene_ior
+        return f
+
+    def LancerRayons(self) -> np.ndarray:
+        """Render the frame; returns RGBA8 (H, W, 4), row 0 = bottom."""
+        f = self._frame()
+        return self._ctx.render(f)
+
+    def LancerRayonsFloat(self) -> np.ndarray:
+        """m_InfoPixel equivalent: float32 (H, W, 3), unclamped."""
+        f = self._frame()
+        return self._ctx.render_float(f)

@@ -1,0 +1,146 @@
+"""Shared test setup.
+
+Markers: tests that need an MI355X are marked ``@pytest.mark.gpu``; everything
+else runs on CPU.  The oracle (oracle/liboracle.so) and the golden fixtures
+(tests/golden/) are the checkers; the product is librt_amd.so, reached only
+through its C ABI (rt_amd is a ctypes binding of include/rt.h).
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "ray-tracing-gpu_amd")
+GOLDEN = os.path.join(REPO, "tests", "golden")
+SCENES = os.path.join(GOLDEN, "scenes")
+if PKG not in sys.path:
+    sys.path.insert(0, PKG)
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device)")
+
+
+def _ensure_built():
+    lib = os.path.join(PKG, "lib", "librt_amd.so")
+    orc = os.path.join(REPO, "oracle", "liboracle.so")
+    if not os.path.exists(lib):
+        subprocess.run(["make", "-s", "-C", PKG], check=True)
+    if not os.path.exists(orc):
+        subprocess.run(["make", "-s", "-C", os.path.join(REPO, "oracle")], check=True)
+
+
+_ensure_built()
+
+VP = ctypes.c_void_p
+
+
+class Oracle:
+    """ctypes view of oracle/liboracle.so (test infrastructure only)."""
+
+    def __init__(self):
+        L = ctypes.CDLL(os.path.join(REPO, "oracle", "liboracle.so"))
+        L.oracle_load.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(VP)]
+        L.oracle_render_window.argtypes = [VP, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, VP, ctypes.c_int]
+        L.oracle_counts.argtypes = [VP, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
+        L.oracle_dump.argtypes = [VP, VP, VP, VP]
+        L.oracle_free.argtypes = [VP]
+        L.oracle_error.argtypes = [VP]
+        L.oracle_error.restype = ctypes.c_char_p
+        L.oracle_intersect.argtypes = [ctypes.c_int, VP, VP, VP, VP, VP]
+        L.oracle_set_params.argtypes = [VP, ctypes.c_int, ctypes.c_float, ctypes.c_float]
+        self.L = L
+
+    def load(self, path, w, h, depth):
+        p = VP()
+        rc = self.L.oracle_load(os.fsencode(path), w, h, depth, ctypes.byref(p))
+        return rc, p
+
+    def render(self, path, w, h, depth, window=None, threads=4):
+        rc, p = self.load(path, w, h, depth)
+        assert rc == 0, (path, rc, self.L.oracle_error(p))
+        r0, r1, c0, c1 = window or (0, h, 0, w)
+        out = np.zeros((r1 - r0, c1 - c0, 3), np.float32)
+        self.L.oracle_render_window(p, r0, r1, c0, c1, out.ctypes.data, threads)
+        self.L.oracle_free(p)
+        return out
+
+    def dump(self, path, w, h, depth=0):
+        rc, p = self.load(path, w, h, depth)
+        assert rc == 0, (path, rc)
+        ns, nl = ctypes.c_int(), ctypes.c_int()
+        self.L.oracle_counts(p, ctypes.byref(ns), ctypes.byref(nl))
+        s = np.zeros((ns.value, 24), np.float32)
+        c = np.zeros(27, np.float32)
+        l = np.zeros((max(nl.value, 1), 7), np.float32)
+        self.L.oracle_dump(p, s.ctypes.data, c.ctypes.data, l.ctypes.data)
+        self.L.oracle_free(p)
+        return s, c, l[: nl.value]
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    return Oracle()
+
+
+@pytest.fixture(scope="session")
+def golden_images():
+    return np.load(os.path.join(GOLDEN, "images.npz"))
+
+
+@pytest.fixture(scope="session")
+def golden_prepared():
+    return np.load(os.path.join(GOLDEN, "prepared.npz"))
+
+
+@pytest.fixture(scope="session")
+def golden_kat():
+    return np.load(os.path.join(GOLDEN, "kat.npz"))
+
+
+@pytest.fixture(scope="session")
+def digests():
+    with open(os.path.join(GOLDEN, "digests.json")) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="session")
+def heightfield_path(tmp_path_factory):
+    from rt_amd import synth
+
+    return synth.write_heightfield(str(tmp_path_factory.mktemp("hf") / "heightfield.dat"))
+
+
+def scene(i: int) -> str:
+    return os.path.join(SCENES, f"scene{i}.dat")
+
+
+def rgba8(rgb: np.ndarray) -> np.ndarray:
+    """GL float -> GL_RGBA8: clamp to [0,1] (NaN -> 0), x255, +0.5, floor; alpha 255."""
+    c = np.where(rgb > 0, np.where(rgb < 1, rgb, np.float32(1)), np.float32(0)).astype(np.float32)
+    q = np.floor(c * np.float32(255) + np.float32(0.5)).astype(np.uint8)
+    return np.concatenate([q, np.full(q.shape[:-1] + (1,), 255, np.uint8)], -1)
+
+
+def bits_equal(a: np.ndarray, b: np.ndarray) -> bool:
+    return a.shape == b.shape and np.array_equal(np.ascontiguousarray(a).view(np.uint32),
+                                                 np.ascontiguousarray(b).view(np.uint32))
+
+
+def ulp_diff(a: np.ndarray, b: np.ndarray) -> int:
+    """Max distance in float32 ULPs (sign-magnitude ordered)."""
+    def key(x):
+        i = np.ascontiguousarray(x, np.float32).view(np.int32).astype(np.int64)
+        return np.where(i < 0, -(i & 0x7FFFFFFF), i)
+    if a.size == 0:
+        return 0
+    return int(np.abs(key(a) - key(b)).max())

@@ -1,0 +1,94 @@
+"""The C ABI boundary: librt_amd.so loads and exports every symbol that
+include/rt.h declares, struct layouts agree with the header, and argument
+errors come back as codes (never exits).  No compute calls: CPU only."""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+import rt_amd
+from conftest import REPO
+
+HEADER = os.path.join(REPO, "include", "rt.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(rt_[a-z_0-9]+)\s*\(", text)))
+
+
+def test_header_symbols_exported():
+    names = declared_functions()
+    assert len(names) >= 20
+    L = rt_amd.lib()
+    for n in names:
+        assert hasattr(L, n), n
+    # the ctypes binding covers exactly the header
+    assert set(names) == set(rt_amd.SIGNATURES)
+    out = subprocess.run(["nm", "-D", "--defined-only", rt_amd.LIB_PATH], capture_output=True, text=True).stdout
+    for n in names:
+        assert re.search(rf"\bT {n}\b", out), n
+
+
+def test_abi_version():
+    assert rt_amd.lib().rt_abi_version() == 1
+
+
+def test_struct_layouts_match_header():
+    src = r"""
+#include <stdio.h>
+#include <stddef.h>
+#include "rt.h"
+int main(void){
+  printf("%zu %zu %zu %zu %zu %zu\n", sizeof(rt_scene_flat), sizeof(rt_frame), sizeof(rt_stats),
+         offsetof(rt_frame, width), offsetof(rt_frame, flags), offsetof(rt_stats, kernel_ms));
+  return 0; }
+"""
+    import tempfile
+
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "l.c")
+        open(c, "w").write(src)
+        exe = os.path.join(d, "l")
+        subprocess.run(["gcc", "-I", os.path.join(REPO, "include"), c, "-o", exe], check=True)
+        vals = list(map(int, subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split()))
+    assert vals == [ctypes.sizeof(rt_amd.SceneFlat), ctypes.sizeof(rt_amd.Frame), ctypes.sizeof(rt_amd.Stats),
+                    rt_amd.Frame.width.offset, rt_amd.Frame.flags.offset, rt_amd.Stats.kernel_ms.offset]
+
+
+def test_null_arguments_are_errors():
+    L = rt_amd.lib()
+    assert L.rt_scene_create(None) == -1
+    assert L.rt_scene_set_resolution(None, 4, 4) == -1
+    assert L.rt_scene_load_file(None, b"x") == -1
+    assert L.rt_upload_scene(None, None) == -1
+    assert L.rt_render(None, None, None) == -1
+    assert L.rt_render_float(None, None, None) == -1
+    assert L.rt_render_async(None, None, None, None, None) == -1
+    assert L.rt_last_stats(None, None) == -1
+    assert L.rt_last_error(None) == b"null context"
+    L.rt_destroy(None)
+    L.rt_scene_destroy(None)
+
+
+def test_call_order_errors():
+    L = rt_amd.lib()
+    h = ctypes.c_void_p()
+    assert L.rt_scene_create(ctypes.byref(h)) == 0
+    f = rt_amd.SceneFlat()
+    assert L.rt_scene_get_flat(h, ctypes.byref(f)) == -4      # before prepare
+    assert L.rt_scene_prepare(h) == -4                         # before load
+    assert L.rt_scene_set_max_bounces(h, -1) == -1
+    L.rt_scene_destroy(h)
+
+
+def test_cli_built():
+    exe = os.path.join(REPO, "ray-tracing-gpu_amd", "lib", "rt_render")
+    assert os.access(exe, os.X_OK)
+    r = subprocess.run([exe], capture_output=True, text=True)
+    assert r.returncode == 1 and "Aucune fichier" in r.stderr

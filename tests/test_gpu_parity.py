@@ -1,0 +1,164 @@
+"""Parity of the HIP path (librt_amd.so through the C ABI) with the reference.
+
+Checkers: the golden fixtures (made from the reference's own sources, see
+tests/golden/make_golden.py) and the oracle restatement.  Bar: RGBA8 within
+1 LSB per channel (north star); in practice the float32 RGB is compared
+bit-for-bit and every deviation is reported (PHONG_ULP below is the only
+allowance: ocml powf vs glibc powf on Phong highlights)."""
+from __future__ import annotations
+
+import hashlib
+
+import numpy as np
+import pytest
+
+import rt_amd
+from conftest import bits_equal, rgba8, scene, ulp_diff
+
+pytestmark = pytest.mark.gpu
+
+# Only scene4 has a specular (Phong) term -> powf.  glibc's powf and ROCm's
+# ocml powf are both faithfully (not correctly) rounded, so a highlight may
+# differ by an ulp or two in float; RGBA8 must still be within 1 LSB.
+PHONG_SCENES = {4}
+PHONG_ULP = 8
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    return rt_amd.Context(0)
+
+
+def render(ctx, path, w, h, depth, as_float=True, rows=None, flags=0):
+    s = rt_amd.Scene(path, w, h, depth)
+    ctx.upload(s)
+    f = s.frame.copy()
+    f.flags = flags
+    if rows:
+        f.row_begin, f.row_end = rows
+    return ctx.render_float(f) if as_float else ctx.render(f)
+
+
+def check(got, want, i):
+    if i in PHONG_SCENES:
+        assert ulp_diff(got, want) <= PHONG_ULP
+    else:
+        assert bits_equal(got, want), f"max |d| {np.abs(got - want).max()} ulps {ulp_diff(got, want)}"
+    assert np.abs(rgba8(got).astype(int) - rgba8(want).astype(int)).max() <= 1
+
+
+@pytest.mark.parametrize("i", range(1, 10))
+@pytest.mark.parametrize("depth", [0, 1, 3, 5])
+def test_scene_images(ctx, golden_images, i, depth):
+    got = render(ctx, scene(i), 64, 48, depth)
+    check(got, golden_images[f"scene{i}_64x48_d{depth}"], i)
+
+
+@pytest.mark.parametrize("wh", [(1, 1), (13, 7), (67, 33)])
+def test_ragged_sizes(ctx, golden_images, wh):
+    w, h = wh
+    check(render(ctx, scene(5), w, h, 3), golden_images[f"scene5_{w}x{h}_d3"], 5)
+
+
+def test_rgba8_is_quantised_float(ctx):
+    for i in (1, 4, 7):
+        s = rt_amd.Scene(scene(i), 96, 64, 5)
+        ctx.upload(s)
+        f = ctx.render_float(s.frame)
+        q = ctx.render(s.frame)
+        assert np.array_equal(q, rgba8(f))
+
+
+@pytest.mark.parametrize("name,i,w,h,depth", [
+    ("scene2_1080p_d0", 2, 1920, 1080, 0),
+    ("scene2_1080p_d3", 2, 1920, 1080, 3),
+    ("scene7_2160p_d5", 7, 3840, 2160, 5),
+    ("scene9_2160p_d5", 9, 3840, 2160, 5),
+])
+def test_big_frame_windows(ctx, golden_images, name, i, w, h, depth):
+    full = render(ctx, scene(i), w, h, depth)
+    keys = [k for k in golden_images.files if k.startswith(name + "_win_")]
+    assert keys
+    for k in keys:
+        r0, r1, c0, c1 = map(int, k.rsplit("_win_", 1)[1].split("_"))
+        check(full[r0:r1, c0:c1], golden_images[k], i)
+
+
+def test_heightfield_windows(ctx, golden_images, heightfield_path):
+    full = render(ctx, heightfield_path, 1920, 1080, 1)
+    for k in [k for k in golden_images.files if k.startswith("hf_1080p_d1_win_")]:
+        r0, r1, c0, c1 = map(int, k.rsplit("_win_", 1)[1].split("_"))
+        check(full[r0:r1, c0:c1], golden_images[k], 0)
+
+
+def test_scene2_1080p_digest_and_counts(ctx, digests):
+    full = render(ctx, scene(2), 1920, 1080, 0, flags=rt_amd.FLAG_STATS)
+    st = ctx.stats()
+    assert hashlib.sha256(full.tobytes()).hexdigest() == digests["scene2_1920x1080_d0_rgb_f32_sha256"]
+    assert hashlib.sha256(rgba8(full).tobytes()).hexdigest() == digests["scene2_1920x1080_d0_rgba8_sha256"]
+    # ray counts of the reference's CPU loop at this config (gprof)
+    assert st.primary_rays == 2_073_600
+    assert st.shadow_rays == 5_618_440
+    assert st.bounce_rays == 0
+
+
+def test_scene2_depth_inert_full_size(ctx):
+    """C4 property at full size: scene2 has no Kr/Kt, so depth 5 == depth 0."""
+    a = render(ctx, scene(2), 3840, 2160, 5, as_float=False)
+    b = render(ctx, scene(2), 3840, 2160, 0, as_float=False)
+    assert np.array_equal(a, b) and (a[..., 3] == 255).all()
+
+
+@pytest.mark.parametrize("nslabs", [2, 3, 8])
+def test_row_slabs_reassemble(ctx, nslabs):
+    """The multi-GPU partition: slabs rendered separately == the full frame."""
+    w, h = 200, 150
+    s = rt_amd.Scene(scene(7), w, h, 3)
+    ctx.upload(s)
+    full = ctx.render(s.frame)
+    parts = []
+    for r in range(nslabs):
+        f = s.frame.copy()
+        f.row_begin, f.row_end = r * h // nslabs, (r + 1) * h // nslabs
+        parts.append(ctx.render(f))
+    assert np.array_equal(np.concatenate(parts, 0), full)
+
+
+def test_async_device_outputs(ctx):
+    torch = pytest.importorskip("torch")
+    s = rt_amd.Scene(scene(6), 128, 96, 3)
+    ctx.upload(s)
+    rgba = torch.zeros((96, 128, 4), dtype=torch.uint8, device="cuda")
+    rgb = torch.zeros((96, 128, 3), dtype=torch.float32, device="cuda")
+    ctx.render_async(s.frame, rgba.data_ptr(), rgb.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(rgba.cpu().numpy(), ctx.render(s.frame))
+    assert bits_equal(rgb.cpu().numpy(), ctx.render_float(s.frame))
+
+
+def test_device_pointer_sync_render(ctx):
+    torch = pytest.importorskip("torch")
+    s = rt_amd.Scene(scene(3), 64, 64, 0)
+    ctx.upload(s)
+    out = torch.zeros((64, 64, 4), dtype=torch.uint8, device="cuda")
+    assert rt_amd.lib().rt_render(ctx._h, rt_amd.ctypes.byref(s.frame), out.data_ptr()) == 0
+    assert np.array_equal(out.cpu().numpy(), ctx.render(s.frame))
+
+
+def test_deep_bounces_and_limits(ctx, oracle):
+    # scene9: two facing mirrors (Kr 0.99) — depth 20 is the reference's default m_NbRebondsMax
+    got = render(ctx, scene(9), 48, 32, 20)
+    want = oracle.render(scene(9), 48, 32, 20)
+    assert bits_equal(got, want)
+    with pytest.raises(rt_amd.RtError) as e:
+        render(ctx, scene(9), 8, 8, 40)
+    assert e.value.code == -6
+
+
+def test_bad_frame_rejected(ctx):
+    s = rt_amd.Scene(scene(1), 16, 16, 0)
+    ctx.upload(s)
+    f = s.frame.copy()
+    f.row_end = 17
+    with pytest.raises(rt_amd.RtError):
+        ctx.render(f)
