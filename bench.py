@@ -141,8 +141,9 @@ def main():
     ctx.upload(scene)
     types = scene.arrays()[0]
 
-    rows = -(-H // world)                      # equal slabs (padded when H % world != 0)
-    r0, r1 = min(H, rank * rows), min(H, (rank + 1) * rows)
+    from rt_amd.dist import gather_frame, slab_rows
+
+    r0, r1, rows = slab_rows(H, world, rank)   # equal slabs (padded when H % world != 0)
     frame = scene.frame.copy()
     frame.row_begin, frame.row_end = r0, r1
     slab = torch.zeros((rows, W, 4), dtype=torch.uint8, device="cuda")
@@ -163,7 +164,7 @@ def main():
         if ev is not None:
             ev[1].record()
         if world > 1:
-            dist.all_gather_into_tensor(full, slab)
+            gather_frame(slab, full, dist)
 
     for _ in range(args.warmup):
         step()

@@ -126,9 +126,10 @@ int rt_upload_scene(rt_ctx*, const rt_scene_flat*);
 int rt_render(rt_ctx*, const rt_frame*, uint8_t* rgba8_out);
 /* Parity/debug: float RGB exactly as m_InfoPixel (unclamped), 3 floats/px. */
 int rt_render_float(rt_ctx*, const rt_frame*, float* rgb_out);
-/* Asynchronous, device pointers only, on `hip_stream` (hipStream_t; NULL =
- * the context's own stream).  Either output may be NULL.  No host sync, no
- * allocation: safe to capture in a hipGraph or to enqueue behind RCCL. */
+/* Asynchronous, device pointers only, enqueued on `hip_stream` (a hipStream_t;
+ * NULL = the HIP null stream, as in every HIP API).  Either output may be
+ * NULL.  No host sync, no allocation: safe to capture in a hipGraph or to
+ * enqueue ahead of an RCCL collective on the same stream. */
 int rt_render_async(rt_ctx*, const rt_frame*, uint8_t* rgba8_dev, float* rgb_dev, void* hip_stream);
 int rt_last_stats(rt_ctx*, rt_stats* out);
 const char* rt_last_error(rt_ctx*);

@@ -735,8 +735,7 @@ RT_EXPORT int rt_render_float(rt_ctx* c, const rt_frame* f, float* rgb_out) { re
 RT_EXPORT int rt_render_async(rt_ctx* c, const rt_frame* f, uint8_t* rgba8_dev, float* rgb_dev, void* stream)
 {
     if (!c || !f) return RT_E_ARG;
-    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
-    return launch(c, f, (unsigned*)rgba8_dev, rgb_dev, st, false);
+    return launch(c, f, (unsigned*)rgba8_dev, rgb_dev, (hipStream_t)stream, false);
 }
 
 RT_EXPORT int rt_last_stats(rt_ctx* c, rt_stats* out)

@@ -103,6 +103,13 @@ def lib() -> ctypes.CDLL:
     """Load librt_amd.so once; raise (never fall back) if it is absent."""
     global _lib
     if _lib is None:
+        # One HIP runtime per process: when PyTorch (the device-memory /
+        # stream / RCCL plumbing) is installed, its bundled libamdhip64.so.7
+        # must be the one librt_amd.so binds to (same SONAME), so load it first.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not os.path.exists(LIB_PATH):
             raise RtError("load", -4, f"{LIB_PATH} not built (run __graft_entry__.build())")
         L = ctypes.CDLL(LIB_PATH)

@@ -1,0 +1,75 @@
+"""The N>1 path on CPU: world_size-2 (and 3) gloo process groups run the
+product's slab partition + gather (rt_amd.dist) with the oracle standing in
+for the per-rank renderer (no GPU here), and the assembled frame must equal
+the single-process frame byte for byte."""
+from __future__ import annotations
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import SCENES, rgba8
+
+from rt_amd.dist import slab_rows
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, path, w, h, depth, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from conftest import Oracle
+    from rt_amd.dist import gather_frame
+
+    r0, r1, rows = slab_rows(h, world, rank)
+    slab = torch.zeros((rows, w, 4), dtype=torch.uint8)
+    if r1 > r0:
+        img = Oracle().render(path, w, h, depth, (r0, r1, 0, w), threads=1)
+        slab[: r1 - r0] = torch.from_numpy(rgba8(img))
+    full = torch.zeros((world * rows, w, 4), dtype=torch.uint8)
+    gather_frame(slab, full, dist)
+    if rank == 0:
+        out_q.put(full[:h].numpy().copy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,h", [(2, 30), (3, 31)])
+def test_gather_matches_single_frame(oracle, world, h):
+    w, depth = 40, 3
+    path = os.path.join(SCENES, "scene7.dat")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, path, w, h, depth, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = rgba8(oracle.render(path, w, h, depth))
+    assert np.array_equal(got, want)
+
+
+def test_slab_rows_cover_frame():
+    for h in (1, 7, 1080, 4320, 2161):
+        for world in (1, 2, 3, 4, 8):
+            spans = [slab_rows(h, world, r) for r in range(world)]
+            rows = [r1 - r0 for r0, r1, _ in spans]
+            assert sum(rows) == h
+            assert all(s[2] == spans[0][2] for s in spans)
+            assert spans[0][0] == 0 and spans[-1][1] == h
+            for a, b in zip(spans, spans[1:]):
+                assert a[1] == b[0]

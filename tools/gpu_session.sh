@@ -1,0 +1,31 @@
+#!/bin/bash
+# One GPU session on the gpurun box: parity tests, smoke, bench, rocprof.
+# Every GPU step has its own time limit; a timeout / crash / abort stops the
+# session (no further GPU work), an ordinary test failure does not.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+STEPS="${STEPS:-tests smoke bench prof}"
+run() {  # name seconds cmd...
+  local name=$1 secs=$2; shift 2
+  echo "== $name: $*" | tee -a gpurun_out/session.log
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc" | tee -a gpurun_out/session.log
+  tail -5 "gpurun_out/$name.log"
+  if [ $rc -ge 124 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then
+    echo "!! stopping session after $name (rc=$rc)"; exit $rc
+  fi
+  return 0
+}
+for s in $STEPS; do
+  case $s in
+    tests) run pytest_gpu 600 python -m pytest tests -m gpu -x -q -rA ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 400 python bench.py ;;
+    bench_all)
+      for c in c1 c2 c3 c4 c4s7 c4s9; do run bench_$c 400 python bench.py --config $c --steps 10 --cpu-seconds 5; done ;;
+    prof) run rocprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 20 --no-cpu-baseline ;;
+  esac
+done
+exit 0
