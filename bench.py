@@ -102,7 +102,7 @@ def cpu_baseline(path, w, h, depth, seconds):
         px += 64
         k += 1
         el = time.perf_counter() - t0
-        if el >= seconds or (k >= len(wins) and el >= seconds / 4):
+        if el >= seconds and k >= min(len(wins), 64):
             break
     free(p)
     return {"value": round(px / el / 1e6, 4), "unit": "Mray/s", "cores": 1, "kind": kind,
