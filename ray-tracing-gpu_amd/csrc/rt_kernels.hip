@@ -27,6 +27,7 @@
 //  * no FMA contraction, IEEE f32 division and sqrt.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -52,13 +53,28 @@ namespace rt {
 // Material (3 x float4): [r g b Ka] [Kd Ks shin Kr] [Kt ior 0 0]
 // Light    (2 x float4): [x y z I]  [r g b 0]
 struct SceneDev {
-    const float4* __restrict__ geom;
+    const float4* __restrict__ geom;    // file order, 64-byte records (above)
     const float4* __restrict__ mat;
     const float4* __restrict__ lights;
-    int n_surf;
-    int n_lights;
-    int opaque_exit;  // filter factors all finite and >= +0
-    int pad;
+    // Per-kind arrays for the closest-hit and any-hit loops (48/32/48 bytes),
+    // each carrying its FILE index; opaque surfaces come first in each array.
+    //   tri  : [p0 e1.x] [e1.y e1.z e2.x e2.y] [e2.z idx 0 0]
+    //   plane: [n cst]   [idx 0 0 0]
+    //   quad : [quad mix.x] [mix.y mix.z lin.x lin.y] [lin.z cst idx 0]
+    const float4* __restrict__ tri;
+    const float4* __restrict__ plane;
+    const float4* __restrict__ quad;
+    const int* __restrict__ translucent;  // file indices with a non-zero filter factor, file order
+    int n_surf, n_lights;
+    int n_tri, n_plane, n_quad;
+    int n_tri_opaque, n_plane_opaque, n_quad_opaque;
+    int n_translucent;
+    // 1: every filter factor is finite and >= +0, so a ray that meets any
+    //    fully opaque surface (factor exactly (0,0,0)) has a filter of exactly
+    //    (+0,+0,+0) whatever the order — opaque surfaces are then an any-hit
+    //    test (stop at the first hit, by kind), and only the translucent ones
+    //    are multiplied, in file order.  0: the file-order product over all.
+    int shadow_split;
 };
 
 struct FrameDev {
@@ -172,25 +188,84 @@ __device__ __forceinline__ Vec3 quadric_normal(const float4 a, const float4 b, c
 
 __device__ __forceinline__ int kind_of(const float4 a) { return __float_as_int(a.x); }
 
-// Scene.cpp:1705-1715: closest hit in file order; strict '<' keeps the first
-// of equal distances.  Returns the winning index (-1 = miss).
+// Lexicographic (distance, file index) minimum: the reference keeps the first
+// surface in file order among equal distances (strict '<', Scene.cpp:1713),
+// which is exactly min over (t, index).  That lets each kind run in its own
+// loop without changing a single winner.
+__device__ __forceinline__ void take_min(bool ok, float t, int idx, float& bt, int& bi)
+{
+    if (ok && t > kEps && (bi < 0 || t < bt || (t == bt && idx < bi))) {
+        bt = t;
+        bi = idx;
+    }
+}
+
+// Triangle test split at the u bound so a wave can drop a triangle that no
+// lane's ray crosses the u-range of (exact: the skipped values could only have
+// produced rejections).
+struct TriU {
+    Vec3 S, P;
+    float inv, u;
+    bool ok;
+};
+__device__ __forceinline__ TriU tri_u(const Vec3 p0, const Vec3 e1, const Vec3 e2, const Vec3 O, const Vec3 D)
+{
+    TriU r;
+    r.P = cross(D, e2);
+    const float det = dot(e1, r.P);
+    r.inv = 1.0f / det;
+    r.S = O - p0;
+    r.u = dot(r.S, r.P) * r.inv;
+    r.ok = !(fabsf(det) < kEps) && !(r.u < 0 || r.u > 1);
+    return r;
+}
+__device__ __forceinline__ bool tri_vt(const TriU& r, const Vec3 e1, const Vec3 e2, const Vec3 D, float& t)
+{
+    const Vec3 Q = cross(r.S, e1);
+    const float v = dot(D, Q) * r.inv;
+    t = dot(e2, Q) * r.inv;
+    return r.ok && !(v < 0 || r.u + v > 1);
+}
+
+struct TriRec {
+    Vec3 p0, e1, e2;
+    int idx;
+};
+__device__ __forceinline__ TriRec load_tri(const SceneDev& S, int k)
+{
+    const float4* r = S.tri + 3 * k;
+    const float4 a = r[0], b = r[1], c = r[2];
+    return TriRec{make3(a.x, a.y, a.z), make3(a.w, b.x, b.y), make3(b.z, b.w, c.x), __float_as_int(c.y)};
+}
+
+// Scene.cpp:1705-1715: closest hit over every surface.  Returns the winning
+// FILE index (-1 = miss) and its distance.
 __device__ __forceinline__ int closest_hit(const SceneDev& S, const Vec3 O, const Vec3 D, float& best_t)
 {
     float bt = -1.0f;
     int bi = -1;
-    for (int i = 0; i < S.n_surf; ++i) {
-        const float4* rec = S.geom + 4 * i;
-        const float4 a = rec[0], b = rec[1], c = rec[2];
+    for (int k = 0; k < S.n_tri; ++k) {
+        const TriRec tr = load_tri(S, k);
+        const TriU r = tri_u(tr.p0, tr.e1, tr.e2, O, D);
+        if (!__any(r.ok)) continue;
         float t;
-        bool ok;
-        const int kind = kind_of(a);
-        if (kind == RT_TRIANGLE) ok = hit_triangle(a, b, c, O, D, t);
-        else if (kind == RT_PLANE) ok = hit_plane(a, b, O, D, t);
-        else ok = hit_quadric(a, b, c, O, D, t);
-        if (ok && t > kEps && (t < bt || bt < 0)) {
-            bt = t;
-            bi = i;
-        }
+        const bool ok = tri_vt(r, tr.e1, tr.e2, D, t);
+        take_min(ok, t, tr.idx, bt, bi);
+    }
+    for (int k = 0; k < S.n_plane; ++k) {
+        const float4 a = S.plane[2 * k], b = S.plane[2 * k + 1];
+        float t;
+        const bool ok = hit_plane(make_float4(0.f, a.x, a.y, a.z), make_float4(a.w, 0.f, 0.f, 0.f), O, D, t);
+        take_min(ok, t, __float_as_int(b.x), bt, bi);
+    }
+    for (int k = 0; k < S.n_quad; ++k) {
+        const float4* r = S.quad + 3 * k;
+        const float4 a = r[0], b = r[1], c = r[2];
+        float t;
+        // repack into the file-order record layout hit_quadric reads
+        const bool ok = hit_quadric(make_float4(0.f, a.x, a.y, a.z), make_float4(a.w, b.x, b.y, b.z),
+                                    make_float4(b.w, c.x, c.y, 0.f), O, D, t);
+        take_min(ok, t, __float_as_int(c.z), bt, bi);
     }
     best_t = bt;
     return bi;
@@ -216,6 +291,21 @@ __device__ __forceinline__ Mat load_mat(const SceneDev& S, int idx)
     return Mat{{m0.x, m0.y, m0.z}, m0.w, m1.x, m1.y, m1.z, m1.w, m2.x, m2.y};
 }
 
+// One file-order surface record against a shadow ray (generic path).
+__device__ __forceinline__ bool shadow_hit_record(const float4* rec, const Vec3 P, const Vec3 L, float dist,
+                                                  Color& fc)
+{
+    const float4 a = rec[0], b = rec[1], c = rec[2], d = rec[3];
+    float t;
+    bool ok;
+    const int kind = kind_of(a);
+    if (kind == RT_TRIANGLE) ok = hit_triangle(a, b, c, P, L, t);
+    else if (kind == RT_PLANE) ok = hit_plane(a, b, P, L, t);
+    else ok = hit_quadric(a, b, c, P, L, t);
+    fc = Color{d.y, d.z, d.w};
+    return ok && t > kEps && t < dist;
+}
+
 // Scene.cpp:1842-1861 ObtenirFiltreDeSurface.  L is the UNNORMALISED light
 // vector; it is normalised here exactly like the reference (in place).
 __device__ __forceinline__ Color shadow_filter(const SceneDev& S, const Vec3 P, Vec3& L,
@@ -224,24 +314,53 @@ __device__ __forceinline__ Color shadow_filter(const SceneDev& S, const Vec3 P, 
     Color F{1.0f, 1.0f, 1.0f};
     const float dist = norm(L);
     L = div_recip(L, dist);
-    bool lit = true;
-    for (int i = 0; i < S.n_surf; ++i) {
-        const float4* rec = S.geom + 4 * i;
-        const float4 a = rec[0], b = rec[1], c = rec[2], d = rec[3];
+    if (!S.shadow_split) {
+        // General case: the product over every surface in file order.
+        for (int i = 0; i < S.n_surf; ++i) {
+            Color fc;
+            if (shadow_hit_record(S.geom + 4 * i, P, L, dist, fc)) F *= fc;
+        }
+        return F;
+    }
+    // Opaque surfaces: any hit zeroes the filter exactly.  A lane stops
+    // counting once occluded; the wave leaves a loop once all lanes are.
+    bool occluded = false;
+    int done = 0, total = S.n_tri_opaque + S.n_plane_opaque + S.n_quad_opaque;
+    for (int k = 0; k < S.n_tri_opaque; ++k) {
+        if (!__any(!occluded)) break;
+        ++done;
+        const TriRec tr = load_tri(S, k);
+        const TriU r = tri_u(tr.p0, tr.e1, tr.e2, P, L);
+        if (!__any(r.ok && !occluded)) continue;
         float t;
-        bool ok;
-        const int kind = kind_of(a);
-        if (kind == RT_TRIANGLE) ok = hit_triangle(a, b, c, P, L, t);
-        else if (kind == RT_PLANE) ok = hit_plane(a, b, P, L, t);
-        else ok = hit_quadric(a, b, c, P, L, t);
-        if (ok && t > kEps && t < dist) {
-            F *= Color{d.y, d.z, d.w};
-            lit = (F.r != 0.0f) | (F.g != 0.0f) | (F.b != 0.0f);
-        }
-        if (S.opaque_exit && !__any(lit)) {
-            skipped += (unsigned)(S.n_surf - 1 - i);
-            break;
-        }
+        const bool ok = tri_vt(r, tr.e1, tr.e2, L, t);
+        occluded |= ok && t > kEps && t < dist;
+    }
+    for (int k = 0; k < S.n_plane_opaque; ++k) {
+        if (!__any(!occluded)) break;
+        ++done;
+        const float4 a = S.plane[2 * k];
+        float t;
+        const bool ok = hit_plane(make_float4(0.f, a.x, a.y, a.z), make_float4(a.w, 0.f, 0.f, 0.f), P, L, t);
+        occluded |= ok && t > kEps && t < dist;
+    }
+    for (int k = 0; k < S.n_quad_opaque; ++k) {
+        if (!__any(!occluded)) break;
+        ++done;
+        const float4* r = S.quad + 3 * k;
+        const float4 a = r[0], b = r[1], c = r[2];
+        float t;
+        const bool ok = hit_quadric(make_float4(0.f, a.x, a.y, a.z), make_float4(a.w, b.x, b.y, b.z),
+                                    make_float4(b.w, c.x, c.y, 0.f), P, L, t);
+        occluded |= ok && t > kEps && t < dist;
+    }
+    skipped += (unsigned)(total - done);
+    if (occluded) return Color{0.0f, 0.0f, 0.0f};
+    // Translucent surfaces, file order (the relative order of the factors the
+    // reference multiplies is preserved; unhit opaque surfaces contribute none).
+    for (int j = 0; j < S.n_translucent; ++j) {
+        Color fc;
+        if (shadow_hit_record(S.geom + 4 * S.translucent[j], P, L, dist, fc)) F *= fc;
     }
     return F;
 }
@@ -447,11 +566,17 @@ struct rt_ctx {
     float4* d_geom = nullptr;
     float4* d_mat = nullptr;
     float4* d_lights = nullptr;
+    float4* d_tri = nullptr;
+    float4* d_plane = nullptr;
+    float4* d_quad = nullptr;
+    int* d_translucent = nullptr;
     StatsDev* d_stats = nullptr;
     void* d_scratch = nullptr;  // staging for host outputs
     size_t scratch_bytes = 0;
     int n_surf = 0, n_lights = 0;
-    int opaque_exit = 0;
+    int n_tri = 0, n_plane = 0, n_quad = 0;
+    int n_tri_opaque = 0, n_plane_opaque = 0, n_quad_opaque = 0, n_translucent = 0;
+    int shadow_split = 0;
     float k_max = 0.0f;         // max(Kr, Kt) over surfaces (NaN ignored)
     bool uploaded = false;
     rt_stats last{};
@@ -505,6 +630,10 @@ RT_EXPORT void rt_destroy(rt_ctx* c)
     hipFree(c->d_geom);
     hipFree(c->d_mat);
     hipFree(c->d_lights);
+    hipFree(c->d_tri);
+    hipFree(c->d_plane);
+    hipFree(c->d_quad);
+    hipFree(c->d_translucent);
     hipFree(c->d_stats);
     hipFree(c->d_scratch);
     if (c->ev0) hipEventDestroy(c->ev0);
@@ -560,6 +689,44 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
         if (m[7] > kmax) kmax = m[7];
         if (m[8] > kmax) kmax = m[8];
     }
+    // Per-kind arrays, opaque surfaces first (file order kept inside each class).
+    auto opaque_at = [&](int i) {
+        const float* o = &geom[16 * (size_t)i];
+        return o[13] == 0.0f && o[14] == 0.0f && o[15] == 0.0f;
+    };
+    std::vector<float> tri, pla, qua;
+    std::vector<int> translucent;
+    int n_tri_o = 0, n_pla_o = 0, n_qua_o = 0;
+    for (int pass = 0; pass < 2; ++pass) {
+        for (int i = 0; i < n; ++i) {
+            if (opaque_at(i) != (pass == 0)) continue;
+            const float* o = &geom[16 * (size_t)i];
+            float idx;
+            std::memcpy(&idx, &i, sizeof(int));
+            const int kind = s->type[i];
+            if (kind == RT_TRIANGLE) {
+                const float r[12] = {o[1], o[2], o[3], o[4], o[5], o[6], o[7], o[8], o[9], idx, 0.f, 0.f};
+                tri.insert(tri.end(), r, r + 12);
+                n_tri_o += pass == 0;
+            } else if (kind == RT_PLANE) {
+                const float r[8] = {o[1], o[2], o[3], o[4], idx, 0.f, 0.f, 0.f};
+                pla.insert(pla.end(), r, r + 8);
+                n_pla_o += pass == 0;
+            } else {
+                const float r[12] = {o[1], o[2], o[3], o[4], o[5], o[6], o[7], o[8], o[9], o[10], idx, 0.f};
+                qua.insert(qua.end(), r, r + 12);
+                n_qua_o += pass == 0;
+            }
+        }
+    }
+    for (int i = 0; i < n; ++i)
+        if (!opaque_at(i)) translucent.push_back(i);
+    const int cnt_tri = (int)(tri.size() / 12), cnt_pla = (int)(pla.size() / 8), cnt_qua = (int)(qua.size() / 12);
+    const int cnt_translucent = (int)translucent.size();
+    tri.resize(std::max<size_t>(tri.size(), 12));
+    pla.resize(std::max<size_t>(pla.size(), 8));
+    qua.resize(std::max<size_t>(qua.size(), 12));
+    translucent.resize(std::max<size_t>(translucent.size(), 1));
     for (int j = 0; j < nl; ++j) {
         const float* l = s->lights + 7 * (size_t)j;
         float* o = &lig[8 * (size_t)j];
@@ -569,7 +736,22 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
     hipFree(c->d_geom);
     hipFree(c->d_mat);
     hipFree(c->d_lights);
-    c->d_geom = c->d_mat = c->d_lights = nullptr;
+    hipFree(c->d_tri);
+    hipFree(c->d_plane);
+    hipFree(c->d_quad);
+    hipFree(c->d_translucent);
+    c->d_geom = c->d_mat = c->d_lights = c->d_tri = c->d_plane = c->d_quad = nullptr;
+    c->d_translucent = nullptr;
+    c->uploaded = false;
+    auto up = [&](void** dst, const void* src, size_t bytes) -> hipError_t {
+        hipError_t e = hipMalloc(dst, bytes);
+        if (e != hipSuccess) return e;
+        return hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice);
+    };
+    HIP_TRY(c, up((void**)&c->d_tri, tri.data(), tri.size() * sizeof(float)));
+    HIP_TRY(c, up((void**)&c->d_plane, pla.data(), pla.size() * sizeof(float)));
+    HIP_TRY(c, up((void**)&c->d_quad, qua.data(), qua.size() * sizeof(float)));
+    HIP_TRY(c, up((void**)&c->d_translucent, translucent.data(), translucent.size() * sizeof(int)));
     HIP_TRY(c, hipMalloc(&c->d_geom, geom.size() * sizeof(float)));
     HIP_TRY(c, hipMalloc(&c->d_mat, mat.size() * sizeof(float)));
     HIP_TRY(c, hipMalloc(&c->d_lights, lig.size() * sizeof(float)));
@@ -578,7 +760,14 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
     HIP_TRY(c, hipMemcpy(c->d_lights, lig.data(), lig.size() * sizeof(float), hipMemcpyHostToDevice));
     c->n_surf = n;
     c->n_lights = nl;
-    c->opaque_exit = opaque ? 1 : 0;
+    c->n_tri = cnt_tri;
+    c->n_plane = cnt_pla;
+    c->n_quad = cnt_qua;
+    c->n_tri_opaque = n_tri_o;
+    c->n_plane_opaque = n_pla_o;
+    c->n_quad_opaque = n_qua_o;
+    c->n_translucent = cnt_translucent;
+    c->shadow_split = opaque ? 1 : 0;
     c->k_max = kmax;
     c->uploaded = true;
     return RT_OK;
@@ -638,7 +827,9 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
         c->err = "reachable bounce depth " + std::to_string(depth) + " exceeds the compiled stack (32)";
         return RT_E_UNSUPPORTED;
     }
-    SceneDev S{c->d_geom, c->d_mat, c->d_lights, c->n_surf, c->n_lights, c->opaque_exit, 0};
+    SceneDev S{c->d_geom, c->d_mat, c->d_lights, c->d_tri, c->d_plane, c->d_quad, c->d_translucent,
+               c->n_surf, c->n_lights, c->n_tri, c->n_plane, c->n_quad,
+               c->n_tri_opaque, c->n_plane_opaque, c->n_quad_opaque, c->n_translucent, c->shadow_split};
     FrameDev F;
     std::memcpy(F.cam, f->cam_pos, sizeof F.cam);
     std::memcpy(F.orient, f->orient, sizeof F.orient);

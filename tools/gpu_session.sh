@@ -25,6 +25,7 @@ for s in $STEPS; do
     bench) run bench 400 python bench.py ;;
     bench_all)
       for c in c1 c2 c3 c4 c4s7 c4s9; do run bench_$c 400 python bench.py --config $c --steps 10 --cpu-seconds 5; done ;;
+    rcp) run rcp_exhaustive 300 tools/rcp_exhaustive ;;
     prof) run rocprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 20 --no-cpu-baseline ;;
   esac
 done
