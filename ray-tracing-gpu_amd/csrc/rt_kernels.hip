@@ -409,7 +409,11 @@ __device__ __forceinline__ Color shade_local(const SceneDev& S, const Mat& m, co
             const Vec3 rf = reflect(L, N);
             const float ps = dot(rf, D);
             if (ps > 0) {
-                const float pf = l0.w * m.ks * powf(ps, m.shin);
+                // pow(x, 0) == 1 for every x (C99 F.9.4.4, glibc and ocml alike):
+                // materials without a shininess never pay for powf.
+                float pw = 1.0f;
+                if (m.shin != 0.0f) pw = powf(ps, m.shin);
+                const float pf = l0.w * m.ks * pw;
                 res += LC * pf;
             }
         }

@@ -25,6 +25,14 @@ for s in $STEPS; do
     bench) run bench 400 python bench.py ;;
     bench_all)
       for c in c1 c2 c3 c4 c4s7 c4s9; do run bench_$c 400 python bench.py --config $c --steps 10 --cpu-seconds 5; done ;;
+    listpmc) run list_counters 120 rocprofv3 -L ;;
+    pmc)
+      B="python bench.py --steps 5 --warmup 1 --no-cpu-baseline --config ${CONFIG:-c2}"
+      run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc -o fetch -- $B
+      run pmc_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc -o write -- $B
+      run pmc_sq 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmc -o sq -- $B
+      run pmc_sq2 300 rocprofv3 --pmc SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM SQ_INSTS_LDS SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_SALU SQ_THREAD_CYCLES_VALU SQ_INSTS_BRANCH --output-format csv -d gpurun_out/pmc -o sq2 -- $B
+      ;;
     rcp) run rcp_exhaustive 300 tools/rcp_exhaustive ;;
     prof) run rocprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 20 --no-cpu-baseline ;;
   esac
