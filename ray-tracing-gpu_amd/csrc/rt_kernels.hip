@@ -39,6 +39,12 @@
 
 #pragma clang fp contract(off)
 
+#ifndef RT_TRI_UNROLL
+#define RT_TRI_UNROLL 1
+#endif
+#define RT_PRAGMA(x) _Pragma(#x)
+#define RT_UNROLL(n) RT_PRAGMA(unroll n)
+
 namespace rt {
 
 // ------------------------------------------------------------ device layout
@@ -65,6 +71,12 @@ struct SceneDev {
     const float4* __restrict__ plane;
     const float4* __restrict__ quad;
     const int* __restrict__ translucent;  // file indices with a non-zero filter factor, file order
+    // Camera-ray form of tri[] for the frame's camera position C (same order):
+    //   [e1 e2.x] [e2.y e2.z S.x S.y] [S.z Q] [tQ idx 0 0]
+    // with S = C - p0, Q = S x e1, tQ = e2 . Q — exactly the values
+    // Triangle.cpp:139-160 computes for a ray whose origin is C, so they are
+    // computed once per camera instead of once per pixel.
+    const float4* __restrict__ tricam;
     int n_surf, n_lights;
     int n_tri, n_plane, n_quad;
     int n_tri_opaque, n_plane_opaque, n_quad_opaque;
@@ -266,6 +278,7 @@ __device__ __forceinline__ int closest_hit(const SceneDev& S, const Vec3 O, cons
 {
     float bt = -1.0f;
     int bi = -1;
+    RT_UNROLL(RT_TRI_UNROLL)
     for (int k = 0; k < S.n_tri; ++k) {
         const TriRec tr = load_tri(S, k);
         const TriU r = tri_u(tr.p0, tr.e1, tr.e2, O, D);
@@ -291,6 +304,62 @@ __device__ __forceinline__ int closest_hit(const SceneDev& S, const Vec3 O, cons
     }
     best_t = bt;
     return bi;
+}
+
+// Closest hit for camera rays (origin = the camera for every lane): the
+// per-triangle values that depend only on the origin come from tricam[].
+__device__ __forceinline__ int closest_hit_camera(const SceneDev& S, const Vec3 O, const Vec3 D, float& best_t)
+{
+    float bt = -1.0f;
+    int bi = -1;
+    for (int k = 0; k < S.n_tri; ++k) {
+        const float4* r = S.tricam + 4 * k;
+        const float4 a = r[0], b = r[1], c = r[2], d = r[3];
+        const Vec3 e1 = make3(a.x, a.y, a.z), e2 = make3(a.w, b.x, b.y);
+        const Vec3 Sv = make3(b.z, b.w, c.x), Q = make3(c.y, c.z, c.w);
+        const Vec3 P = cross(D, e2);
+        const float det = dot(e1, P);
+        const float inv = recip_det(det);
+        const float u = dot(Sv, P) * inv;
+        const float v = dot(D, Q) * inv;
+        const float t = d.x * inv;
+        const bool ok = !(fabsf(det) < kEps) & !((u < 0) | (u > 1)) & !((v < 0) | (u + v > 1));
+        take_min(ok, t, __float_as_int(d.y), bt, bi);
+    }
+    for (int k = 0; k < S.n_plane; ++k) {
+        const float4 a = S.plane[2 * k], b = S.plane[2 * k + 1];
+        float t;
+        const bool ok = hit_plane(make_float4(0.f, a.x, a.y, a.z), make_float4(a.w, 0.f, 0.f, 0.f), O, D, t);
+        take_min(ok, t, __float_as_int(b.x), bt, bi);
+    }
+    for (int k = 0; k < S.n_quad; ++k) {
+        const float4* r = S.quad + 3 * k;
+        const float4 a = r[0], b = r[1], c = r[2];
+        float t;
+        const bool ok = hit_quadric(make_float4(0.f, a.x, a.y, a.z), make_float4(a.w, b.x, b.y, b.z),
+                                    make_float4(b.w, c.x, c.y, 0.f), O, D, t);
+        take_min(ok, t, __float_as_int(c.z), bt, bi);
+    }
+    best_t = bt;
+    return bi;
+}
+
+// tricam[] for camera position C (one thread per triangle).
+__global__ void rt_camera_prepass(const float4* __restrict__ tri, int n, float cx, float cy, float cz,
+                                  float4* __restrict__ tricam)
+{
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const float4 a = tri[3 * k], b = tri[3 * k + 1], c = tri[3 * k + 2];
+    const Vec3 p0 = make3(a.x, a.y, a.z), e1 = make3(a.w, b.x, b.y), e2 = make3(b.z, b.w, c.x);
+    const Vec3 Sv = make3(cx, cy, cz) - p0;
+    const Vec3 Q = cross(Sv, e1);
+    const float tq = dot(e2, Q);
+    float4* o = tricam + 4 * k;
+    o[0] = make_float4(e1.x, e1.y, e1.z, e2.x);
+    o[1] = make_float4(e2.y, e2.z, Sv.x, Sv.y);
+    o[2] = make_float4(Sv.z, Q.x, Q.y, Q.z);
+    o[3] = make_float4(tq, c.y, 0.f, 0.f);
 }
 
 __device__ __forceinline__ Vec3 hit_normal(const SceneDev& S, int idx, const Vec3 O, const Vec3 D, float t)
@@ -436,7 +505,7 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
     const Color bg{F.bg[0], F.bg[1], F.bg[2]};
     if constexpr (MAXD == 0) {
         float t;
-        const int idx = closest_hit(S, O, D, t);
+        const int idx = closest_hit_camera(S, O, D, t);
         if (idx < 0) return bg;
         const Vec3 N = hit_normal(S, idx, O, D, t);
         const Mat m = load_mat(S, idx);
@@ -447,11 +516,12 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
         int sp = 0;
         float rior = 1.0f, energy = 1.0f;
         Color ret{0.f, 0.f, 0.f};
-        bool trace = true;
+        bool trace = true, camera_ray = true;
         for (;;) {
             if (trace) {
                 float t;
-                const int idx = closest_hit(S, O, D, t);
+                const int idx = camera_ray ? closest_hit_camera(S, O, D, t) : closest_hit(S, O, D, t);
+                camera_ray = false;
                 ret = bg;
                 if (idx >= 0) {
                     const Vec3 N = hit_normal(S, idx, O, D, t);
@@ -596,6 +666,9 @@ struct rt_ctx {
     float4* d_plane = nullptr;
     float4* d_quad = nullptr;
     int* d_translucent = nullptr;
+    float4* d_tricam = nullptr;
+    float cam_key[3] = {0.f, 0.f, 0.f};
+    bool cam_valid = false;
     StatsDev* d_stats = nullptr;
     void* d_scratch = nullptr;  // staging for host outputs
     size_t scratch_bytes = 0;
@@ -660,6 +733,7 @@ RT_EXPORT void rt_destroy(rt_ctx* c)
     hipFree(c->d_plane);
     hipFree(c->d_quad);
     hipFree(c->d_translucent);
+    hipFree(c->d_tricam);
     hipFree(c->d_stats);
     hipFree(c->d_scratch);
     if (c->ev0) hipEventDestroy(c->ev0);
@@ -766,6 +840,9 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
     hipFree(c->d_plane);
     hipFree(c->d_quad);
     hipFree(c->d_translucent);
+    hipFree(c->d_tricam);
+    c->d_tricam = nullptr;
+    c->cam_valid = false;
     c->d_geom = c->d_mat = c->d_lights = c->d_tri = c->d_plane = c->d_quad = nullptr;
     c->d_translucent = nullptr;
     c->uploaded = false;
@@ -778,6 +855,7 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
     HIP_TRY(c, up((void**)&c->d_plane, pla.data(), pla.size() * sizeof(float)));
     HIP_TRY(c, up((void**)&c->d_quad, qua.data(), qua.size() * sizeof(float)));
     HIP_TRY(c, up((void**)&c->d_translucent, translucent.data(), translucent.size() * sizeof(int)));
+    HIP_TRY(c, hipMalloc((void**)&c->d_tricam, (tri.size() / 12) * 16 * sizeof(float)));
     HIP_TRY(c, hipMalloc(&c->d_geom, geom.size() * sizeof(float)));
     HIP_TRY(c, hipMalloc(&c->d_mat, mat.size() * sizeof(float)));
     HIP_TRY(c, hipMalloc(&c->d_lights, lig.size() * sizeof(float)));
@@ -853,7 +931,7 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
         c->err = "reachable bounce depth " + std::to_string(depth) + " exceeds the compiled stack (32)";
         return RT_E_UNSUPPORTED;
     }
-    SceneDev S{c->d_geom, c->d_mat, c->d_lights, c->d_tri, c->d_plane, c->d_quad, c->d_translucent,
+    SceneDev S{c->d_geom, c->d_mat, c->d_lights, c->d_tri, c->d_plane, c->d_quad, c->d_translucent, c->d_tricam,
                c->n_surf, c->n_lights, c->n_tri, c->n_plane, c->n_quad,
                c->n_tri_opaque, c->n_plane_opaque, c->n_quad_opaque, c->n_translucent, c->shadow_split};
     FrameDev F;
@@ -877,6 +955,15 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
     c->last.stack_depth = cap;
     if (rows == 0) return RT_OK;
     if (f->flags & RT_FLAG_STATS) HIP_TRY(c, hipMemsetAsync(c->d_stats, 0, sizeof(StatsDev), st));
+    // Camera-ray triangle values: recomputed only when the camera moves.
+    if (c->n_tri > 0 && (!c->cam_valid || std::memcmp(c->cam_key, f->cam_pos, sizeof c->cam_key) != 0)) {
+        const float* cp = f->cam_pos;
+        hipLaunchKernelGGL(rt_camera_prepass, dim3((c->n_tri + 255) / 256), dim3(256), 0, st, c->d_tri, c->n_tri,
+                           cp[0], cp[1], cp[2], c->d_tricam);
+        HIP_TRY(c, hipGetLastError());
+        std::memcpy(c->cam_key, f->cam_pos, sizeof c->cam_key);
+        c->cam_valid = true;
+    }
     dim3 grid((f->width + 15) / 16, (rows + 15) / 16);
     if (timed) HIP_TRY(c, hipEventRecord(c->ev0, st));
     StatsDev* stats = c->d_stats;
