@@ -77,6 +77,10 @@ struct SceneDev {
     // Triangle.cpp:139-160 computes for a ray whose origin is C, so they are
     // computed once per camera instead of once per pixel.
     const float4* __restrict__ tricam;
+    // Camera records are 64 B (vs 40 B); while the triangle list fits the
+    // scalar cache they win (C2: -3%), past it the extra misses lose (C3: +10%,
+    // tools/ab_variants.py), so the host enables them for small lists only.
+    int use_tricam;
     int n_surf, n_lights;
     int n_tri, n_plane, n_quad;
     int n_tri_opaque, n_plane_opaque, n_quad_opaque;
@@ -308,23 +312,49 @@ __device__ __forceinline__ int closest_hit(const SceneDev& S, const Vec3 O, cons
 
 // Closest hit for camera rays (origin = the camera for every lane): the
 // per-triangle values that depend only on the origin come from tricam[].
+#ifndef RT_GROUP
+#define RT_GROUP 4
+#endif
+
+// One camera-ray triangle test: exact u first, the rest only if some lane of
+// the wave is inside the u bounds.
+__device__ __forceinline__ void camera_tri(const float4 a, const float4 b, const float4 c, const float4 d,
+                                           const Vec3 D, float& bt, int& bi)
+{
+    const Vec3 e1 = make3(a.x, a.y, a.z), e2 = make3(a.w, b.x, b.y);
+    const Vec3 Sv = make3(b.z, b.w, c.x), Q = make3(c.y, c.z, c.w);
+    const Vec3 P = cross(D, e2);
+    const float det = dot(e1, P);
+    const float inv = recip_det(det);
+    const float u = dot(Sv, P) * inv;
+    const bool okU = !(fabsf(det) < kEps) & !((u < 0) | (u > 1));
+    if (!__any(okU)) return;
+    const float v = dot(D, Q) * inv;
+    const float t = d.x * inv;
+    take_min(okU & !((v < 0) | (u + v > 1)), t, __float_as_int(d.y), bt, bi);
+}
+
+// Closest hit for camera rays (origin = the camera for every lane): the
+// per-triangle values that depend only on the origin come from tricam[].
+// Records are fetched RT_GROUP at a time so the scalar loads of a group are
+// all in flight before its first test.
 __device__ __forceinline__ int closest_hit_camera(const SceneDev& S, const Vec3 O, const Vec3 D, float& best_t)
 {
     float bt = -1.0f;
     int bi = -1;
-    for (int k = 0; k < S.n_tri; ++k) {
+    int k = 0;
+    for (; k + RT_GROUP <= S.n_tri; k += RT_GROUP) {
+        float4 rec[RT_GROUP][4];
+#pragma unroll
+        for (int g = 0; g < RT_GROUP; ++g)
+#pragma unroll
+            for (int w = 0; w < 4; ++w) rec[g][w] = S.tricam[4 * (k + g) + w];
+#pragma unroll
+        for (int g = 0; g < RT_GROUP; ++g) camera_tri(rec[g][0], rec[g][1], rec[g][2], rec[g][3], D, bt, bi);
+    }
+    for (; k < S.n_tri; ++k) {
         const float4* r = S.tricam + 4 * k;
-        const float4 a = r[0], b = r[1], c = r[2], d = r[3];
-        const Vec3 e1 = make3(a.x, a.y, a.z), e2 = make3(a.w, b.x, b.y);
-        const Vec3 Sv = make3(b.z, b.w, c.x), Q = make3(c.y, c.z, c.w);
-        const Vec3 P = cross(D, e2);
-        const float det = dot(e1, P);
-        const float inv = recip_det(det);
-        const float u = dot(Sv, P) * inv;
-        const float v = dot(D, Q) * inv;
-        const float t = d.x * inv;
-        const bool ok = !(fabsf(det) < kEps) & !((u < 0) | (u > 1)) & !((v < 0) | (u + v > 1));
-        take_min(ok, t, __float_as_int(d.y), bt, bi);
+        camera_tri(r[0], r[1], r[2], r[3], D, bt, bi);
     }
     for (int k = 0; k < S.n_plane; ++k) {
         const float4 a = S.plane[2 * k], b = S.plane[2 * k + 1];
@@ -505,7 +535,7 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
     const Color bg{F.bg[0], F.bg[1], F.bg[2]};
     if constexpr (MAXD == 0) {
         float t;
-        const int idx = closest_hit_camera(S, O, D, t);
+        const int idx = S.use_tricam ? closest_hit_camera(S, O, D, t) : closest_hit(S, O, D, t);
         if (idx < 0) return bg;
         const Vec3 N = hit_normal(S, idx, O, D, t);
         const Mat m = load_mat(S, idx);
@@ -520,7 +550,7 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
         for (;;) {
             if (trace) {
                 float t;
-                const int idx = camera_ray ? closest_hit_camera(S, O, D, t) : closest_hit(S, O, D, t);
+                const int idx = (camera_ray && S.use_tricam) ? closest_hit_camera(S, O, D, t) : closest_hit(S, O, D, t);
                 camera_ray = false;
                 ret = bg;
                 if (idx >= 0) {
@@ -897,6 +927,9 @@ static int reachable_depth(const rt_ctx* c, const rt_frame* f)
     return levels;
 }
 
+// 256 camera records = 16 KB, the scalar data cache.
+static constexpr int kTricamMaxTriangles = 256;
+
 typedef void (*kernel_fn)(const SceneDev, const FrameDev, unsigned*, float*, StatsDev*);
 
 static kernel_fn pick_kernel(int depth, int& cap)
@@ -931,8 +964,9 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
         c->err = "reachable bounce depth " + std::to_string(depth) + " exceeds the compiled stack (32)";
         return RT_E_UNSUPPORTED;
     }
+    const int use_tricam = c->n_tri > 0 && c->n_tri <= kTricamMaxTriangles;
     SceneDev S{c->d_geom, c->d_mat, c->d_lights, c->d_tri, c->d_plane, c->d_quad, c->d_translucent, c->d_tricam,
-               c->n_surf, c->n_lights, c->n_tri, c->n_plane, c->n_quad,
+               use_tricam, c->n_surf, c->n_lights, c->n_tri, c->n_plane, c->n_quad,
                c->n_tri_opaque, c->n_plane_opaque, c->n_quad_opaque, c->n_translucent, c->shadow_split};
     FrameDev F;
     std::memcpy(F.cam, f->cam_pos, sizeof F.cam);
@@ -956,7 +990,7 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
     if (rows == 0) return RT_OK;
     if (f->flags & RT_FLAG_STATS) HIP_TRY(c, hipMemsetAsync(c->d_stats, 0, sizeof(StatsDev), st));
     // Camera-ray triangle values: recomputed only when the camera moves.
-    if (c->n_tri > 0 && (!c->cam_valid || std::memcmp(c->cam_key, f->cam_pos, sizeof c->cam_key) != 0)) {
+    if (use_tricam && (!c->cam_valid || std::memcmp(c->cam_key, f->cam_pos, sizeof c->cam_key) != 0)) {
         const float* cp = f->cam_pos;
         hipLaunchKernelGGL(rt_camera_prepass, dim3((c->n_tri + 255) / 256), dim3(256), 0, st, c->d_tri, c->n_tri,
                            cp[0], cp[1], cp[2], c->d_tricam);
