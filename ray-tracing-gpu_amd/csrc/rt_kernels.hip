@@ -81,6 +81,14 @@ struct SceneDev {
     // scalar cache they win (C2: -3%), past it the extra misses lose (C3: +10%,
     // tools/ab_variants.py), so the host enables them for small lists only.
     int use_tricam;
+    // Bounding-cone culling (exact: it only skips triangles no lane's ray can
+    // reach).  Per (apex, triangle), 2 float4: [dir-to-sphere-centre, cosT]
+    // [distance from the apex to the sphere, 1/that, 0, 0], where the sphere
+    // bounds the triangle (inflated for float slop) and cosT is the cosine of
+    // the half-angle it subtends from the apex minus a margin.  Apex = the
+    // camera (cone_cam) or light l (cone_light + 2*n_tri*l).
+    const float4* __restrict__ cone_cam;
+    const float4* __restrict__ cone_light;
     int n_surf, n_lights;
     int n_tri, n_plane, n_quad;
     int n_tri_opaque, n_plane_opaque, n_quad_opaque;
@@ -278,12 +286,17 @@ __device__ __forceinline__ TriRec load_tri(const SceneDev& S, int k)
 
 // Scene.cpp:1705-1715: closest hit over every surface.  Returns the winning
 // FILE index (-1 = miss) and its distance.
+template <bool CAMERA>
 __device__ __forceinline__ int closest_hit(const SceneDev& S, const Vec3 O, const Vec3 D, float& best_t)
 {
     float bt = -1.0f;
     int bi = -1;
     RT_UNROLL(RT_TRI_UNROLL)
     for (int k = 0; k < S.n_tri; ++k) {
+        if constexpr (CAMERA) {  // rays from the camera: skip triangles outside every lane's cone
+            const float4 c = S.cone_cam[2 * k];
+            if (!__any(dot(D, make3(c.x, c.y, c.z)) >= c.w)) continue;
+        }
         const TriRec tr = load_tri(S, k);
         const TriU r = tri_u(tr.p0, tr.e1, tr.e2, O, D);
         if (!__any(r.ok)) continue;
@@ -343,16 +356,9 @@ __device__ __forceinline__ int closest_hit_camera(const SceneDev& S, const Vec3 
     float bt = -1.0f;
     int bi = -1;
     int k = 0;
-    for (; k + RT_GROUP <= S.n_tri; k += RT_GROUP) {
-        float4 rec[RT_GROUP][4];
-#pragma unroll
-        for (int g = 0; g < RT_GROUP; ++g)
-#pragma unroll
-            for (int w = 0; w < 4; ++w) rec[g][w] = S.tricam[4 * (k + g) + w];
-#pragma unroll
-        for (int g = 0; g < RT_GROUP; ++g) camera_tri(rec[g][0], rec[g][1], rec[g][2], rec[g][3], D, bt, bi);
-    }
     for (; k < S.n_tri; ++k) {
+        const float4 cc = S.cone_cam[2 * k];
+        if (!__any(dot(D, make3(cc.x, cc.y, cc.z)) >= cc.w)) continue;
         const float4* r = S.tricam + 4 * k;
         camera_tri(r[0], r[1], r[2], r[3], D, bt, bi);
     }
@@ -392,6 +398,32 @@ __global__ void rt_camera_prepass(const float4* __restrict__ tri, int n, float c
     o[3] = make_float4(tq, c.y, 0.f, 0.f);
 }
 
+// Cone records for apex A (one thread per triangle).  sph = bounding sphere
+// (centre, radius already inflated on the host).  Margins: the radius grows
+// by 2e-5 of the apex distance and the cosine threshold drops by 2e-5 — both
+// far above the float rounding of this test (~1e-7), so a triangle is only
+// skipped when no float ray from A could reach its sphere.
+__global__ void rt_cone_prepass(const float4* __restrict__ sph, int n, float ax, float ay, float az,
+                                float4* __restrict__ out)
+{
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const float4 s = sph[k];
+    const Vec3 v = make3(s.x - ax, s.y - ay, s.z - az);
+    const float dv = norm(v);
+    const float r = s.w + 2e-5f * dv;
+    float4 c0 = make_float4(0.f, 0.f, 0.f, -2.0f), c1 = make_float4(-INFINITY, 0.f, 0.f, 0.f);
+    if (dv > r && isfinite(dv) && isfinite(r)) {  // apex outside the sphere
+        const float inv = 1.0f / dv;
+        const float sn = r * inv;
+        const float dmin = (dv - r) * (1.0f - 1e-5f);
+        c0 = make_float4(v.x * inv, v.y * inv, v.z * inv, sqrtf(1.0f - sn * sn) - 2e-5f);
+        c1 = make_float4(dmin, 2.0f / dmin, 0.f, 0.f);
+    }
+    out[2 * k] = c0;
+    out[2 * k + 1] = c1;
+}
+
 __device__ __forceinline__ Vec3 hit_normal(const SceneDev& S, int idx, const Vec3 O, const Vec3 D, float t)
 {
     const float4* rec = S.geom + 4 * idx;
@@ -429,7 +461,7 @@ __device__ __forceinline__ bool shadow_hit_record(const float4* rec, const Vec3 
 
 // Scene.cpp:1842-1861 ObtenirFiltreDeSurface.  L is the UNNORMALISED light
 // vector; it is normalised here exactly like the reference (in place).
-__device__ __forceinline__ Color shadow_filter(const SceneDev& S, const Vec3 P, Vec3& L,
+__device__ __forceinline__ Color shadow_filter(const SceneDev& S, int light, const Vec3 P, Vec3& L,
                                                unsigned& skipped)
 {
     Color F{1.0f, 1.0f, 1.0f};
@@ -447,9 +479,17 @@ __device__ __forceinline__ Color shadow_filter(const SceneDev& S, const Vec3 P, 
     // counting once occluded; the wave leaves a loop once all lanes are.
     bool occluded = false;
     int done = 0, total = S.n_tri_opaque + S.n_plane_opaque + S.n_quad_opaque;
+    const float4* cone = S.cone_light + 2 * (size_t)S.n_tri * light;
+    // The float ray P + t*L (L normalised, |L - exact| <= ~6 ulp) can stray
+    // from the exact segment to the light by <= dist * 1e-6 at distance
+    // >= cone.y from the light: widen each lane's cone by that angle.
+    const float slack = dist * 1e-6f;
     for (int k = 0; k < S.n_tri_opaque; ++k) {
         if (!__any(!occluded)) break;
         ++done;
+        const float4 c0 = cone[2 * k], c1 = cone[2 * k + 1];
+        const bool reach = !occluded & (c1.x < dist) & (-dot(L, make3(c0.x, c0.y, c0.z)) >= c0.w - slack * c1.y);
+        if (!__any(reach)) continue;
         const TriRec tr = load_tri(S, k);
         const TriU r = tri_u(tr.p0, tr.e1, tr.e2, P, L);
         if (!__any(r.ok && !occluded)) continue;
@@ -501,7 +541,12 @@ __device__ __forceinline__ Color shade_local(const SceneDev& S, const Mat& m, co
         Vec3 L = make3(l0.x, l0.y, l0.z) - P;
         if (dot(L, N) > 0) {
             ++cnt.shadow;
-            const Color F = shadow_filter(S, P, L, cnt.skipped);
+#ifdef RT_ABLATE_SHADOW  // timing-only build: no shadow rays
+            L = div_recip(L, norm(L));
+            const Color F{1.f, 1.f, 1.f};
+#else
+            const Color F = shadow_filter(S, li, P, L, cnt.skipped);
+#endif
             const Color LC = Color{l1.x, l1.y, l1.z} * F;
             const float g = l0.w * m.kd * dot(N, L);
             res += (m.color * g) * LC;
@@ -534,9 +579,15 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
 {
     const Color bg{F.bg[0], F.bg[1], F.bg[2]};
     if constexpr (MAXD == 0) {
+#ifdef RT_ABLATE_ALL  // timing-only build: ray set-up and store only
+        return Color{D.x, D.y, D.z};
+#endif
         float t;
-        const int idx = S.use_tricam ? closest_hit_camera(S, O, D, t) : closest_hit(S, O, D, t);
+        const int idx = S.use_tricam ? closest_hit_camera(S, O, D, t) : closest_hit<true>(S, O, D, t);
         if (idx < 0) return bg;
+#ifdef RT_ABLATE_SHADE  // timing-only build: primary closest hit only
+        return Color{t, (float)idx, 0.f};
+#endif
         const Vec3 N = hit_normal(S, idx, O, D, t);
         const Mat m = load_mat(S, idx);
         const Vec3 P = O + t * D;
@@ -550,7 +601,8 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
         for (;;) {
             if (trace) {
                 float t;
-                const int idx = (camera_ray && S.use_tricam) ? closest_hit_camera(S, O, D, t) : closest_hit(S, O, D, t);
+                const int idx = camera_ray ? (S.use_tricam ? closest_hit_camera(S, O, D, t) : closest_hit<true>(S, O, D, t))
+                                           : closest_hit<false>(S, O, D, t);
                 camera_ray = false;
                 ret = bg;
                 if (idx >= 0) {
@@ -697,6 +749,9 @@ struct rt_ctx {
     float4* d_quad = nullptr;
     int* d_translucent = nullptr;
     float4* d_tricam = nullptr;
+    float4* d_trisph = nullptr;
+    float4* d_cone_cam = nullptr;
+    float4* d_cone_light = nullptr;
     float cam_key[3] = {0.f, 0.f, 0.f};
     bool cam_valid = false;
     StatsDev* d_stats = nullptr;
@@ -764,6 +819,9 @@ RT_EXPORT void rt_destroy(rt_ctx* c)
     hipFree(c->d_quad);
     hipFree(c->d_translucent);
     hipFree(c->d_tricam);
+    hipFree(c->d_trisph);
+    hipFree(c->d_cone_cam);
+    hipFree(c->d_cone_light);
     hipFree(c->d_stats);
     hipFree(c->d_scratch);
     if (c->ev0) hipEventDestroy(c->ev0);
@@ -871,7 +929,10 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
     hipFree(c->d_quad);
     hipFree(c->d_translucent);
     hipFree(c->d_tricam);
-    c->d_tricam = nullptr;
+    hipFree(c->d_trisph);
+    hipFree(c->d_cone_cam);
+    hipFree(c->d_cone_light);
+    c->d_tricam = c->d_trisph = c->d_cone_cam = c->d_cone_light = nullptr;
     c->cam_valid = false;
     c->d_geom = c->d_mat = c->d_lights = c->d_tri = c->d_plane = c->d_quad = nullptr;
     c->d_translucent = nullptr;
@@ -886,6 +947,44 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
     HIP_TRY(c, up((void**)&c->d_quad, qua.data(), qua.size() * sizeof(float)));
     HIP_TRY(c, up((void**)&c->d_translucent, translucent.data(), translucent.size() * sizeof(int)));
     HIP_TRY(c, hipMalloc((void**)&c->d_tricam, (tri.size() / 12) * 16 * sizeof(float)));
+    // Bounding sphere per triangle (tri[] order), in double, inflated by a
+    // relative 1e-4 of the radius and of the coordinates' magnitude so the
+    // float triangle test's rounding slop near an edge stays inside it.
+    const size_t ntr = tri.size() / 12;
+    std::vector<float> sph(ntr * 4);
+    for (size_t k = 0; k < ntr; ++k) {
+        const float* r = &tri[12 * k];
+        double p[3][3];
+        for (int a = 0; a < 3; ++a) {
+            p[0][a] = r[a];
+            p[1][a] = (double)r[a] + (double)r[3 + a];
+            p[2][a] = (double)r[a] + (double)r[6 + a];
+        }
+        double ctr[3], rad = 0, mag = 0;
+        for (int a = 0; a < 3; ++a) ctr[a] = (p[0][a] + p[1][a] + p[2][a]) / 3.0;
+        for (int q = 0; q < 3; ++q) {
+            double d2 = 0;
+            for (int a = 0; a < 3; ++a) {
+                d2 += (p[q][a] - ctr[a]) * (p[q][a] - ctr[a]);
+                mag = std::max(mag, std::fabs(p[q][a]));
+            }
+            rad = std::max(rad, std::sqrt(d2));
+        }
+        const double infl = rad * (1.0 + 1e-4) + 1e-4 * mag + 1e-6;
+        for (int a = 0; a < 3; ++a) sph[4 * k + a] = (float)ctr[a];
+        sph[4 * k + 3] = (float)(infl * (1.0 + 1e-6));  // round up
+    }
+    sph.resize(std::max<size_t>(sph.size(), 4));
+    HIP_TRY(c, up((void**)&c->d_trisph, sph.data(), sph.size() * sizeof(float)));
+    HIP_TRY(c, hipMalloc((void**)&c->d_cone_cam, std::max<size_t>(ntr, 1) * 2 * sizeof(float4)));
+    HIP_TRY(c, hipMalloc((void**)&c->d_cone_light, std::max<size_t>(ntr * nl, 1) * 2 * sizeof(float4)));
+    for (int j = 0; j < nl && ntr > 0; ++j) {
+        const float* l = s->lights + 7 * (size_t)j;
+        hipLaunchKernelGGL(rt_cone_prepass, dim3((unsigned)((ntr + 255) / 256)), dim3(256), 0, 0, c->d_trisph,
+                           (int)ntr, l[0], l[1], l[2], c->d_cone_light + 2 * ntr * j);
+        HIP_TRY(c, hipGetLastError());
+    }
+    HIP_TRY(c, hipDeviceSynchronize());
     HIP_TRY(c, hipMalloc(&c->d_geom, geom.size() * sizeof(float)));
     HIP_TRY(c, hipMalloc(&c->d_mat, mat.size() * sizeof(float)));
     HIP_TRY(c, hipMalloc(&c->d_lights, lig.size() * sizeof(float)));
@@ -966,7 +1065,7 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
     }
     const int use_tricam = c->n_tri > 0 && c->n_tri <= kTricamMaxTriangles;
     SceneDev S{c->d_geom, c->d_mat, c->d_lights, c->d_tri, c->d_plane, c->d_quad, c->d_translucent, c->d_tricam,
-               use_tricam, c->n_surf, c->n_lights, c->n_tri, c->n_plane, c->n_quad,
+               use_tricam, c->d_cone_cam, c->d_cone_light, c->n_surf, c->n_lights, c->n_tri, c->n_plane, c->n_quad,
                c->n_tri_opaque, c->n_plane_opaque, c->n_quad_opaque, c->n_translucent, c->shadow_split};
     FrameDev F;
     std::memcpy(F.cam, f->cam_pos, sizeof F.cam);
@@ -990,10 +1089,15 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
     if (rows == 0) return RT_OK;
     if (f->flags & RT_FLAG_STATS) HIP_TRY(c, hipMemsetAsync(c->d_stats, 0, sizeof(StatsDev), st));
     // Camera-ray triangle values: recomputed only when the camera moves.
-    if (use_tricam && (!c->cam_valid || std::memcmp(c->cam_key, f->cam_pos, sizeof c->cam_key) != 0)) {
+    if (c->n_tri > 0 && (!c->cam_valid || std::memcmp(c->cam_key, f->cam_pos, sizeof c->cam_key) != 0)) {
         const float* cp = f->cam_pos;
-        hipLaunchKernelGGL(rt_camera_prepass, dim3((c->n_tri + 255) / 256), dim3(256), 0, st, c->d_tri, c->n_tri,
-                           cp[0], cp[1], cp[2], c->d_tricam);
+        if (use_tricam) {
+            hipLaunchKernelGGL(rt_camera_prepass, dim3((c->n_tri + 255) / 256), dim3(256), 0, st, c->d_tri, c->n_tri,
+                               cp[0], cp[1], cp[2], c->d_tricam);
+            HIP_TRY(c, hipGetLastError());
+        }
+        hipLaunchKernelGGL(rt_cone_prepass, dim3((c->n_tri + 255) / 256), dim3(256), 0, st, c->d_trisph, c->n_tri,
+                           cp[0], cp[1], cp[2], c->d_cone_cam);
         HIP_TRY(c, hipGetLastError());
         std::memcpy(c->cam_key, f->cam_pos, sizeof c->cam_key);
         c->cam_valid = true;
