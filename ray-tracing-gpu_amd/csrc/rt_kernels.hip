@@ -532,33 +532,160 @@ struct Counters {
 
 // Scene.cpp:1742-1777: ambient + every light (N.L gate on the unnormalised
 // light vector, filter, Lambert "Gouraud" term, Phong term).
+// Shadow rays of up to LB lights from the same point P, against the OPAQUE
+// surfaces, in one pass over the surface list (shadow_split scenes only).
+// Each light's any-hit result is exactly the per-light loop's; sharing the
+// pass shares the record loads, the loop overhead and the light-independent
+// part of the triangle test (S = P - p0, Q = S x e1, e2 . Q — the same
+// values Triangle.cpp:143-158 computes for every light's ray from P).
+#ifndef RT_LIGHT_BATCH
+#define RT_LIGHT_BATCH 4
+#endif
+constexpr int kLightBatch = RT_LIGHT_BATCH;
+
+__device__ __forceinline__ void shadow_opaque_batch(const SceneDev& S, int l0, int nl, const Vec3 P,
+                                                    const Vec3 (&L)[kLightBatch], const float (&dist)[kLightBatch],
+                                                    bool (&occ)[kLightBatch])
+{
+    const float4* cone = S.cone_light + 2 * (size_t)S.n_tri * l0;
+    const size_t cstride = 2 * (size_t)S.n_tri;
+    float slack[kLightBatch];
+#pragma unroll
+    for (int j = 0; j < kLightBatch; ++j) slack[j] = dist[j] * 1e-6f;
+    for (int k = 0; k < S.n_tri_opaque; ++k) {
+        bool live = false;
+#pragma unroll
+        for (int j = 0; j < kLightBatch; ++j) live |= (j < nl) & !occ[j];
+        if (!__any(live)) break;
+        bool reach[kLightBatch];
+        bool any_reach = false;
+#pragma unroll
+        for (int j = 0; j < kLightBatch; ++j) {
+            reach[j] = false;
+            if (j < nl) {
+                const float4 c0 = cone[cstride * j + 2 * k], c1 = cone[cstride * j + 2 * k + 1];
+                reach[j] = !occ[j] & (c1.x < dist[j]) &
+                           (-dot(L[j], make3(c0.x, c0.y, c0.z)) >= c0.w - slack[j] * c1.y);
+                any_reach |= reach[j];
+            }
+        }
+        if (!__any(any_reach)) continue;
+        const TriRec tr = load_tri(S, k);
+        const Vec3 Sv = P - tr.p0;
+        const Vec3 Q = cross(Sv, tr.e1);
+        const float tq = dot(tr.e2, Q);
+#pragma unroll
+        for (int j = 0; j < kLightBatch; ++j) {
+            if (j < nl && __any(reach[j])) {
+                const Vec3 Pv = cross(L[j], tr.e2);
+                const float det = dot(tr.e1, Pv);
+                const float inv = recip_det(det);
+                const float u = dot(Sv, Pv) * inv;
+                const float v = dot(L[j], Q) * inv;
+                const float t = tq * inv;
+                const bool ok = !(fabsf(det) < kEps) & !((u < 0) | (u > 1)) & !((v < 0) | (u + v > 1));
+                occ[j] |= ok & (t > kEps) & (t < dist[j]);
+            }
+        }
+    }
+    for (int k = 0; k < S.n_plane_opaque; ++k) {
+        const float4 a = S.plane[2 * k];
+#pragma unroll
+        for (int j = 0; j < kLightBatch; ++j) {
+            if (j < nl && __any(!occ[j])) {
+                float t;
+                const bool ok = hit_plane(make_float4(0.f, a.x, a.y, a.z), make_float4(a.w, 0.f, 0.f, 0.f), P, L[j], t);
+                occ[j] |= ok & (t > kEps) & (t < dist[j]);
+            }
+        }
+    }
+    for (int k = 0; k < S.n_quad_opaque; ++k) {
+        const float4* r = S.quad + 3 * k;
+        const float4 a = r[0], b = r[1], c = r[2];
+#pragma unroll
+        for (int j = 0; j < kLightBatch; ++j) {
+            if (j < nl && __any(!occ[j])) {
+                float t;
+                const bool ok = hit_quadric(make_float4(0.f, a.x, a.y, a.z), make_float4(a.w, b.x, b.y, b.z),
+                                            make_float4(b.w, c.x, c.y, 0.f), P, L[j], t);
+                occ[j] |= ok & (t > kEps) & (t < dist[j]);
+            }
+        }
+    }
+}
+
+// Scene.cpp:1742-1777: ambient + every light (N.L gate on the unnormalised
+// light vector, filter, Lambert "Gouraud" term, Phong term).  Lights are
+// accumulated strictly in file order; only the filters of a batch of lights
+// are computed ahead (they do not depend on the colour being accumulated).
+__device__ __forceinline__ void add_light(Color& res, const Mat& m, const float4 l0, const float4 l1, const Vec3 N,
+                                          const Vec3 L, const Vec3 D, const Color F)
+{
+    const Color LC = Color{l1.x, l1.y, l1.z} * F;
+    const float g = l0.w * m.kd * dot(N, L);
+    res += (m.color * g) * LC;
+    const Vec3 rf = reflect(L, N);
+    const float ps = dot(rf, D);
+    if (ps > 0) {
+        // pow(x, 0) == 1 for every x (C99 F.9.4.4, glibc and ocml alike):
+        // materials without a shininess never pay for powf.
+        float pw = 1.0f;
+        if (m.shin != 0.0f) pw = powf(ps, m.shin);
+        const float pf = l0.w * m.ks * pw;
+        res += LC * pf;
+    }
+}
+
 __device__ __forceinline__ Color shade_local(const SceneDev& S, const Mat& m, const Vec3 P, const Vec3 N,
                                              const Vec3 D, Counters& cnt)
 {
     Color res = m.color * m.ka;
-    for (int li = 0; li < S.n_lights; ++li) {
-        const float4 l0 = S.lights[2 * li], l1 = S.lights[2 * li + 1];
-        Vec3 L = make3(l0.x, l0.y, l0.z) - P;
-        if (dot(L, N) > 0) {
-            ++cnt.shadow;
-#ifdef RT_ABLATE_SHADOW  // timing-only build: no shadow rays
-            L = div_recip(L, norm(L));
-            const Color F{1.f, 1.f, 1.f};
-#else
-            const Color F = shadow_filter(S, li, P, L, cnt.skipped);
-#endif
-            const Color LC = Color{l1.x, l1.y, l1.z} * F;
-            const float g = l0.w * m.kd * dot(N, L);
-            res += (m.color * g) * LC;
-            const Vec3 rf = reflect(L, N);
-            const float ps = dot(rf, D);
-            if (ps > 0) {
-                // pow(x, 0) == 1 for every x (C99 F.9.4.4, glibc and ocml alike):
-                // materials without a shininess never pay for powf.
-                float pw = 1.0f;
-                if (m.shin != 0.0f) pw = powf(ps, m.shin);
-                const float pf = l0.w * m.ks * pw;
-                res += LC * pf;
+    if (!S.shadow_split) {
+        for (int li = 0; li < S.n_lights; ++li) {
+            const float4 l0 = S.lights[2 * li], l1 = S.lights[2 * li + 1];
+            Vec3 L = make3(l0.x, l0.y, l0.z) - P;
+            if (dot(L, N) > 0) {
+                ++cnt.shadow;
+                const Color F = shadow_filter(S, li, P, L, cnt.skipped);
+                add_light(res, m, l0, l1, N, L, D, F);
+            }
+        }
+        return res;
+    }
+    for (int lb = 0; lb < S.n_lights; lb += kLightBatch) {
+        const int nl = S.n_lights - lb < kLightBatch ? S.n_lights - lb : kLightBatch;
+        Vec3 L[kLightBatch];
+        float dist[kLightBatch];
+        bool gate[kLightBatch], occ[kLightBatch];
+#pragma unroll
+        for (int j = 0; j < kLightBatch; ++j) {
+            gate[j] = false;
+            dist[j] = 0.0f;
+            L[j] = make3(0.f, 0.f, 0.f);
+            if (j < nl) {
+                const float4 l0 = S.lights[2 * (lb + j)];
+                const Vec3 Lr = make3(l0.x, l0.y, l0.z) - P;
+                gate[j] = dot(Lr, N) > 0;          // Scene.cpp:1756, unnormalised
+                dist[j] = norm(Lr);                // Scene.cpp:1847-1848
+                L[j] = div_recip(Lr, dist[j]);
+                cnt.shadow += gate[j];
+            }
+            occ[j] = !gate[j];
+        }
+        shadow_opaque_batch(S, lb, nl, P, L, dist, occ);
+#pragma unroll
+        for (int j = 0; j < kLightBatch; ++j) {
+            if (j < nl && gate[j]) {
+                const float4 l0 = S.lights[2 * (lb + j)], l1 = S.lights[2 * (lb + j) + 1];
+                Color F{0.0f, 0.0f, 0.0f};
+                if (!occ[j]) {  // translucent surfaces, file order
+                    F = Color{1.0f, 1.0f, 1.0f};
+                    for (int q = 0; q < S.n_translucent; ++q) {
+                        Color fc;
+                        if (shadow_hit_record(S.geom + 4 * S.translucent[q], P, L[j], dist[j], fc)) F *= fc;
+                    }
+                }
+                add_light(res, m, l0, l1, N, L[j], D, F);
             }
         }
     }
