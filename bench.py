@@ -7,8 +7,10 @@ MI355X vs host CPU.  A step renders ONE full frame of the configured workload
 (default C2 = the reference's scene2.dat at 1920x1080, max bounces 3) from a
 scene already resident in HBM into an RGBA8 framebuffer in HBM.  With N ranks
 (one process per GPU, torch.distributed over RCCL) every rank renders its
-contiguous row slab and the slabs are assembled with one RCCL all-gather over
-xGMI inside the timed step (strong scaling: the frame is fixed).
+contiguous row slab and the slabs are gathered to rank 0 with grouped RCCL
+point-to-point transfers over xGMI (rt_amd.dist.RootGather, double-buffered so
+frame k's gather overlaps frame k+1's render); the timed region ends after the
+last gather (strong scaling: the frame is fixed).
 
 value = primary rays (= pixels) of all ranks / max-over-ranks time, in Mray/s.
 The roofline entry prices the trace kernel against the FP32 vector peak with
@@ -141,14 +143,14 @@ def main():
     ctx.upload(scene)
     types = scene.arrays()[0]
 
-    from rt_amd.dist import gather_frame, slab_rows
+    from rt_amd.dist import RootGather, slab_rows
 
     r0, r1, rows = slab_rows(H, world, rank)   # equal slabs (padded when H % world != 0)
     frame = scene.frame.copy()
     frame.row_begin, frame.row_end = r0, r1
-    slab = torch.zeros((rows, W, 4), dtype=torch.uint8, device="cuda")
-    full = torch.zeros((world * rows, W, 4), dtype=torch.uint8, device="cuda") if world > 1 else slab
     stream = torch.cuda.current_stream().cuda_stream
+    gather = RootGather(dist, H, W, "cuda") if world > 1 else None
+    single = torch.zeros((rows, W, 4), dtype=torch.uint8, device="cuda")
 
     # one counted render (atomics) for the algorithmic work of this rank's slab
     sf = frame.copy()
@@ -157,14 +159,19 @@ def main():
     st = ctx.stats()
     flops = algorithmic_flops(types, st.primary_rays, st.bounce_rays, st.shadow_rays)
 
+    counter = [0]
+
     def step(ev=None):
+        k = counter[0]
+        counter[0] += 1
+        out = gather.target(k) if gather else single
         if ev is not None:
             ev[0].record()
-        ctx.render_async(frame, slab.data_ptr(), 0, stream)
+        ctx.render_async(frame, out.data_ptr(), 0, stream)
         if ev is not None:
             ev[1].record()
-        if world > 1:
-            gather_frame(slab, full, dist)
+        if gather:
+            gather.submit(k)   # slab -> rank 0 over xGMI, overlapping the next render
 
     for _ in range(args.warmup):
         step()
@@ -175,6 +182,8 @@ def main():
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(events[k])
+    if gather:
+        gather.finish()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -214,14 +223,14 @@ def main():
             "data": f"reference scene file {name}" if name != "heightfield" else "synthetic 50k-triangle heightfield (rt_amd.synth)",
             "config": {"workload": f"{name} {W}x{H} max_bounces={depth}", "width": W, "height": H,
                        "max_bounces": depth, "surfaces": int(types.shape[0]),
-                       "parallelism": f"row-slab x{world}" + (" + RCCL all-gather" if world > 1 else "")},
+                       "parallelism": f"row-slab x{world}" + (" + RCCL p2p gather to rank 0 (double-buffered)" if world > 1 else "")},
             "total_rays_per_s_M": round((tot_primary + tot_bounce + tot_shadow) * args.steps / elapsed / 1e6, 3),
             "rays_per_frame": {"primary": int(tot_primary), "bounce": int(tot_bounce), "shadow": int(tot_shadow)},
             "kernel_ms": round(kernel_ms, 4),
             "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
                          "frac_vs_nofma_issue_peak": round(achieved / PEAK_NOFMA_TOPS, 4),
-                         "flops_per_launch": int(flops), "kernel": f"rt_trace_kernel<{st.stack_depth}>"},
+                         "flops_per_launch": int(flops), "kernel": f"rt_trace_kernel<{st.stack_depth},{st.light_batch}>"},
         }
         if world == 1 and not args.no_cpu_baseline:
             cb = cpu_baseline(path, W, H, depth, args.cpu_seconds)

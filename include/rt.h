@@ -97,7 +97,7 @@ typedef struct rt_stats {
                                       all-lanes-opaque early exit           */
     float kernel_ms;       /* last render's kernel time (hipEvent)          */
     int32_t stack_depth;   /* compiled bounce-stack depth that ran          */
-    int32_t reserved;
+    int32_t light_batch;   /* lights sharing one shadow pass in that kernel */
 } rt_stats;
 
 /* ------------------------------------------------------------ host scene */

@@ -538,11 +538,10 @@ struct Counters {
 // pass shares the record loads, the loop overhead and the light-independent
 // part of the triangle test (S = P - p0, Q = S x e1, e2 . Q — the same
 // values Triangle.cpp:143-158 computes for every light's ray from P).
-#ifndef RT_LIGHT_BATCH
-#define RT_LIGHT_BATCH 4
-#endif
-constexpr int kLightBatch = RT_LIGHT_BATCH;
-
+// LB (lights per pass) is a kernel template parameter: 3 wins on scenes whose
+// triangle list is small (C2: -2..5%), 1 on big lists, where the extra VGPRs
+// cost occupancy (C3: +5..16% for 2..4), tools/ab_variants.py.
+template <int kLightBatch>
 __device__ __forceinline__ void shadow_opaque_batch(const SceneDev& S, int l0, int nl, const Vec3 P,
                                                     const Vec3 (&L)[kLightBatch], const float (&dist)[kLightBatch],
                                                     bool (&occ)[kLightBatch])
@@ -636,6 +635,7 @@ __device__ __forceinline__ void add_light(Color& res, const Mat& m, const float4
     }
 }
 
+template <int kLightBatch>
 __device__ __forceinline__ Color shade_local(const SceneDev& S, const Mat& m, const Vec3 P, const Vec3 N,
                                              const Vec3 D, Counters& cnt)
 {
@@ -672,7 +672,7 @@ __device__ __forceinline__ Color shade_local(const SceneDev& S, const Mat& m, co
             }
             occ[j] = !gate[j];
         }
-        shadow_opaque_batch(S, lb, nl, P, L, dist, occ);
+        shadow_opaque_batch<kLightBatch>(S, lb, nl, P, L, dist, occ);
 #pragma unroll
         for (int j = 0; j < kLightBatch; ++j) {
             if (j < nl && gate[j]) {
@@ -701,7 +701,7 @@ struct Frame {
     int surf, stage;
 };
 
-template <int MAXD>
+template <int MAXD, int LB>
 __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, Counters& cnt)
 {
     const Color bg{F.bg[0], F.bg[1], F.bg[2]};
@@ -718,7 +718,7 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
         const Vec3 N = hit_normal(S, idx, O, D, t);
         const Mat m = load_mat(S, idx);
         const Vec3 P = O + t * D;
-        return shade_local(S, m, P, N, D, cnt);
+        return shade_local<LB>(S, m, P, N, D, cnt);
     } else {
         Frame stk[MAXD];
         int sp = 0;
@@ -736,7 +736,7 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
                     const Vec3 N = hit_normal(S, idx, O, D, t);
                     const Mat m = load_mat(S, idx);
                     const Vec3 P = O + t * D;
-                    const Color acc = shade_local(S, m, P, N, D, cnt);
+                    const Color acc = shade_local<LB>(S, m, P, N, D, cnt);
                     // Scene.cpp:1779-1781 / :1790-1792 gates; bounces == sp
                     const float er = m.kr * energy;
                     const float et = m.kt * energy;
@@ -816,7 +816,7 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
     }
 }
 
-template <int MAXD>
+template <int MAXD, int LB>
 __global__ __launch_bounds__(256) void rt_trace_kernel(const SceneDev S, const FrameDev F, unsigned* __restrict__ rgba,
                                                        float* __restrict__ rgbf, StatsDev* __restrict__ stats)
 {
@@ -838,7 +838,7 @@ __global__ __launch_bounds__(256) void rt_trace_kernel(const SceneDev S, const F
         const Vec3 D = normalize(d0 * M);
         const Vec3 O = make3(F.cam[0], F.cam[1], F.cam[2]);
         cnt.primary = 1;
-        c = radiance<MAXD>(S, F, O, D, cnt);
+        c = radiance<MAXD, LB>(S, F, O, D, cnt);
         const size_t o = (size_t)ly * F.width + px;
         if (rgbf) {
             rgbf[3 * o] = c.r;
@@ -1158,12 +1158,18 @@ static constexpr int kTricamMaxTriangles = 256;
 
 typedef void (*kernel_fn)(const SceneDev, const FrameDev, unsigned*, float*, StatsDev*);
 
-static kernel_fn pick_kernel(int depth, int& cap)
+static kernel_fn pick_kernel(int depth, bool batch_lights, int& cap, int& lb)
 {
-#define RT_PICK(N)                                 \
-    if (depth <= N) {                              \
-        cap = N;                                   \
-        return (kernel_fn)&rt_trace_kernel<N>;     \
+    lb = 1;
+    if (depth == 0 && batch_lights) {
+        cap = 0;
+        lb = 3;
+        return (kernel_fn)&rt_trace_kernel<0, 3>;
+    }
+#define RT_PICK(N)                                   \
+    if (depth <= N) {                                \
+        cap = N;                                     \
+        return (kernel_fn)&rt_trace_kernel<N, 1>;    \
     }
     RT_STACK_DEPTHS(RT_PICK)
 #undef RT_PICK
@@ -1184,8 +1190,8 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
         return RT_E_ARG;
     }
     const int depth = reachable_depth(c, f);
-    int cap = 0;
-    kernel_fn k = pick_kernel(depth, cap);
+    int cap = 0, lb = 1;
+    kernel_fn k = pick_kernel(depth, c->n_lights > 1 && c->n_tri <= kTricamMaxTriangles, cap, lb);
     if (!k) {
         c->err = "reachable bounce depth " + std::to_string(depth) + " exceeds the compiled stack (32)";
         return RT_E_UNSUPPORTED;
@@ -1213,6 +1219,7 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
     const int rows = f->row_end - f->row_begin;
     c->last = rt_stats{};
     c->last.stack_depth = cap;
+    c->last.light_batch = lb;
     if (rows == 0) return RT_OK;
     if (f->flags & RT_FLAG_STATS) HIP_TRY(c, hipMemsetAsync(c->d_stats, 0, sizeof(StatsDev), st));
     // Camera-ray triangle values: recomputed only when the camera moves.

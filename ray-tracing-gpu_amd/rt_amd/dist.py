@@ -2,15 +2,23 @@
 
 One process per GPU (torch.distributed; backend "nccl" is RCCL on ROCm).
 Every pixel is independent and the scene is read-only, so a frame partitions
-into contiguous row slabs with no exchange until the very end, where ONE
-all-gather over xGMI assembles the RGBA8 frame.  Slabs are
-equal-height (the last one padded) so the gather is a single
-``all_gather_into_tensor`` whose output is the frame in row order — no
-permutation pass.
+into contiguous row slabs with no exchange until the very end, where the
+slabs meet in ONE gather over xGMI:
+
+* ``RootGather`` — the frame is assembled on rank 0 (the display / writer):
+  rank 0 renders its slab straight into the frame buffer and receives every
+  other slab with grouped point-to-point RCCL sends/receives, so each peer
+  uses its own direct xGMI link to the root (RCCL has no ncclGather).  Frames
+  are double-buffered, so the gather of frame k runs on RCCL's stream while
+  frame k+1 renders on the compute stream.
+* ``gather_frame`` — the all-gather form (every rank gets the frame).
+
+Slabs are equal-height (the last one padded) so a frame is one contiguous
+buffer of ``world * rows`` rows in row order — no permutation pass.
 """
 from __future__ import annotations
 
-from typing import Tuple
+from typing import List, Optional, Tuple
 
 
 def slab_rows(height: int, world: int, rank: int) -> Tuple[int, int, int]:
@@ -24,7 +32,7 @@ def slab_rows(height: int, world: int, rank: int) -> Tuple[int, int, int]:
 
 
 def gather_frame(slab, full, dist, group=None):
-    """Assemble equal-height slabs into `full` ([world*rows, W, 4]) on every
+    """All-gather equal-height slabs into `full` ([world*rows, W, 4]) on every
     rank.  RCCL: one all-gather; gloo (CPU tests): the list form."""
     world = dist.get_world_size(group)
     if world == 1:
@@ -37,3 +45,70 @@ def gather_frame(slab, full, dist, group=None):
         return full
     dist.all_gather_into_tensor(full, slab, group=group)
     return full
+
+
+class RootGather:
+    """Double-buffered gather of row slabs to rank 0.
+
+    Per frame k: ``out = g.target(k)`` is where this rank renders its slab
+    (on rank 0 a view into frame buffer k % depth); ``g.submit(k)`` posts the
+    sends/receives asynchronously; ``g.frame(k)`` (rank 0) is the assembled
+    frame once ``g.wait(k)`` (or ``g.finish()``) has run.
+    """
+
+    def __init__(self, dist, height: int, width: int, device, depth: int = 2, dtype=None, channels: int = 4):
+        import torch
+
+        self.dist = dist
+        self.world = dist.get_world_size()
+        self.rank = dist.get_rank()
+        self.H, self.W = height, width
+        _, _, self.rows = slab_rows(height, self.world, self.rank)
+        self.depth = depth
+        dtype = dtype or torch.uint8
+        shape_full = (self.world * self.rows, width, channels)
+        shape_slab = (self.rows, width, channels)
+        if self.rank == 0:
+            self.frames = [torch.zeros(shape_full, dtype=dtype, device=device) for _ in range(depth)]
+            self.slabs = [f[: self.rows] for f in self.frames]
+        else:
+            self.frames = []
+            self.slabs = [torch.zeros(shape_slab, dtype=dtype, device=device) for _ in range(depth)]
+        self.pending: List[Optional[list]] = [None] * depth
+
+    def target(self, k: int):
+        """Buffer to render frame k's slab into (waits until it is free)."""
+        self.wait(k)
+        return self.slabs[k % self.depth]
+
+    def submit(self, k: int):
+        if self.world == 1:
+            return
+        d, b = self.dist, k % self.depth
+        ops = []
+        if self.rank == 0:
+            for r in range(1, self.world):
+                view = self.frames[b][r * self.rows:(r + 1) * self.rows]
+                ops.append(d.P2POp(d.irecv, view, r))
+        else:
+            ops.append(d.P2POp(d.isend, self.slabs[b], 0))
+        if d.get_backend() == "gloo":
+            works = [op.op(op.tensor, op.peer) for op in ops]
+        else:
+            works = d.batch_isend_irecv(ops)
+        self.pending[b] = works
+
+    def wait(self, k: int):
+        b = k % self.depth
+        if self.pending[b] is not None:
+            for w in self.pending[b]:
+                w.wait()
+            self.pending[b] = None
+
+    def finish(self):
+        for b in range(self.depth):
+            self.wait(b)
+
+    def frame(self, k: int):
+        """Rank 0: the assembled frame k (H rows, bottom-up)."""
+        return self.frames[k % self.depth][: self.H]

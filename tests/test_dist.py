@@ -45,6 +45,53 @@ def _worker(rank, world, port, path, w, h, depth, out_q):
     dist.destroy_process_group()
 
 
+def _worker_root(rank, world, port, path, w, h, depth, out_q):
+    """RootGather: 3 frames through the double-buffered p2p gather."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from conftest import Oracle
+    from rt_amd.dist import RootGather
+
+    g = RootGather(dist, h, w, "cpu", depth=2)
+    r0, r1, rows = slab_rows(h, world, rank)
+    frames = []
+    for k in range(3):
+        buf = g.target(k)
+        buf.zero_()
+        if r1 > r0:
+            # frame k = the scene at depth k (different images per frame)
+            img = Oracle().render(path, w, h, k, (r0, r1, 0, w), threads=1)
+            buf[: r1 - r0] = torch.from_numpy(rgba8(img))
+        g.submit(k)
+        if rank == 0 and k >= 1:
+            g.wait(k - 1)
+            frames.append(g.frame(k - 1).numpy().copy())
+    g.finish()
+    if rank == 0:
+        frames.append(g.frame(2).numpy().copy())
+        out_q.put(frames)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,h", [(2, 30), (3, 31)])
+def test_root_gather_pipelined(oracle, world, h):
+    w = 36
+    path = os.path.join(SCENES, "scene7.dat")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_root, args=(r, world, port, path, w, h, 0, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for k in range(3):
+        assert np.array_equal(got[k], rgba8(oracle.render(path, w, h, k))), k
+
+
 @pytest.mark.parametrize("world,h", [(2, 30), (3, 31)])
 def test_gather_matches_single_frame(oracle, world, h):
     w, depth = 40, 3
