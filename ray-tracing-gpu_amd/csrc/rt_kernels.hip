@@ -323,6 +323,64 @@ __device__ __forceinline__ int closest_hit(const SceneDev& S, const Vec3 O, cons
     return bi;
 }
 
+// ----------------------------------------------- scalar prefetch (s_load)
+// hipcc sinks a plain load of the next record below the culling branch, so
+// every iteration waits a full scalar-cache round trip.  These issue the
+// s_load in inline asm at the top of the iteration and retire it with an
+// s_waitcnt that also "redefines" the registers (so no use can be scheduled
+// before it).  Every path must reach rt_swait before the registers die, or a
+// late load could land in reallocated SGPRs.  hipcc's own SMEM waits are
+// always lgkmcnt(0) (SMEM returns out of order), so they stay correct.
+#ifndef RT_PF_CAMERA
+#define RT_PF_CAMERA 0
+#endif
+#ifndef RT_PF_SHADOW
+#define RT_PF_SHADOW 1
+#endif
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x16 __attribute__((ext_vector_type(16)));
+__device__ __forceinline__ u32x4 rt_sload4(const void* p)
+{
+    u32x4 r;
+    asm volatile("s_load_dwordx4 %0, %1, 0x0" : "=s"(r) : "s"(p));
+    return r;
+}
+__device__ __forceinline__ u32x16 rt_sload16(const void* p)
+{
+    u32x16 r;
+    asm volatile("s_load_dwordx16 %0, %1, 0x0" : "=s"(r) : "s"(p));
+    return r;
+}
+typedef unsigned int u32x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ u32x8 rt_sload8(const void* p)
+{
+    u32x8 r;
+    asm volatile("s_load_dwordx8 %0, %1, 0x0" : "=s"(r) : "s"(p));
+    return r;
+}
+__device__ __forceinline__ void rt_swait(u32x8& a)
+{
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(a));
+}
+__device__ __forceinline__ float4 f4(const u32x8 v, int q)
+{
+    return make_float4(__uint_as_float(v[4 * q]), __uint_as_float(v[4 * q + 1]), __uint_as_float(v[4 * q + 2]),
+                       __uint_as_float(v[4 * q + 3]));
+}
+__device__ __forceinline__ void rt_swait(u32x4& a, u32x16& b)
+{
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(a), "+s"(b));
+}
+__device__ __forceinline__ float4 f4(const u32x4 v)
+{
+    return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+}
+__device__ __forceinline__ float4 f4(const u32x16 v, int q)
+{
+    return make_float4(__uint_as_float(v[4 * q]), __uint_as_float(v[4 * q + 1]), __uint_as_float(v[4 * q + 2]),
+                       __uint_as_float(v[4 * q + 3]));
+}
+
 // Closest hit for camera rays (origin = the camera for every lane): the
 // per-triangle values that depend only on the origin come from tricam[].
 #ifndef RT_GROUP
@@ -355,13 +413,32 @@ __device__ __forceinline__ int closest_hit_camera(const SceneDev& S, const Vec3 
 {
     float bt = -1.0f;
     int bi = -1;
-    int k = 0;
-    for (; k < S.n_tri; ++k) {
+#if RT_PF_CAMERA
+    if (S.n_tri > 0) {
+        // record k+1 (cone + camera record) is in flight while k is tested
+        u32x4 cone = rt_sload4(S.cone_cam);
+        u32x16 rec = rt_sload16(S.tricam);
+        rt_swait(cone, rec);
+        for (int k = 0; k < S.n_tri; ++k) {
+            const int kn = k + 1 < S.n_tri ? k + 1 : k;
+            u32x4 cone_n = rt_sload4(S.cone_cam + 2 * kn);
+            u32x16 rec_n = rt_sload16(S.tricam + 4 * kn);
+            const float4 cc = f4(cone);
+            if (__any(dot(D, make3(cc.x, cc.y, cc.z)) >= cc.w))
+                camera_tri(f4(rec, 0), f4(rec, 1), f4(rec, 2), f4(rec, 3), D, bt, bi);
+            rt_swait(cone_n, rec_n);
+            cone = cone_n;
+            rec = rec_n;
+        }
+    }
+#else
+    for (int k = 0; k < S.n_tri; ++k) {
         const float4 cc = S.cone_cam[2 * k];
         if (!__any(dot(D, make3(cc.x, cc.y, cc.z)) >= cc.w)) continue;
         const float4* r = S.tricam + 4 * k;
         camera_tri(r[0], r[1], r[2], r[3], D, bt, bi);
     }
+#endif
     for (int k = 0; k < S.n_plane; ++k) {
         const float4 a = S.plane[2 * k], b = S.plane[2 * k + 1];
         float t;
@@ -541,7 +618,7 @@ struct Counters {
 // LB (lights per pass) is a kernel template parameter: 3 wins on scenes whose
 // triangle list is small (C2: -2..5%), 1 on big lists, where the extra VGPRs
 // cost occupancy (C3: +5..16% for 2..4), tools/ab_variants.py.
-template <int kLightBatch>
+template <int kLightBatch, bool PF>
 __device__ __forceinline__ void shadow_opaque_batch(const SceneDev& S, int l0, int nl, const Vec3 P,
                                                     const Vec3 (&L)[kLightBatch], const float (&dist)[kLightBatch],
                                                     bool (&occ)[kLightBatch])
@@ -551,39 +628,72 @@ __device__ __forceinline__ void shadow_opaque_batch(const SceneDev& S, int l0, i
     float slack[kLightBatch];
 #pragma unroll
     for (int j = 0; j < kLightBatch; ++j) slack[j] = dist[j] * 1e-6f;
+    // cone records of triangle k+1 (all lights of the batch) are in flight
+    // while triangle k is tested
+    u32x8 cn[kLightBatch];
+    if (PF && S.n_tri_opaque > 0) {
+#pragma unroll
+        for (int j = 0; j < kLightBatch; ++j) {
+            cn[j] = rt_sload8(cone + cstride * (j < nl ? j : 0));
+            rt_swait(cn[j]);
+        }
+    }
     for (int k = 0; k < S.n_tri_opaque; ++k) {
         bool live = false;
 #pragma unroll
         for (int j = 0; j < kLightBatch; ++j) live |= (j < nl) & !occ[j];
         if (!__any(live)) break;
+        const int kn = k + 1 < S.n_tri_opaque ? k + 1 : k;
+        u32x8 cnn[kLightBatch];
+        if constexpr (PF) {
+#pragma unroll
+            for (int j = 0; j < kLightBatch; ++j) cnn[j] = rt_sload8(cone + cstride * (j < nl ? j : 0) + 2 * kn);
+        } else {
+            (void)kn;
+        }
         bool reach[kLightBatch];
         bool any_reach = false;
 #pragma unroll
         for (int j = 0; j < kLightBatch; ++j) {
             reach[j] = false;
             if (j < nl) {
-                const float4 c0 = cone[cstride * j + 2 * k], c1 = cone[cstride * j + 2 * k + 1];
+                float4 c0, c1;
+                if constexpr (PF) {
+                    c0 = f4(cn[j], 0);
+                    c1 = f4(cn[j], 1);
+                } else {
+                    c0 = cone[cstride * j + 2 * k];
+                    c1 = cone[cstride * j + 2 * k + 1];
+                }
                 reach[j] = !occ[j] & (c1.x < dist[j]) &
                            (-dot(L[j], make3(c0.x, c0.y, c0.z)) >= c0.w - slack[j] * c1.y);
                 any_reach |= reach[j];
             }
         }
-        if (!__any(any_reach)) continue;
-        const TriRec tr = load_tri(S, k);
-        const Vec3 Sv = P - tr.p0;
-        const Vec3 Q = cross(Sv, tr.e1);
-        const float tq = dot(tr.e2, Q);
+        if (__any(any_reach)) {
+            const TriRec tr = load_tri(S, k);
+            const Vec3 Sv = P - tr.p0;
+            const Vec3 Q = cross(Sv, tr.e1);
+            const float tq = dot(tr.e2, Q);
 #pragma unroll
-        for (int j = 0; j < kLightBatch; ++j) {
-            if (j < nl && __any(reach[j])) {
-                const Vec3 Pv = cross(L[j], tr.e2);
-                const float det = dot(tr.e1, Pv);
-                const float inv = recip_det(det);
-                const float u = dot(Sv, Pv) * inv;
-                const float v = dot(L[j], Q) * inv;
-                const float t = tq * inv;
-                const bool ok = !(fabsf(det) < kEps) & !((u < 0) | (u > 1)) & !((v < 0) | (u + v > 1));
-                occ[j] |= ok & (t > kEps) & (t < dist[j]);
+            for (int j = 0; j < kLightBatch; ++j) {
+                if (j < nl && __any(reach[j])) {
+                    const Vec3 Pv = cross(L[j], tr.e2);
+                    const float det = dot(tr.e1, Pv);
+                    const float inv = recip_det(det);
+                    const float u = dot(Sv, Pv) * inv;
+                    const float v = dot(L[j], Q) * inv;
+                    const float t = tq * inv;
+                    const bool ok = !(fabsf(det) < kEps) & !((u < 0) | (u > 1)) & !((v < 0) | (u + v > 1));
+                    occ[j] |= ok & (t > kEps) & (t < dist[j]);
+                }
+            }
+        }
+        if constexpr (PF) {
+#pragma unroll
+            for (int j = 0; j < kLightBatch; ++j) {
+                rt_swait(cnn[j]);
+                cn[j] = cnn[j];
             }
         }
     }
@@ -635,7 +745,7 @@ __device__ __forceinline__ void add_light(Color& res, const Mat& m, const float4
     }
 }
 
-template <int kLightBatch>
+template <int kLightBatch, bool PF>
 __device__ __forceinline__ Color shade_local(const SceneDev& S, const Mat& m, const Vec3 P, const Vec3 N,
                                              const Vec3 D, Counters& cnt)
 {
@@ -672,7 +782,7 @@ __device__ __forceinline__ Color shade_local(const SceneDev& S, const Mat& m, co
             }
             occ[j] = !gate[j];
         }
-        shadow_opaque_batch<kLightBatch>(S, lb, nl, P, L, dist, occ);
+        shadow_opaque_batch<kLightBatch, PF>(S, lb, nl, P, L, dist, occ);
 #pragma unroll
         for (int j = 0; j < kLightBatch; ++j) {
             if (j < nl && gate[j]) {
@@ -701,7 +811,7 @@ struct Frame {
     int surf, stage;
 };
 
-template <int MAXD, int LB>
+template <int MAXD, int LB, bool PF>
 __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, Counters& cnt)
 {
     const Color bg{F.bg[0], F.bg[1], F.bg[2]};
@@ -718,7 +828,7 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
         const Vec3 N = hit_normal(S, idx, O, D, t);
         const Mat m = load_mat(S, idx);
         const Vec3 P = O + t * D;
-        return shade_local<LB>(S, m, P, N, D, cnt);
+        return shade_local<LB, PF>(S, m, P, N, D, cnt);
     } else {
         Frame stk[MAXD];
         int sp = 0;
@@ -736,7 +846,7 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
                     const Vec3 N = hit_normal(S, idx, O, D, t);
                     const Mat m = load_mat(S, idx);
                     const Vec3 P = O + t * D;
-                    const Color acc = shade_local<LB>(S, m, P, N, D, cnt);
+                    const Color acc = shade_local<LB, PF>(S, m, P, N, D, cnt);
                     // Scene.cpp:1779-1781 / :1790-1792 gates; bounces == sp
                     const float er = m.kr * energy;
                     const float et = m.kt * energy;
@@ -816,7 +926,7 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
     }
 }
 
-template <int MAXD, int LB>
+template <int MAXD, int LB, bool PF>
 __global__ __launch_bounds__(256) void rt_trace_kernel(const SceneDev S, const FrameDev F, unsigned* __restrict__ rgba,
                                                        float* __restrict__ rgbf, StatsDev* __restrict__ stats)
 {
@@ -838,7 +948,7 @@ __global__ __launch_bounds__(256) void rt_trace_kernel(const SceneDev S, const F
         const Vec3 D = normalize(d0 * M);
         const Vec3 O = make3(F.cam[0], F.cam[1], F.cam[2]);
         cnt.primary = 1;
-        c = radiance<MAXD, LB>(S, F, O, D, cnt);
+        c = radiance<MAXD, LB, PF>(S, F, O, D, cnt);
         const size_t o = (size_t)ly * F.width + px;
         if (rgbf) {
             rgbf[3 * o] = c.r;
@@ -1158,18 +1268,26 @@ static constexpr int kTricamMaxTriangles = 256;
 
 typedef void (*kernel_fn)(const SceneDev, const FrameDev, unsigned*, float*, StatsDev*);
 
-static kernel_fn pick_kernel(int depth, bool batch_lights, int& cap, int& lb)
+// Kernel variants (tools/ab_variants.py, MI355X): small triangle lists
+// batch 3 lights per shadow pass (C2 -4%); big lists (> 256 triangles) run
+// one light per pass with the next cone record prefetched in flight
+// (C3 -15%); bounce kernels use neither (each regressed scene7 by 4%).
+static kernel_fn pick_kernel(int depth, bool big, int n_lights, int& cap, int& lb)
 {
     lb = 1;
-    if (depth == 0 && batch_lights) {
+    if (depth == 0 && big) {
+        cap = 0;
+        return (kernel_fn)&rt_trace_kernel<0, 1, true>;
+    }
+    if (depth == 0 && n_lights > 1) {
         cap = 0;
         lb = 3;
-        return (kernel_fn)&rt_trace_kernel<0, 3>;
+        return (kernel_fn)&rt_trace_kernel<0, 3, false>;
     }
-#define RT_PICK(N)                                   \
-    if (depth <= N) {                                \
-        cap = N;                                     \
-        return (kernel_fn)&rt_trace_kernel<N, 1>;    \
+#define RT_PICK(N)                                          \
+    if (depth <= N) {                                       \
+        cap = N;                                            \
+        return (kernel_fn)&rt_trace_kernel<N, 1, false>;    \
     }
     RT_STACK_DEPTHS(RT_PICK)
 #undef RT_PICK
@@ -1191,7 +1309,7 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
     }
     const int depth = reachable_depth(c, f);
     int cap = 0, lb = 1;
-    kernel_fn k = pick_kernel(depth, c->n_lights > 1 && c->n_tri <= kTricamMaxTriangles, cap, lb);
+    kernel_fn k = pick_kernel(depth, c->n_tri > kTricamMaxTriangles, c->n_lights, cap, lb);
     if (!k) {
         c->err = "reachable bounce depth " + std::to_string(depth) + " exceeds the compiled stack (32)";
         return RT_E_UNSUPPORTED;
