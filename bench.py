@@ -175,20 +175,35 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # Kernel time, measured live over the timed region with HIP events on the
+    # stream the kernel is launched on: at N=1 the stream runs nothing but the
+    # trace kernel, so one event pair around the K launches / K is the average
+    # launch duration (back-to-back, no event packets between launches, which
+    # would add their own dispatch latency).  At N>1 the compute stream also
+    # waits for gather buffers, so each launch gets its own event pair.
+    per_launch = world > 1
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(args.steps if per_launch else 1)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    if not per_launch:
+        events[0][0].record()
     for k in range(args.steps):
-        step(events[k])
+        step(events[k] if per_launch else None)
+    if not per_launch:
+        events[0][1].record()
     if gather:
         gather.finish()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kernel_ms = sum(a.elapsed_time(b) for a, b in events) / args.steps
+    if per_launch:
+        kernel_ms = sum(a.elapsed_time(b) for a, b in events) / args.steps
+    else:
+        kernel_ms = events[0][0].elapsed_time(events[0][1]) / args.steps
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -34,8 +34,17 @@ for s in $STEPS; do
       run pmc_sq2 300 rocprofv3 --pmc SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM SQ_INSTS_LDS SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_SALU SQ_THREAD_CYCLES_VALU SQ_INSTS_BRANCH --output-format csv -d gpurun_out/pmc -o sq2 -- $B
       ;;
     ab) run ab_${CONFIG:-c2} 600 python tools/ab_variants.py --config ${CONFIG:-c2} ray-tracing-gpu_amd/lib/var/*.so ;;
+    pmcvar)
+      for L in ray-tracing-gpu_amd/lib/var/*.so; do
+        n=$(basename $L .so)
+        export RT_AMD_LIB=$PWD/$L
+        run pmcvar_$n 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmcvar/$n -o sq -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline --config ${CONFIG:-c2}
+        unset RT_AMD_LIB
+      done ;;
+    fastmath) run fastmath_check 600 tools/fastmath_check ;;
     rcp) run rcp_exhaustive 300 tools/rcp_exhaustive ;;
-    prof) run rocprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 20 --no-cpu-baseline ;;
+    prof) run rocprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 200 --no-cpu-baseline --config ${CONFIG:-c2}
+          python tools/prof_summary.py gpurun_out/prof/run_kernel_trace.csv > gpurun_out/prof/summary.json ;;
   esac
 done
 exit 0
