@@ -119,10 +119,13 @@ struct StatsDev {
 
 // ----------------------------------------------------- exact fast reciprocal
 // IEEE 1.0f/x in 3 VALU instead of the ~10-instruction division expansion:
-// v_rcp_f32 then one FMA Newton step.  tools/rcp_exhaustive.hip checked it
-// against 1.0f/x on gfx950 for EVERY float with |x| in [2^-125, 2^125]
-// (4,194,304,002 values, 0 mismatches; v_rcp_f32 alone: 448,837,500).
-// Outside that range (and for NaN/Inf) the wave takes the IEEE division.
+// rcp_nr (rt_fastmath.h: v_rcp_f32 then one FMA Newton step), checked by
+// tools/fastmath_check.hip against 1.0f/x on gfx950 for EVERY float with |x|
+// in [2^-125, 2^125] (4,194,304,002 values, 0 mismatches; v_rcp_f32 alone:
+// 448,837,500 mismatches).  Outside that range (and for NaN/Inf) the wave
+// takes the IEEE division.  (The same header's exact division and sqrt
+// sequences were measured too: their domain guards cost more than they save
+// in this kernel, so the compiler's IEEE expansions stay.)
 // For Det: lanes with |Det| < EPSILON are rejected whatever InvDet is
 // (Triangle.cpp:141-142), so only the others must be in range.
 __device__ __forceinline__ float recip_det(float det)
@@ -131,24 +134,6 @@ __device__ __forceinline__ float recip_det(float det)
     const bool need_ieee = !(a <= 0x1p125f) & !(a < kEps);
     if (__builtin_expect(__any(need_ieee), 0)) return 1.0f / det;
     return rcp_nr(det);
-}
-
-// Device forms of Vecteur3.h Norme / Normaliser / operator/(REAL): same
-// expressions, with sqrt and 1/x through rt_fastmath.h (bit-identical on its
-// domain; the wave falls back to IEEE otherwise).
-__device__ __forceinline__ float dnorm(Vec3 v) { return sqrt_w(v.x * v.x + v.y * v.y + v.z * v.z); }
-__device__ __forceinline__ Vec3 ddiv_recip(Vec3 v, float s)
-{
-    const float inv = recip_w(s);
-    return {v.x * inv, v.y * inv, v.z * inv};
-}
-__device__ __forceinline__ Vec3 dnormalize(Vec3 v)
-{
-    const float len = dnorm(v);
-    // lanes with len <= EPSILON return ZERO and never use the reciprocal
-    const bool need = (len > kEps) & !in_rcp_domain(len);
-    const float inv = __builtin_expect(__any(need), 0) ? 1.0f / len : rcp_nr(len);
-    return len > kEps ? v * inv : make3(0.f, 0.f, 0.f);
 }
 
 // --------------------------------------------------------- primitive tests
@@ -179,12 +164,8 @@ __device__ __forceinline__ bool hit_plane(const float4 a, const float4 b, const 
 {
     const Vec3 n = make3(a.y, a.z, a.w);
     const float vd = dot(n, D);
-    const float num = -(dot(n, O) + b.x);
-    const bool ok = fabsf(vd) > kEps;
-    // only lanes that report a hit need the exact quotient
-    if (__builtin_expect(__any(ok & !in_div_domain(num, vd)), 0)) t = num / vd;
-    else t = div_nr(num, vd, rcp_nr(vd));
-    return ok;
+    t = -(dot(n, O) + b.x) / vd;
+    return fabsf(vd) > kEps;
 }
 
 // Quadrique.cpp:171-194 — the three coefficients, expression trees verbatim.
@@ -214,19 +195,11 @@ __device__ __forceinline__ bool hit_quadric(const float4 a, const float4 b, cons
 {
     const QuadCoef k = quad_coef(a, b, c, O, D);
     if (k.A != 0.0f) {
-        float Ka, Kb;
-        if (__builtin_expect(__any(!in_div_domain(-k.B, k.A) | !in_div_domain(k.C, k.A)), 0)) {
-            Ka = -k.B / k.A;
-            Kb = k.C / k.A;
-        } else {
-            const float y = rcp_nr(k.A);  // one RN(1/A) serves both quotients
-            Ka = div_nr(-k.B, k.A, y);
-            Kb = div_nr(k.C, k.A, y);
-        }
+        const float Ka = -k.B / k.A;
+        const float Kb = k.C / k.A;
         float delta = Ka * Ka - Kb;
         const bool pos = delta > 0;
-        if (__builtin_expect(__any(pos & !in_sqrt_domain(delta)), 0)) delta = sqrtf(delta);
-        else delta = sqrt_cr(delta);
+        delta = sqrtf(delta);
         const float t0 = Ka - delta;
         const float t1 = Ka + delta;
         float dist = t0 < t1 ? t0 : t1;
@@ -252,9 +225,9 @@ __device__ __forceinline__ Vec3 quadric_normal(const float4 a, const float4 b, c
         n.x = 2.0f * q.x * hp.x + m.y * hp.z + m.z * hp.y + l.x;
         n.y = 2.0f * q.y * hp.y + m.x * hp.z + m.z * hp.x + l.y;
         n.z = 2.0f * q.z * hp.z + m.x * hp.y + m.y * hp.x + l.z;
-        return dnormalize(n);
+        return normalize(n);
     }
-    return dnormalize(l);
+    return normalize(l);
 }
 
 __device__ __forceinline__ int kind_of(const float4 a) { return __float_as_int(a.x); }
@@ -567,8 +540,8 @@ __device__ __forceinline__ Color shadow_filter(const SceneDev& S, int light, con
                                                unsigned& skipped)
 {
     Color F{1.0f, 1.0f, 1.0f};
-    const float dist = dnorm(L);
-    L = ddiv_recip(L, dist);
+    const float dist = norm(L);
+    L = div_recip(L, dist);
     if (!S.shadow_split) {
         // General case: the product over every surface in file order.
         for (int i = 0; i < S.n_surf; ++i) {
@@ -801,15 +774,13 @@ __device__ __forceinline__ Color shade_local(const SceneDev& S, const Mat& m, co
                 const float4 l0 = S.lights[2 * (lb + j)];
                 const Vec3 Lr = make3(l0.x, l0.y, l0.z) - P;
                 gate[j] = dot(Lr, N) > 0;          // Scene.cpp:1756, unnormalised
-                dist[j] = dnorm(Lr);               // Scene.cpp:1847-1848
-                L[j] = ddiv_recip(Lr, dist[j]);
+                dist[j] = norm(Lr);                // Scene.cpp:1847-1848
+                L[j] = div_recip(Lr, dist[j]);
                 cnt.shadow += gate[j];
             }
             occ[j] = !gate[j];
         }
-#ifndef RT_ABLATE_SHADOW  // timing-only build: no shadow tests
         shadow_opaque_batch<kLightBatch, PF>(S, lb, nl, P, L, dist, occ);
-#endif
 #pragma unroll
         for (int j = 0; j < kLightBatch; ++j) {
             if (j < nl && gate[j]) {
@@ -972,7 +943,7 @@ __global__ __launch_bounds__(256) void rt_trace_kernel(const SceneDev S, const F
         Mat4 M;
 #pragma unroll
         for (int i = 0; i < 16; ++i) M.m[i >> 2][i & 3] = F.orient[i];
-        const Vec3 D = dnormalize(d0 * M);
+        const Vec3 D = normalize(d0 * M);
         const Vec3 O = make3(F.cam[0], F.cam[1], F.cam[2]);
         cnt.primary = 1;
         c = radiance<MAXD, LB, PF>(S, F, O, D, cnt);

@@ -42,7 +42,7 @@ for s in $STEPS; do
         unset RT_AMD_LIB
       done ;;
     fastmath) run fastmath_check 600 tools/fastmath_check ;;
-    rcp) run rcp_exhaustive 300 tools/rcp_exhaustive ;;
+
     prof) run rocprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 200 --no-cpu-baseline --config ${CONFIG:-c2}
           python tools/prof_summary.py gpurun_out/prof/run_kernel_trace.csv > gpurun_out/prof/summary.json ;;
   esac
