@@ -473,30 +473,85 @@ __global__ void rt_camera_prepass(const float4* __restrict__ tri, int n, float c
     o[3] = make_float4(tq, c.y, 0.f, 0.f);
 }
 
-// Cone records for apex A (one thread per triangle).  sph = bounding sphere
-// (centre, radius already inflated on the host).  Margins: the radius grows
-// by 2e-5 of the apex distance and the cosine threshold drops by 2e-5 — both
-// far above the float rounding of this test (~1e-7), so a triangle is only
-// skipped when no float ray from A could reach its sphere.
-__global__ void rt_cone_prepass(const float4* __restrict__ sph, int n, float ax, float ay, float az,
-                                float4* __restrict__ out)
+// Cone records for apex A (one thread per triangle, in double).
+//
+// Culling a triangle for a ray that misses its bounding cone is exact only if
+// the reference's float test could not have reported a hit for that ray
+// either.  Its rounding (Triangle.cpp:127-172 in f32, eps = 2^-24) gives,
+// with S = origin - p0, L = longest edge, N = e1 x e2, a = |D . N|/|N|:
+//   u, v, u+v  within  x = k (rho + 2 delta)  of their exact values,
+//   delta = 9 eps |S| L / |det|,  rho = 7 eps L^2 / |det| + 3 eps,
+//   k = 1/(1 - rho_cap),  rho_cap = rho at the reference's |det| >= 0.01 gate,
+// so a reported hit means the ray crosses the plane within 3 x L of the
+// triangle, i.e. within G/a + tau, G = gS |S| + gL, tau = 9 k eps L (coef[]
+// holds gS, gL, rho_cap).  The cone is built on the sphere grown by a margin
+// m, so a culled ray is safe where G/a + tau <= m (well conditioned); where
+// it is nearly parallel to the plane it crosses it far away instead:
+// dist(X, tri) >= h/a - (h + dv + r), h = the apex's distance to the plane.
+// One of the two holds for EVERY a iff
+//   h >= G (m + Rp) / (m - tau)            (Rp = h + dv + r),
+// which fixes m per pair: 1% of r, or what this needs (up to 10 r; beyond
+// that the pair is never culled).  Shadow rays have |S| <= dist + dv + r, so
+// the condition holds up to a distance cap (c1.z; m is sized so that the
+// cap reaches dtarget).  In the well conditioned case the reference's t errs
+// by <= m/3: dmin absorbs it for a sphere beyond P, a second cap on dist for
+// a sphere behind the light.  Rounding of the cull test itself: radius
+// + 2e-5 dv, cosine - 2e-5.
+//
+//   camera: c0 = [dir to centre, cosT]   (c1 unused)
+//   light : c0 = [dir to centre, cosT]   c1 = [dmin, 2/dmin, dcap, 0]
+// "always test": cosT = -2, dmin = dcap = -inf.
+__global__ void rt_cone_prepass(const float4* __restrict__ tri, const float4* __restrict__ sph,
+                                const float4* __restrict__ nrm, const float4* __restrict__ coef, int n, float ax,
+                                float ay, float az, int camera, float dtarget, float4* __restrict__ out)
 {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
-    const float4 s = sph[k];
-    const Vec3 v = make3(s.x - ax, s.y - ay, s.z - az);
-    const float dv = norm(v);
-    const float r = s.w + 2e-5f * dv;
-    float4 c0 = make_float4(0.f, 0.f, 0.f, -2.0f), c1 = make_float4(-INFINITY, 0.f, 0.f, 0.f);
-    if (dv > r && isfinite(dv) && isfinite(r)) {  // apex outside the sphere
-        const float inv = 1.0f / dv;
-        const float sn = r * inv;
-        const float dmin = (dv - r) * (1.0f - 1e-5f);
-        c0 = make_float4(v.x * inv, v.y * inv, v.z * inv, sqrtf(1.0f - sn * sn) - 2e-5f);
-        c1 = make_float4(dmin, 2.0f / dmin, 0.f, 0.f);
+    const float4 s = sph[k], nr = nrm[k], cf = coef[k], p0 = tri[3 * k];
+    const double vx = (double)s.x - ax, vy = (double)s.y - ay, vz = (double)s.z - az;
+    const double dv = sqrt(vx * vx + vy * vy + vz * vz);
+    const double r0 = s.w, L = nr.w, gS = cf.x, gL = cf.y, rho_cap = cf.z;
+    const double h = fabs(nr.x * ((double)ax - p0.x) + nr.y * ((double)ay - p0.y) + nr.z * ((double)az - p0.z));
+    const double h_eff = 0.998 * h - 1e-6 * (dv + r0);  // float normal; shadow ray passes within 1e-3 h of A
+    const double tau = 18.0 * 0x1p-24 * L;                // k <= 2
+    const double Rp = 1.001 * h + dv + r0 + 1e-6 * dv;
+    // |S| bound and the G the margin must cover
+    const double G = gS * ((camera ? 0.0 : (double)dtarget * 1.0001) + dv + r0) + gL;
+    double m = 0.01 * r0;
+    if (h_eff > 1.01 * G) m = fmax(m, 1.001 * (h_eff * tau + 1.01 * G * Rp) / (h_eff - 1.01 * G));
+    const double rc = r0 + m + 2e-5 * dv;  // cone radius
+    float4 c0 = make_float4(0.f, 0.f, 0.f, -2.0f);
+    float4 c1 = make_float4(-INFINITY, 0.f, -INFINITY, 0.f);
+    if (rho_cap >= 0.0 && h_eff > 1.01 * G && m <= 10.0 * r0 && m > 2.0 * tau && dv - rc > m / 3.0 + 0.02 &&
+        isfinite(dv) && isfinite(gS) && isfinite(gL)) {
+        const double phi = 1.01 * (m + Rp) / (m - tau);
+        const double cosT = sqrt(1.0 - (rc / dv) * (rc / dv)) - 2e-5;
+        const float4 cone = make_float4((float)(vx / dv), (float)(vy / dv), (float)(vz / dv), (float)cosT);
+        if (camera) {
+            if (h_eff >= (gS * (dv + r0) + gL) * phi) c0 = cone;
+        } else {
+            const double dmin = (dv - rc - m / 3.0) * (1.0 - 1e-5);
+            const double dcap1 = ((h_eff / phi - gL) / gS - dv - r0) / 1.0001;
+            const double rhoN = fmin(m / (3.0 * L), rho_cap);  // rho where well conditioned
+            const double dcap2 =
+                rhoN > 0.0 ? ((dv - rc) * (1.0 - rhoN) - m / 3.0) / rhoN / 1.01 : INFINITY;
+            const double dcap = fmin(fmin(dcap1, dcap2), 1000.0 * h);
+            if (dcap > 0.0) {
+                c0 = cone;
+                c1 = make_float4((float)dmin, (float)(2.0 / dmin), (float)(dcap * (1.0 - 1e-6)), 0.f);
+            }
+        }
     }
     out[2 * k] = c0;
     out[2 * k + 1] = c1;
+}
+
+// Shadow-ray cull predicate (L normalised towards the light, dist to it):
+// the segment reaches the sphere's distance and the cone, or the lane lies
+// beyond the distance the culling argument covers (c1.z).
+__device__ __forceinline__ bool light_reach(const float4 c0, const float4 c1, const Vec3 L, float dist, float slack)
+{
+    return ((c1.x < dist) & (-dot(L, make3(c0.x, c0.y, c0.z)) >= c0.w - slack * c1.y)) | (dist > c1.z);
 }
 
 __device__ __forceinline__ Vec3 hit_normal(const SceneDev& S, int idx, const Vec3 O, const Vec3 D, float t)
@@ -563,7 +618,7 @@ __device__ __forceinline__ Color shadow_filter(const SceneDev& S, int light, con
         if (!__any(!occluded)) break;
         ++done;
         const float4 c0 = cone[2 * k], c1 = cone[2 * k + 1];
-        const bool reach = !occluded & (c1.x < dist) & (-dot(L, make3(c0.x, c0.y, c0.z)) >= c0.w - slack * c1.y);
+        const bool reach = !occluded & light_reach(c0, c1, L, dist, slack);
         if (!__any(reach)) continue;
         const TriRec tr = load_tri(S, k);
         const TriU r = tri_u(tr.p0, tr.e1, tr.e2, P, L);
@@ -663,8 +718,7 @@ __device__ __forceinline__ void shadow_opaque_batch(const SceneDev& S, int l0, i
                     c0 = cone[cstride * j + 2 * k];
                     c1 = cone[cstride * j + 2 * k + 1];
                 }
-                reach[j] = !occ[j] & (c1.x < dist[j]) &
-                           (-dot(L[j], make3(c0.x, c0.y, c0.z)) >= c0.w - slack[j] * c1.y);
+                reach[j] = !occ[j] & light_reach(c0, c1, L[j], dist[j], slack[j]);
                 any_reach |= reach[j];
             }
         }
@@ -987,6 +1041,8 @@ struct rt_ctx {
     float4* d_trisph = nullptr;
     float4* d_cone_cam = nullptr;
     float4* d_cone_light = nullptr;
+    float4* d_trinrm = nullptr;
+    float4* d_tricoef = nullptr;
     float cam_key[3] = {0.f, 0.f, 0.f};
     bool cam_valid = false;
     StatsDev* d_stats = nullptr;
@@ -1057,6 +1113,8 @@ RT_EXPORT void rt_destroy(rt_ctx* c)
     hipFree(c->d_trisph);
     hipFree(c->d_cone_cam);
     hipFree(c->d_cone_light);
+    hipFree(c->d_trinrm);
+    hipFree(c->d_tricoef);
     hipFree(c->d_stats);
     hipFree(c->d_scratch);
     if (c->ev0) hipEventDestroy(c->ev0);
@@ -1167,7 +1225,9 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
     hipFree(c->d_trisph);
     hipFree(c->d_cone_cam);
     hipFree(c->d_cone_light);
-    c->d_tricam = c->d_trisph = c->d_cone_cam = c->d_cone_light = nullptr;
+    hipFree(c->d_trinrm);
+    hipFree(c->d_tricoef);
+    c->d_tricam = c->d_trisph = c->d_cone_cam = c->d_cone_light = c->d_trinrm = c->d_tricoef = nullptr;
     c->cam_valid = false;
     c->d_geom = c->d_mat = c->d_lights = c->d_tri = c->d_plane = c->d_quad = nullptr;
     c->d_translucent = nullptr;
@@ -1182,11 +1242,15 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
     HIP_TRY(c, up((void**)&c->d_quad, qua.data(), qua.size() * sizeof(float)));
     HIP_TRY(c, up((void**)&c->d_translucent, translucent.data(), translucent.size() * sizeof(int)));
     HIP_TRY(c, hipMalloc((void**)&c->d_tricam, (tri.size() / 12) * 16 * sizeof(float)));
-    // Bounding sphere per triangle (tri[] order), in double, inflated by a
-    // relative 1e-4 of the radius and of the coordinates' magnitude so the
-    // float triangle test's rounding slop near an edge stays inside it.
+    // Per triangle (tri[] order), for rt_cone_prepass: the bounding sphere of
+    // the triangle the reference tests (p0, p0 + e1, p0 + e2 with the float
+    // edges; radius measured from the float-rounded centre), the unit normal
+    // and longest edge, and the rounding-bound coefficients gS, gL, rho_cap.
+    // rho_cap = -1: det can be too inexact at the reference's 0.01 gate
+    // (longest edge >~ 110) — never culled.
     const size_t ntr = tri.size() / 12;
-    std::vector<float> sph(ntr * 4);
+    std::vector<float> sph(ntr * 4), nrm(ntr * 4), coef(ntr * 4);
+    const double eps = 0x1p-24;
     for (size_t k = 0; k < ntr; ++k) {
         const float* r = &tri[12 * k];
         double p[3][3];
@@ -1195,28 +1259,60 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
             p[1][a] = (double)r[a] + (double)r[3 + a];
             p[2][a] = (double)r[a] + (double)r[6 + a];
         }
-        double ctr[3], rad = 0, mag = 0;
-        for (int a = 0; a < 3; ++a) ctr[a] = (p[0][a] + p[1][a] + p[2][a]) / 3.0;
+        float ctr[3];
+        for (int a = 0; a < 3; ++a) ctr[a] = (float)((p[0][a] + p[1][a] + p[2][a]) / 3.0);
+        double rad = 0, L2 = 0;
         for (int q = 0; q < 3; ++q) {
             double d2 = 0;
-            for (int a = 0; a < 3; ++a) {
-                d2 += (p[q][a] - ctr[a]) * (p[q][a] - ctr[a]);
-                mag = std::max(mag, std::fabs(p[q][a]));
-            }
+            for (int a = 0; a < 3; ++a) d2 += (p[q][a] - ctr[a]) * (p[q][a] - ctr[a]);
             rad = std::max(rad, std::sqrt(d2));
+            for (int w = q + 1; w < 3; ++w) {
+                double l2 = 0;
+                for (int a = 0; a < 3; ++a) l2 += (p[q][a] - p[w][a]) * (p[q][a] - p[w][a]);
+                L2 = std::max(L2, l2);
+            }
         }
-        const double infl = rad * (1.0 + 1e-4) + 1e-4 * mag + 1e-6;
-        for (int a = 0; a < 3; ++a) sph[4 * k + a] = (float)ctr[a];
-        sph[4 * k + 3] = (float)(infl * (1.0 + 1e-6));  // round up
+        rad = rad * (1.0 + 1e-9);
+        for (int a = 0; a < 3; ++a) sph[4 * k + a] = ctr[a];
+        sph[4 * k + 3] = std::nextafter((float)rad, INFINITY);
+        const double e1[3] = {r[3], r[4], r[5]}, e2[3] = {r[6], r[7], r[8]};
+        const double nx = e1[1] * e2[2] - e1[2] * e2[1], ny = e1[2] * e2[0] - e1[0] * e2[2],
+                     nz = e1[0] * e2[1] - e1[1] * e2[0];
+        const double nn = std::sqrt(nx * nx + ny * ny + nz * nz);
+        const double L = std::sqrt(L2) * (1.0 + 1e-9);
+        const double dl = 7.0 * eps * L * L;
+        const double rho_cap = dl < 0.01 ? dl / (0.01 - dl) + 3.0 * eps : INFINITY;
+        const bool fine = nn > 0 && std::isfinite(nn) && rho_cap <= 0.5;
+        const double kk = fine ? 1.0 / (1.0 - rho_cap) : 2.0;
+        nrm[4 * k] = fine ? (float)(nx / nn) : 0.f;
+        nrm[4 * k + 1] = fine ? (float)(ny / nn) : 0.f;
+        nrm[4 * k + 2] = fine ? (float)(nz / nn) : 0.f;
+        nrm[4 * k + 3] = std::nextafter((float)L, INFINITY);
+        coef[4 * k] = fine ? (float)(54.0 * kk * eps * L * L / nn * 1.01) : 0.f;
+        coef[4 * k + 1] = fine ? (float)(21.0 * kk * eps * L * L * L / nn * 1.01) : 0.f;
+        coef[4 * k + 2] = fine ? (float)(rho_cap * 1.01) : -1.0f;
+        coef[4 * k + 3] = 0.0f;
     }
     sph.resize(std::max<size_t>(sph.size(), 4));
+    nrm.resize(std::max<size_t>(nrm.size(), 4));
+    coef.resize(std::max<size_t>(coef.size(), 4));
     HIP_TRY(c, up((void**)&c->d_trisph, sph.data(), sph.size() * sizeof(float)));
+    HIP_TRY(c, up((void**)&c->d_trinrm, nrm.data(), nrm.size() * sizeof(float)));
+    HIP_TRY(c, up((void**)&c->d_tricoef, coef.data(), coef.size() * sizeof(float)));
     HIP_TRY(c, hipMalloc((void**)&c->d_cone_cam, std::max<size_t>(ntr, 1) * 2 * sizeof(float4)));
     HIP_TRY(c, hipMalloc((void**)&c->d_cone_light, std::max<size_t>(ntr * nl, 1) * 2 * sizeof(float4)));
     for (int j = 0; j < nl && ntr > 0; ++j) {
         const float* l = s->lights + 7 * (size_t)j;
-        hipLaunchKernelGGL(rt_cone_prepass, dim3((unsigned)((ntr + 255) / 256)), dim3(256), 0, 0, c->d_trisph,
-                           (int)ntr, l[0], l[1], l[2], c->d_cone_light + 2 * ntr * j);
+        // shadow rays are culled up to 4x the light's farthest triangle
+        double far = 0;
+        for (size_t k = 0; k < ntr; ++k) {
+            double d2 = 0;
+            for (int a = 0; a < 3; ++a) d2 += ((double)sph[4 * k + a] - l[a]) * ((double)sph[4 * k + a] - l[a]);
+            far = std::max(far, std::sqrt(d2) + sph[4 * k + 3]);
+        }
+        hipLaunchKernelGGL(rt_cone_prepass, dim3((unsigned)((ntr + 255) / 256)), dim3(256), 0, 0, c->d_tri, c->d_trisph,
+                           c->d_trinrm, c->d_tricoef, (int)ntr, l[0], l[1], l[2], 0, (float)(4.0 * far),
+                           c->d_cone_light + 2 * ntr * j);
         HIP_TRY(c, hipGetLastError());
     }
     HIP_TRY(c, hipDeviceSynchronize());
@@ -1346,8 +1442,8 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
                                cp[0], cp[1], cp[2], c->d_tricam);
             HIP_TRY(c, hipGetLastError());
         }
-        hipLaunchKernelGGL(rt_cone_prepass, dim3((c->n_tri + 255) / 256), dim3(256), 0, st, c->d_trisph, c->n_tri,
-                           cp[0], cp[1], cp[2], c->d_cone_cam);
+        hipLaunchKernelGGL(rt_cone_prepass, dim3((c->n_tri + 255) / 256), dim3(256), 0, st, c->d_tri, c->d_trisph,
+                           c->d_trinrm, c->d_tricoef, c->n_tri, cp[0], cp[1], cp[2], 1, 0.0f, c->d_cone_cam);
         HIP_TRY(c, hipGetLastError());
         std::memcpy(c->cam_key, f->cam_pos, sizeof c->cam_key);
         c->cam_valid = true;

@@ -1,0 +1,60 @@
+"""Bounding-cone culling under stress (tests/cull_scenes.py): cameras and
+lights in the planes of triangles, slivers, tiny and oversized triangles, a
+far light.  The culled GPU loops must return the reference's image bit for
+bit (golden: tests/golden/cull.npz, made by make_cull_golden.py from the
+reference's own sources); the oracle is pinned against the same images."""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import pytest
+
+import cull_scenes
+from conftest import bits_equal
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.fixture(scope="module")
+def cull_golden():
+    with np.load(os.path.join(HERE, "golden", "cull.npz")) as z:
+        return {k: z[k] for k in z.files}
+
+
+def _cases():
+    with np.load(os.path.join(HERE, "golden", "cull.npz")) as z:
+        names = sorted(z.files)
+    out = []
+    for n in names:
+        seed, wh, d = n[2:].split("_")
+        w, h = map(int, wh.split("x"))
+        out.append((n, int(seed), w, h, int(d[1:])))
+    return out
+
+
+CASES = _cases()
+
+
+def _path(tmp_path, seed, depth):
+    return cull_scenes.write(str(tmp_path / f"cs{seed}_{depth}.dat"), seed, 0.3 if depth else 0.0)
+
+
+@pytest.mark.parametrize("name,seed,w,h,depth", [c for c in CASES if c[2] <= 160])
+def test_oracle_matches_reference(oracle, cull_golden, tmp_path, name, seed, w, h, depth):
+    got = oracle.render(_path(tmp_path, seed, depth), w, h, depth)
+    assert bits_equal(got, cull_golden[name])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,seed,w,h,depth", CASES)
+def test_gpu_matches_reference(cull_golden, tmp_path, name, seed, w, h, depth):
+    import rt_amd
+
+    ctx = rt_amd.Context(0)
+    s = rt_amd.Scene(_path(tmp_path, seed, depth), w, h, depth)
+    ctx.upload(s)
+    got = ctx.render_float(s.frame)
+    want = cull_golden[name]
+    bad = np.argwhere(~(got.view(np.uint32) == want.view(np.uint32)).all(-1))
+    assert bits_equal(got, want), f"{len(bad)} pixels differ, first {bad[:5].tolist()}"
