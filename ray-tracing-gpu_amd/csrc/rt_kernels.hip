@@ -455,6 +455,136 @@ __device__ __forceinline__ int closest_hit_camera(const SceneDev& S, const Vec3 
     return bi;
 }
 
+// ------------------------------------------------ wave-level (packet) culling
+// When all 64 lanes of a wave are active (checked at run time, so the result
+// never depends on how the compiler shaped the control flow), the wave's
+// rays from a common apex (the camera, or one light for shadow rays) fit in
+// one cone [w, W] (w: the centre lane's direction, cos W = min over lanes).
+// A triangle whose cone [v, T] from the same apex satisfies
+// angle(w, v) > W + T cannot be reached by any lane (spherical triangle
+// inequality), so 64 triangles are culled per wave instruction — one lane
+// per triangle — and only the ballot's survivors are tested exactly.  The
+// per-lane predicates above remain the definition; the margins here only
+// widen them (cos W lowered, sin W raised, cos(W + T) lowered by 2e-6 and by
+// the shadow ray's direction slack).
+__device__ __forceinline__ bool wave_full() { return __builtin_amdgcn_read_exec() == ~0ull; }
+
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v)
+{
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float readlanef(float v, int lane)
+{
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+// Min / max over all 64 lanes (full exec only): quad, half-row and row
+// exchanges by DPP, then the four row results.
+__device__ __forceinline__ float wave_min(float v)
+{
+    v = fminf(v, dppf<0xB1>(v));   // quad_perm [1,0,3,2]
+    v = fminf(v, dppf<0x4E>(v));   // quad_perm [2,3,0,1]
+    v = fminf(v, dppf<0x141>(v));  // row_half_mirror
+    v = fminf(v, dppf<0x140>(v));  // row_mirror
+    return fminf(fminf(readlanef(v, 0), readlanef(v, 16)), fminf(readlanef(v, 32), readlanef(v, 48)));
+}
+__device__ __forceinline__ float wave_max(float v)
+{
+    v = fmaxf(v, dppf<0xB1>(v));
+    v = fmaxf(v, dppf<0x4E>(v));
+    v = fmaxf(v, dppf<0x141>(v));
+    v = fmaxf(v, dppf<0x140>(v));
+    return fmaxf(fmaxf(readlanef(v, 0), readlanef(v, 16)), fmaxf(readlanef(v, 32), readlanef(v, 48)));
+}
+struct WaveCone {
+    Vec3 w;
+    float cosW, sinW;
+    bool ok;
+};
+// Cone of the live lanes' unit directions d (apex shared).  ok = false when
+// no lane is live or the spread exceeds 60 degrees (then W + T could pass pi).
+__device__ __forceinline__ WaveCone wave_cone(const Vec3 d, bool live)
+{
+    WaveCone c;
+    const unsigned long long lm = __ballot(live);
+    c.ok = lm != 0;
+    if (!c.ok) return c;
+    const int ref = ((lm >> 36) & 1ull) ? 36 : (int)__builtin_ctzll(lm);
+    c.w = make3(readlanef(d.x, ref), readlanef(d.y, ref), readlanef(d.z, ref));
+    float cd = dot(d, c.w);
+    cd = live ? (cd == cd ? cd : -1.0f) : 1.0f;
+    c.cosW = wave_min(cd) - 1e-6f;
+    c.ok = c.cosW >= 0.5f;
+    c.sinW = sqrtf(fmaxf(0.0f, 1.0f - c.cosW * c.cosW)) + 1e-6f;
+    return c;
+}
+// May some ray of the wave cone reach the triangle cone [c0.xyz, c0.w; c1.w]?
+// ang = extra angular slack.
+__device__ __forceinline__ bool cone_overlap(const WaveCone& wc, const float4 c0, float sinT, float ang)
+{
+    const float lim = wc.cosW * c0.w - wc.sinW * sinT - 2e-6f - ang;
+    return !(c0.w > 0.0f) | (dot(wc.w, make3(c0.x, c0.y, c0.z)) >= lim);
+}
+
+// Closest hit for camera rays, wave-culled (full wave, cone ok).
+__device__ __forceinline__ int closest_hit_camera_wave(const SceneDev& S, const WaveCone& wc, const Vec3 O,
+                                                       const Vec3 D, float& best_t)
+{
+    float bt = -1.0f;
+    int bi = -1;
+    const int lane = (int)(threadIdx.x & 63);
+    for (int k0 = 0; k0 < S.n_tri; k0 += 64) {
+        const int k = k0 + lane;
+        bool reach = false;
+        if (k < S.n_tri) {
+            const float4 c0 = S.cone_cam[2 * k], c1 = S.cone_cam[2 * k + 1];
+            reach = cone_overlap(wc, c0, c1.w, 0.0f);
+        }
+        unsigned long long m = __ballot(reach);
+        while (m) {
+            const int kk = k0 + (int)__builtin_ctzll(m);
+            m &= m - 1;
+            if (S.use_tricam) {
+                const float4* r = S.tricam + 4 * kk;
+                camera_tri(r[0], r[1], r[2], r[3], D, bt, bi);
+            } else {
+                const TriRec tr = load_tri(S, kk);
+                const TriU r = tri_u(tr.p0, tr.e1, tr.e2, O, D);
+                if (!__any(r.ok)) continue;
+                float t;
+                const bool ok = tri_vt(r, tr.e1, tr.e2, D, t);
+                take_min(ok, t, tr.idx, bt, bi);
+            }
+        }
+    }
+    for (int k = 0; k < S.n_plane; ++k) {
+        const float4 a = S.plane[2 * k], b = S.plane[2 * k + 1];
+        float t;
+        const bool ok = hit_plane(make_float4(0.f, a.x, a.y, a.z), make_float4(a.w, 0.f, 0.f, 0.f), O, D, t);
+        take_min(ok, t, __float_as_int(b.x), bt, bi);
+    }
+    for (int k = 0; k < S.n_quad; ++k) {
+        const float4* r = S.quad + 3 * k;
+        const float4 a = r[0], b = r[1], c = r[2];
+        float t;
+        const bool ok = hit_quadric(make_float4(0.f, a.x, a.y, a.z), make_float4(a.w, b.x, b.y, b.z),
+                                    make_float4(b.w, c.x, c.y, 0.f), O, D, t);
+        take_min(ok, t, __float_as_int(c.z), bt, bi);
+    }
+    best_t = bt;
+    return bi;
+}
+
+// Primary rays: wave-culled when the whole wave is here, else per lane.
+__device__ __forceinline__ int closest_hit_primary(const SceneDev& S, const Vec3 O, const Vec3 D, float& t)
+{
+    if (wave_full()) {
+        const WaveCone wc = wave_cone(D, true);
+        if (wc.ok) return closest_hit_camera_wave(S, wc, O, D, t);
+    }
+    return S.use_tricam ? closest_hit_camera(S, O, D, t) : closest_hit<true>(S, O, D, t);
+}
+
 // tricam[] for camera position C (one thread per triangle).
 __global__ void rt_camera_prepass(const float4* __restrict__ tri, int n, float cx, float cy, float cz,
                                   float4* __restrict__ tricam)
@@ -498,9 +628,10 @@ __global__ void rt_camera_prepass(const float4* __restrict__ tri, int n, float c
 // a sphere behind the light.  Rounding of the cull test itself: radius
 // + 2e-5 dv, cosine - 2e-5.
 //
-//   camera: c0 = [dir to centre, cosT]   (c1 unused)
-//   light : c0 = [dir to centre, cosT]   c1 = [dmin, 2/dmin, dcap, 0]
-// "always test": cosT = -2, dmin = dcap = -inf.
+//   camera: c0 = [dir to centre, cosT]   c1 = [0, 0, 0, sinT]
+//   light : c0 = [dir to centre, cosT]   c1 = [dmin, 2/dmin, dcap, sinT]
+// (sinT >= sin of the angle whose cosine is cosT, for the wave-level test)
+// "always test": cosT = -2, sinT = 2, dmin = dcap = -inf.
 __global__ void rt_cone_prepass(const float4* __restrict__ tri, const float4* __restrict__ sph,
                                 const float4* __restrict__ nrm, const float4* __restrict__ coef, int n, float ax,
                                 float ay, float az, int camera, float dtarget, float4* __restrict__ out)
@@ -521,14 +652,18 @@ __global__ void rt_cone_prepass(const float4* __restrict__ tri, const float4* __
     if (h_eff > 1.01 * G) m = fmax(m, 1.001 * (h_eff * tau + 1.01 * G * Rp) / (h_eff - 1.01 * G));
     const double rc = r0 + m + 2e-5 * dv;  // cone radius
     float4 c0 = make_float4(0.f, 0.f, 0.f, -2.0f);
-    float4 c1 = make_float4(-INFINITY, 0.f, -INFINITY, 0.f);
+    float4 c1 = make_float4(-INFINITY, 0.f, -INFINITY, 2.0f);
     if (rho_cap >= 0.0 && h_eff > 1.01 * G && m <= 10.0 * r0 && m > 2.0 * tau && dv - rc > m / 3.0 + 0.02 &&
         isfinite(dv) && isfinite(gS) && isfinite(gL)) {
         const double phi = 1.01 * (m + Rp) / (m - tau);
         const double cosT = sqrt(1.0 - (rc / dv) * (rc / dv)) - 2e-5;
         const float4 cone = make_float4((float)(vx / dv), (float)(vy / dv), (float)(vz / dv), (float)cosT);
+        const float sinT = (float)(sqrt(fmax(0.0, 1.0 - (double)cone.w * cone.w)) + 1e-7);
         if (camera) {
-            if (h_eff >= (gS * (dv + r0) + gL) * phi) c0 = cone;
+            if (h_eff >= (gS * (dv + r0) + gL) * phi) {
+                c0 = cone;
+                c1 = make_float4(0.f, 0.f, 0.f, sinT);
+            }
         } else {
             const double dmin = (dv - rc - m / 3.0) * (1.0 - 1e-5);
             const double dcap1 = ((h_eff / phi - gL) / gS - dv - r0) / 1.0001;
@@ -538,7 +673,7 @@ __global__ void rt_cone_prepass(const float4* __restrict__ tri, const float4* __
             const double dcap = fmin(fmin(dcap1, dcap2), 1000.0 * h);
             if (dcap > 0.0) {
                 c0 = cone;
-                c1 = make_float4((float)dmin, (float)(2.0 / dmin), (float)(dcap * (1.0 - 1e-6)), 0.f);
+                c1 = make_float4((float)dmin, (float)(2.0 / dmin), (float)(dcap * (1.0 - 1e-6)), sinT);
             }
         }
     }
@@ -775,6 +910,88 @@ __device__ __forceinline__ void shadow_opaque_batch(const SceneDev& S, int l0, i
     }
 }
 
+// shadow_opaque_batch with wave-level culling (full wave; every light of the
+// batch with a live lane must have ok cones — else the caller uses the
+// per-lane form).  Same any-hit results: a triangle no lane of the wave can
+// reach is skipped, the rest are tested exactly per lane.
+template <int kLightBatch>
+__device__ __forceinline__ void shadow_opaque_wave(const SceneDev& S, int l0, int nl, const Vec3 P,
+                                                   const Vec3 (&L)[kLightBatch], const float (&dist)[kLightBatch],
+                                                   bool (&occ)[kLightBatch], const WaveCone (&wc)[kLightBatch],
+                                                   const float (&dmax)[kLightBatch])
+{
+    const float4* cone = S.cone_light + 2 * (size_t)S.n_tri * l0;
+    const size_t cstride = 2 * (size_t)S.n_tri;
+    const int lane = (int)(threadIdx.x & 63);
+    for (int k0 = 0; k0 < S.n_tri_opaque; k0 += 64) {
+        bool live = false;
+#pragma unroll
+        for (int j = 0; j < kLightBatch; ++j) live |= (j < nl) & !occ[j];
+        if (!__any(live)) break;
+        const int k = k0 + lane;
+        unsigned long long mj[kLightBatch], m = 0;
+#pragma unroll
+        for (int j = 0; j < kLightBatch; ++j) {
+            mj[j] = 0;
+            if (j < nl && wc[j].ok) {
+                bool reach = false;
+                if (k < S.n_tri_opaque) {
+                    const float4 c0 = cone[cstride * j + 2 * k], c1 = cone[cstride * j + 2 * k + 1];
+                    reach = ((c1.x < dmax[j]) & cone_overlap(wc[j], c0, c1.w, dmax[j] * 1e-6f * c1.y)) |
+                            (dmax[j] > c1.z);
+                }
+                mj[j] = __ballot(reach);
+                m |= mj[j];
+            }
+        }
+        while (m) {
+            const int b = (int)__builtin_ctzll(m);
+            m &= m - 1;
+            const TriRec tr = load_tri(S, k0 + b);
+            const Vec3 Sv = P - tr.p0;
+            const Vec3 Q = cross(Sv, tr.e1);
+            const float tq = dot(tr.e2, Q);
+#pragma unroll
+            for (int j = 0; j < kLightBatch; ++j) {
+                if (((mj[j] >> b) & 1ull) && __any(!occ[j])) {
+                    const Vec3 Pv = cross(L[j], tr.e2);
+                    const float det = dot(tr.e1, Pv);
+                    const float inv = recip_det(det);
+                    const float u = dot(Sv, Pv) * inv;
+                    const float v = dot(L[j], Q) * inv;
+                    const float t = tq * inv;
+                    const bool ok = !(fabsf(det) < kEps) & !((u < 0) | (u > 1)) & !((v < 0) | (u + v > 1));
+                    occ[j] |= ok & (t > kEps) & (t < dist[j]);
+                }
+            }
+        }
+    }
+    for (int k = 0; k < S.n_plane_opaque; ++k) {
+        const float4 a = S.plane[2 * k];
+#pragma unroll
+        for (int j = 0; j < kLightBatch; ++j) {
+            if (j < nl && __any(!occ[j])) {
+                float t;
+                const bool ok = hit_plane(make_float4(0.f, a.x, a.y, a.z), make_float4(a.w, 0.f, 0.f, 0.f), P, L[j], t);
+                occ[j] |= ok & (t > kEps) & (t < dist[j]);
+            }
+        }
+    }
+    for (int k = 0; k < S.n_quad_opaque; ++k) {
+        const float4* r = S.quad + 3 * k;
+        const float4 a = r[0], b = r[1], c = r[2];
+#pragma unroll
+        for (int j = 0; j < kLightBatch; ++j) {
+            if (j < nl && __any(!occ[j])) {
+                float t;
+                const bool ok = hit_quadric(make_float4(0.f, a.x, a.y, a.z), make_float4(a.w, b.x, b.y, b.z),
+                                            make_float4(b.w, c.x, c.y, 0.f), P, L[j], t);
+                occ[j] |= ok & (t > kEps) & (t < dist[j]);
+            }
+        }
+    }
+}
+
 // Scene.cpp:1742-1777: ambient + every light (N.L gate on the unnormalised
 // light vector, filter, Lambert "Gouraud" term, Phong term).  Lights are
 // accumulated strictly in file order; only the filters of a batch of lights
@@ -799,14 +1016,16 @@ __device__ __forceinline__ void add_light(Color& res, const Mat& m, const float4
 
 template <int kLightBatch, bool PF>
 __device__ __forceinline__ Color shade_local(const SceneDev& S, const Mat& m, const Vec3 P, const Vec3 N,
-                                             const Vec3 D, Counters& cnt)
+                                             const Vec3 D, Counters& cnt, bool active = true)
 {
+    // active = false: a lane kept in step with its wave (no hit / outside the
+    // frame) whose result is discarded; it casts no shadow rays.
     Color res = m.color * m.ka;
     if (!S.shadow_split) {
         for (int li = 0; li < S.n_lights; ++li) {
             const float4 l0 = S.lights[2 * li], l1 = S.lights[2 * li + 1];
             Vec3 L = make3(l0.x, l0.y, l0.z) - P;
-            if (dot(L, N) > 0) {
+            if (active && dot(L, N) > 0) {
                 ++cnt.shadow;
                 const Color F = shadow_filter(S, li, P, L, cnt.skipped);
                 add_light(res, m, l0, l1, N, L, D, F);
@@ -827,14 +1046,30 @@ __device__ __forceinline__ Color shade_local(const SceneDev& S, const Mat& m, co
             if (j < nl) {
                 const float4 l0 = S.lights[2 * (lb + j)];
                 const Vec3 Lr = make3(l0.x, l0.y, l0.z) - P;
-                gate[j] = dot(Lr, N) > 0;          // Scene.cpp:1756, unnormalised
+                gate[j] = active & (dot(Lr, N) > 0);  // Scene.cpp:1756, unnormalised
                 dist[j] = norm(Lr);                // Scene.cpp:1847-1848
                 L[j] = div_recip(Lr, dist[j]);
                 cnt.shadow += gate[j];
             }
             occ[j] = !gate[j];
         }
-        shadow_opaque_batch<kLightBatch, PF>(S, lb, nl, P, L, dist, occ);
+        bool use_wave = wave_full();
+        WaveCone wc[kLightBatch];
+        float dmax[kLightBatch];
+        if (use_wave) {
+#pragma unroll
+            for (int j = 0; j < kLightBatch; ++j) {
+                wc[j].ok = false;
+                dmax[j] = 0.0f;
+                if (j < nl) {
+                    wc[j] = wave_cone(-L[j], gate[j]);  // directions from the light
+                    dmax[j] = wave_max(gate[j] ? (dist[j] == dist[j] ? dist[j] : INFINITY) : 0.0f);
+                    use_wave &= wc[j].ok | !__any(gate[j]);
+                }
+            }
+        }
+        if (use_wave) shadow_opaque_wave<kLightBatch>(S, lb, nl, P, L, dist, occ, wc, dmax);
+        else shadow_opaque_batch<kLightBatch, PF>(S, lb, nl, P, L, dist, occ);
 #pragma unroll
         for (int j = 0; j < kLightBatch; ++j) {
             if (j < nl && gate[j]) {
@@ -864,7 +1099,7 @@ struct Frame {
 };
 
 template <int MAXD, int LB, bool PF>
-__device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, Counters& cnt)
+__device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, Counters& cnt, bool live)
 {
     const Color bg{F.bg[0], F.bg[1], F.bg[2]};
     if constexpr (MAXD == 0) {
@@ -872,15 +1107,20 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
         return Color{D.x, D.y, D.z};
 #endif
         float t;
-        const int idx = S.use_tricam ? closest_hit_camera(S, O, D, t) : closest_hit<true>(S, O, D, t);
-        if (idx < 0) return bg;
+        const int idx = closest_hit_primary(S, O, D, t);
+        // Lanes that miss (or lie outside the frame) stay in step through the
+        // shading so the wave stays whole for wave-level shadow culling.
+        const bool hit = idx >= 0;
+        if (!__any(hit & live)) return bg;
 #ifdef RT_ABLATE_SHADE  // timing-only build: primary closest hit only
         return Color{t, (float)idx, 0.f};
 #endif
-        const Vec3 N = hit_normal(S, idx, O, D, t);
-        const Mat m = load_mat(S, idx);
+        const int sidx = hit ? idx : 0;
+        const Vec3 N = hit_normal(S, sidx, O, D, t);
+        const Mat m = load_mat(S, sidx);
         const Vec3 P = O + t * D;
-        return shade_local<LB, PF>(S, m, P, N, D, cnt);
+        const Color c = shade_local<LB, PF>(S, m, P, N, D, cnt, hit & live);
+        return hit ? c : bg;
     } else {
         Frame stk[MAXD];
         int sp = 0;
@@ -890,8 +1130,7 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
         for (;;) {
             if (trace) {
                 float t;
-                const int idx = camera_ray ? (S.use_tricam ? closest_hit_camera(S, O, D, t) : closest_hit<true>(S, O, D, t))
-                                           : closest_hit<false>(S, O, D, t);
+                const int idx = camera_ray ? closest_hit_primary(S, O, D, t) : closest_hit<false>(S, O, D, t);
                 camera_ray = false;
                 ret = bg;
                 if (idx >= 0) {
@@ -991,23 +1230,29 @@ __global__ __launch_bounds__(256) void rt_trace_kernel(const SceneDev S, const F
 
     Counters cnt;
     Color c{0.f, 0.f, 0.f};
-    if (valid) {
+    // Without bounces every lane runs (lanes outside the frame on a clamped
+    // pixel, result dropped) so edge waves stay whole for wave-level culling.
+    if (MAXD == 0 || valid) {
+        const int pxc = px < F.width ? px : F.width - 1;
+        const int pyc = py < F.row_end ? py : F.row_end - 1;
         // Scene.cpp:1543-1552: (float)(2*PixX) * InvW - 1, then * HalfW
-        const Vec3 d0 = make3((2 * px * F.inv_w - 1) * F.half_w, (2 * py * F.inv_h - 1) * F.half_h, -1.0f);
+        const Vec3 d0 = make3((2 * pxc * F.inv_w - 1) * F.half_w, (2 * pyc * F.inv_h - 1) * F.half_h, -1.0f);
         Mat4 M;
 #pragma unroll
         for (int i = 0; i < 16; ++i) M.m[i >> 2][i & 3] = F.orient[i];
         const Vec3 D = normalize(d0 * M);
         const Vec3 O = make3(F.cam[0], F.cam[1], F.cam[2]);
-        cnt.primary = 1;
-        c = radiance<MAXD, LB, PF>(S, F, O, D, cnt);
-        const size_t o = (size_t)ly * F.width + px;
-        if (rgbf) {
-            rgbf[3 * o] = c.r;
-            rgbf[3 * o + 1] = c.g;
-            rgbf[3 * o + 2] = c.b;
+        cnt.primary = valid ? 1u : 0u;
+        c = radiance<MAXD, LB, PF>(S, F, O, D, cnt, valid);
+        if (valid) {
+            const size_t o = (size_t)ly * F.width + px;
+            if (rgbf) {
+                rgbf[3 * o] = c.r;
+                rgbf[3 * o + 1] = c.g;
+                rgbf[3 * o + 2] = c.b;
+            }
+            if (rgba) rgba[o] = unorm8(c.r) | (unorm8(c.g) << 8) | (unorm8(c.b) << 16) | 0xFF000000u;
         }
-        if (rgba) rgba[o] = unorm8(c.r) | (unorm8(c.g) << 8) | (unorm8(c.b) << 16) | 0xFF000000u;
     }
     if (F.flags & RT_FLAG_STATS) {
         atomicAdd(&stats->primary, (unsigned long long)cnt.primary);
