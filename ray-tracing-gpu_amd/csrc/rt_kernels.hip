@@ -576,9 +576,10 @@ __device__ __forceinline__ int closest_hit_camera_wave(const SceneDev& S, const 
 }
 
 // Primary rays: wave-culled when the whole wave is here, else per lane.
+template <bool WAVE>
 __device__ __forceinline__ int closest_hit_primary(const SceneDev& S, const Vec3 O, const Vec3 D, float& t)
 {
-    if (wave_full()) {
+    if (WAVE && wave_full()) {
         const WaveCone wc = wave_cone(D, true);
         if (wc.ok) return closest_hit_camera_wave(S, wc, O, D, t);
     }
@@ -1014,7 +1015,7 @@ __device__ __forceinline__ void add_light(Color& res, const Mat& m, const float4
     }
 }
 
-template <int kLightBatch, bool PF>
+template <int kLightBatch, bool PF, bool WAVE>
 __device__ __forceinline__ Color shade_local(const SceneDev& S, const Mat& m, const Vec3 P, const Vec3 N,
                                              const Vec3 D, Counters& cnt, bool active = true)
 {
@@ -1053,7 +1054,7 @@ __device__ __forceinline__ Color shade_local(const SceneDev& S, const Mat& m, co
             }
             occ[j] = !gate[j];
         }
-        bool use_wave = wave_full();
+        bool use_wave = WAVE && wave_full();
         WaveCone wc[kLightBatch];
         float dmax[kLightBatch];
         if (use_wave) {
@@ -1098,7 +1099,7 @@ struct Frame {
     int surf, stage;
 };
 
-template <int MAXD, int LB, bool PF>
+template <int MAXD, int LB, bool PF, bool WAVE>
 __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, Counters& cnt, bool live)
 {
     const Color bg{F.bg[0], F.bg[1], F.bg[2]};
@@ -1107,7 +1108,7 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
         return Color{D.x, D.y, D.z};
 #endif
         float t;
-        const int idx = closest_hit_primary(S, O, D, t);
+        const int idx = closest_hit_primary<WAVE>(S, O, D, t);
         // Lanes that miss (or lie outside the frame) stay in step through the
         // shading so the wave stays whole for wave-level shadow culling.
         const bool hit = idx >= 0;
@@ -1119,7 +1120,7 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
         const Vec3 N = hit_normal(S, sidx, O, D, t);
         const Mat m = load_mat(S, sidx);
         const Vec3 P = O + t * D;
-        const Color c = shade_local<LB, PF>(S, m, P, N, D, cnt, hit & live);
+        const Color c = shade_local<LB, PF, WAVE>(S, m, P, N, D, cnt, hit & live);
         return hit ? c : bg;
     } else {
         Frame stk[MAXD];
@@ -1130,14 +1131,14 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
         for (;;) {
             if (trace) {
                 float t;
-                const int idx = camera_ray ? closest_hit_primary(S, O, D, t) : closest_hit<false>(S, O, D, t);
+                const int idx = camera_ray ? closest_hit_primary<WAVE>(S, O, D, t) : closest_hit<false>(S, O, D, t);
                 camera_ray = false;
                 ret = bg;
                 if (idx >= 0) {
                     const Vec3 N = hit_normal(S, idx, O, D, t);
                     const Mat m = load_mat(S, idx);
                     const Vec3 P = O + t * D;
-                    const Color acc = shade_local<LB, PF>(S, m, P, N, D, cnt);
+                    const Color acc = shade_local<LB, PF, WAVE>(S, m, P, N, D, cnt);
                     // Scene.cpp:1779-1781 / :1790-1792 gates; bounces == sp
                     const float er = m.kr * energy;
                     const float et = m.kt * energy;
@@ -1217,7 +1218,7 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
     }
 }
 
-template <int MAXD, int LB, bool PF>
+template <int MAXD, int LB, bool PF, bool WAVE>
 __global__ __launch_bounds__(256) void rt_trace_kernel(const SceneDev S, const FrameDev F, unsigned* __restrict__ rgba,
                                                        float* __restrict__ rgbf, StatsDev* __restrict__ stats)
 {
@@ -1243,7 +1244,7 @@ __global__ __launch_bounds__(256) void rt_trace_kernel(const SceneDev S, const F
         const Vec3 D = normalize(d0 * M);
         const Vec3 O = make3(F.cam[0], F.cam[1], F.cam[2]);
         cnt.primary = valid ? 1u : 0u;
-        c = radiance<MAXD, LB, PF>(S, F, O, D, cnt, valid);
+        c = radiance<MAXD, LB, PF, WAVE>(S, F, O, D, cnt, valid);
         if (valid) {
             const size_t o = (size_t)ly * F.width + px;
             if (rgbf) {
@@ -1607,26 +1608,31 @@ static constexpr int kTricamMaxTriangles = 256;
 
 typedef void (*kernel_fn)(const SceneDev, const FrameDev, unsigned*, float*, StatsDev*);
 
-// Kernel variants (tools/ab_variants.py, MI355X): small triangle lists
-// batch 3 lights per shadow pass (C2 -4%); big lists (> 256 triangles) run
-// one light per pass with the next cone record prefetched in flight
-// (C3 -15%); bounce kernels use neither (each regressed scene7 by 4%).
-static kernel_fn pick_kernel(int depth, bool big, int n_lights, int& cap, int& lb)
+// Kernel variants (tools/ab_variants.py, MI355X).  Without bounces and with
+// triangles: wave-level culling, RT_WAVE_LB lights per shadow pass.  Without
+// triangles nothing is culled: small light batches as before.  Bounce
+// kernels: per-lane culling, one light per pass (LB 3 / prefetch each
+// regressed scene7 by 4%).
+#ifndef RT_WAVE_LB
+#define RT_WAVE_LB 2
+#endif
+static kernel_fn pick_kernel(int depth, int n_tri, int n_lights, int& cap, int& lb)
 {
     lb = 1;
-    if (depth == 0 && big) {
+    if (depth == 0 && n_tri > 0) {
         cap = 0;
-        return (kernel_fn)&rt_trace_kernel<0, 1, true>;
+        lb = RT_WAVE_LB;
+        return (kernel_fn)&rt_trace_kernel<0, RT_WAVE_LB, false, true>;
     }
     if (depth == 0 && n_lights > 1) {
         cap = 0;
         lb = 3;
-        return (kernel_fn)&rt_trace_kernel<0, 3, false>;
+        return (kernel_fn)&rt_trace_kernel<0, 3, false, false>;
     }
-#define RT_PICK(N)                                          \
-    if (depth <= N) {                                       \
-        cap = N;                                            \
-        return (kernel_fn)&rt_trace_kernel<N, 1, false>;    \
+#define RT_PICK(N)                                                 \
+    if (depth <= N) {                                              \
+        cap = N;                                                   \
+        return (kernel_fn)&rt_trace_kernel<N, 1, false, false>;    \
     }
     RT_STACK_DEPTHS(RT_PICK)
 #undef RT_PICK
@@ -1648,7 +1654,7 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
     }
     const int depth = reachable_depth(c, f);
     int cap = 0, lb = 1;
-    kernel_fn k = pick_kernel(depth, c->n_tri > kTricamMaxTriangles, c->n_lights, cap, lb);
+    kernel_fn k = pick_kernel(depth, c->n_tri, c->n_lights, cap, lb);
     if (!k) {
         c->err = "reachable bounce depth " + std::to_string(depth) + " exceeds the compiled stack (32)";
         return RT_E_UNSUPPORTED;
