@@ -59,6 +59,13 @@ namespace rt {
 // hoisted to upload time: same operands, same IEEE subtraction, same bits.
 // Material (3 x float4): [r g b Ka] [Kd Ks shin Kr] [Kt ior 0 0]
 // Light    (2 x float4): [x y z I]  [r g b 0]
+// Cone records per apex, rt_cone_prepass: kConeRec float4 per triangle, as
+// [2 x n_tri: c0 c1 per triangle][3 x n_tri: the three edge planes].
+constexpr int kConeRec = 5;
+#ifndef RT_EDGES
+#define RT_EDGES 1
+#endif
+
 struct SceneDev {
     const float4* __restrict__ geom;    // file order, 64-byte records (above)
     const float4* __restrict__ mat;
@@ -82,12 +89,16 @@ struct SceneDev {
     // scalar cache they win (C2: -3%), past it the extra misses lose (C3: +10%,
     // tools/ab_variants.py), so the host enables them for small lists only.
     int use_tricam;
+    // wave-level edge-plane test on sphere survivors (small triangle lists:
+    // loose spheres of large triangles; on big lists it costs more than it
+    // culls — C2 -22%, C3 +14%, tools/ab_variants.py)
+    int use_edges;
     // Bounding-cone culling (exact: it only skips triangles no lane's ray can
     // reach).  Per (apex, triangle), 2 float4: [dir-to-sphere-centre, cosT]
     // [distance from the apex to the sphere, 1/that, 0, 0], where the sphere
     // bounds the triangle (inflated for float slop) and cosT is the cosine of
     // the half-angle it subtends from the apex minus a margin.  Apex = the
-    // camera (cone_cam) or light l (cone_light + 2*n_tri*l).
+    // camera (cone_cam) or light l (cone_light + kConeRec*n_tri*l).
     const float4* __restrict__ cone_cam;
     const float4* __restrict__ cone_light;
     int n_surf, n_lights;
@@ -515,7 +526,7 @@ __device__ __forceinline__ WaveCone wave_cone(const Vec3 d, bool live)
     cd = live ? (cd == cd ? cd : -1.0f) : 1.0f;
     c.cosW = wave_min(cd) - 1e-6f;
     c.ok = c.cosW >= 0.5f;
-    c.sinW = sqrtf(fmaxf(0.0f, 1.0f - c.cosW * c.cosW)) + 1e-6f;
+    c.sinW = __builtin_amdgcn_sqrtf(fmaxf(0.0f, 1.0f - c.cosW * c.cosW)) + 1e-6f;
     return c;
 }
 // May some ray of the wave cone reach the triangle cone [c0.xyz, c0.w; c1.w]?
@@ -524,6 +535,21 @@ __device__ __forceinline__ bool cone_overlap(const WaveCone& wc, const float4 c0
 {
     const float lim = wc.cosW * c0.w - wc.sinW * sinT - 2e-6f - ang;
     return !(c0.w > 0.0f) | (dot(wc.w, make3(c0.x, c0.y, c0.z)) >= lim);
+}
+
+// May some ray of the wave cone pass on the inner side (up to the margin
+// in e.w) of one edge plane [e.xyz, e.w]?  max over the cone of d . n is
+// 1 if the cone contains n, else cos(angle(w, n) - W).
+__device__ __forceinline__ bool edge_open(const WaveCone& wc, const float4 e, float ang)
+{
+    const float c = dot(wc.w, make3(e.x, e.y, e.z));
+    const float sn = __builtin_amdgcn_sqrtf(fmaxf(0.0f, 1.0f - c * c)) + 1e-6f;
+    const float mx = c >= wc.cosW ? 1.0f : c * wc.cosW + sn * wc.sinW;
+    return !(mx + 2e-6f + ang < e.w);
+}
+__device__ __forceinline__ bool edges_open(const WaveCone& wc, const float4* e, float ang)
+{
+    return edge_open(wc, e[0], ang) & edge_open(wc, e[1], ang) & edge_open(wc, e[2], ang);
 }
 
 // Closest hit for camera rays, wave-culled (full wave, cone ok).
@@ -535,11 +561,14 @@ __device__ __forceinline__ int closest_hit_camera_wave(const SceneDev& S, const 
     const int lane = (int)(threadIdx.x & 63);
     for (int k0 = 0; k0 < S.n_tri; k0 += 64) {
         const int k = k0 + lane;
-        bool reach = false;
+        float4 c0 = make_float4(0.f, 0.f, 0.f, 1.f), c1 = make_float4(0.f, 0.f, 0.f, 0.f);  // no reach
         if (k < S.n_tri) {
-            const float4 c0 = S.cone_cam[2 * k], c1 = S.cone_cam[2 * k + 1];
-            reach = cone_overlap(wc, c0, c1.w, 0.0f);
+            c0 = S.cone_cam[2 * k];
+            c1 = S.cone_cam[2 * k + 1];
         }
+        bool reach = cone_overlap(wc, c0, c1.w, 0.0f);
+        // edge records only for sphere survivors
+        if (RT_EDGES && S.use_edges && reach) reach = edges_open(wc, S.cone_cam + 2 * S.n_tri + 3 * k, 0.0f);
         unsigned long long m = __ballot(reach);
         while (m) {
             const int kk = k0 + (int)__builtin_ctzll(m);
@@ -631,8 +660,17 @@ __global__ void rt_camera_prepass(const float4* __restrict__ tri, int n, float c
 //
 //   camera: c0 = [dir to centre, cosT]   c1 = [0, 0, 0, sinT]
 //   light : c0 = [dir to centre, cosT]   c1 = [dmin, 2/dmin, dcap, sinT]
+//   edges : [n_e, lim] for the three edges (wave-level test only; stored
+//           after the n_tri [c0 c1] pairs)
 // (sinT >= sin of the angle whose cosine is cosT, for the wave-level test)
-// "always test": cosT = -2, sinT = 2, dmin = dcap = -inf.
+// "always test": cosT = -2, sinT = 2, dmin = dcap = -inf, lim = -4.
+//
+// Edge planes: the plane through A and edge e of the triangle, unit normal
+// n_e pointing at the third vertex.  A reported hit puts the crossing X
+// within m of the triangle (above), so on the inner side of every edge plane
+// up to m, at distance >= s_min = dv - r - m from A: the direction d from A
+// has d . n_e >= -m / s_min =: lim for all three edges.  A wave whose cone
+// has max d . n_e < lim for some edge reaches no point of the triangle.
 __global__ void rt_cone_prepass(const float4* __restrict__ tri, const float4* __restrict__ sph,
                                 const float4* __restrict__ nrm, const float4* __restrict__ coef, int n, float ax,
                                 float ay, float az, int camera, float dtarget, float4* __restrict__ out)
@@ -678,8 +716,39 @@ __global__ void rt_cone_prepass(const float4* __restrict__ tri, const float4* __
             }
         }
     }
+    float4 ce[3];
+    for (int e = 0; e < 3; ++e) ce[e] = make_float4(0.f, 0.f, 0.f, -4.0f);
+    if (c0.w > 0.0f) {  // a culled pair: add its edge planes
+        const float4 b1 = tri[3 * k + 1], c2r = tri[3 * k + 2];
+        const double V[3][3] = {{p0.x, p0.y, p0.z},
+                                {(double)p0.x + p0.w, (double)p0.y + b1.x, (double)p0.z + b1.y},
+                                {(double)p0.x + b1.z, (double)p0.y + b1.w, (double)p0.z + c2r.x}};
+        const double smin = dv - r0 - m;
+        const float lim = (float)(-m / smin - 1e-5);
+        bool good = smin > 0.0;
+        for (int e = 0; e < 3 && good; ++e) {
+            const int i = e, j = (e + 1) % 3, q = (e + 2) % 3;
+            const double ax_ = V[i][0] - ax, ay_ = V[i][1] - ay, az_ = V[i][2] - az;
+            const double bx_ = V[j][0] - ax, by_ = V[j][1] - ay, bz_ = V[j][2] - az;
+            double nx = ay_ * bz_ - az_ * by_, ny = az_ * bx_ - ax_ * bz_, nz = ax_ * by_ - ay_ * bx_;
+            const double nn = sqrt(nx * nx + ny * ny + nz * nz);
+            const double side = nx * (V[q][0] - ax) + ny * (V[q][1] - ay) + nz * (V[q][2] - az);
+            if (!(nn > 0.0) || !isfinite(nn) || side == 0.0) {
+                good = false;
+                break;
+            }
+            const double sg = side > 0.0 ? 1.0 : -1.0;
+            ce[e] = make_float4((float)(sg * nx / nn), (float)(sg * ny / nn), (float)(sg * nz / nn), lim);
+        }
+        if (!good)
+            for (int e = 0; e < 3; ++e) ce[e] = make_float4(0.f, 0.f, 0.f, -4.0f);
+    }
     out[2 * k] = c0;
     out[2 * k + 1] = c1;
+    float4* oe = out + 2 * (size_t)n + 3 * k;
+    oe[0] = ce[0];
+    oe[1] = ce[1];
+    oe[2] = ce[2];
 }
 
 // Shadow-ray cull predicate (L normalised towards the light, dist to it):
@@ -745,7 +814,7 @@ __device__ __forceinline__ Color shadow_filter(const SceneDev& S, int light, con
     // counting once occluded; the wave leaves a loop once all lanes are.
     bool occluded = false;
     int done = 0, total = S.n_tri_opaque + S.n_plane_opaque + S.n_quad_opaque;
-    const float4* cone = S.cone_light + 2 * (size_t)S.n_tri * light;
+    const float4* cone = S.cone_light + kConeRec * (size_t)S.n_tri * light;
     // The float ray P + t*L (L normalised, |L - exact| <= ~6 ulp) can stray
     // from the exact segment to the light by <= dist * 1e-6 at distance
     // >= cone.y from the light: widen each lane's cone by that angle.
@@ -812,8 +881,8 @@ __device__ __forceinline__ void shadow_opaque_batch(const SceneDev& S, int l0, i
                                                     const Vec3 (&L)[kLightBatch], const float (&dist)[kLightBatch],
                                                     bool (&occ)[kLightBatch])
 {
-    const float4* cone = S.cone_light + 2 * (size_t)S.n_tri * l0;
-    const size_t cstride = 2 * (size_t)S.n_tri;
+    const float4* cone = S.cone_light + kConeRec * (size_t)S.n_tri * l0;
+    const size_t cstride = kConeRec * (size_t)S.n_tri;
     float slack[kLightBatch];
 #pragma unroll
     for (int j = 0; j < kLightBatch; ++j) slack[j] = dist[j] * 1e-6f;
@@ -921,8 +990,8 @@ __device__ __forceinline__ void shadow_opaque_wave(const SceneDev& S, int l0, in
                                                    bool (&occ)[kLightBatch], const WaveCone (&wc)[kLightBatch],
                                                    const float (&dmax)[kLightBatch])
 {
-    const float4* cone = S.cone_light + 2 * (size_t)S.n_tri * l0;
-    const size_t cstride = 2 * (size_t)S.n_tri;
+    const float4* cone = S.cone_light + kConeRec * (size_t)S.n_tri * l0;
+    const size_t cstride = kConeRec * (size_t)S.n_tri;
     const int lane = (int)(threadIdx.x & 63);
     for (int k0 = 0; k0 < S.n_tri_opaque; k0 += 64) {
         bool live = false;
@@ -930,17 +999,29 @@ __device__ __forceinline__ void shadow_opaque_wave(const SceneDev& S, int l0, in
         for (int j = 0; j < kLightBatch; ++j) live |= (j < nl) & !occ[j];
         if (!__any(live)) break;
         const int k = k0 + lane;
+        // every record load of the batch first (one wait), then the tests
+        float4 c0[kLightBatch], c1[kLightBatch];
+#pragma unroll
+        for (int j = 0; j < kLightBatch; ++j) {
+            c0[j] = make_float4(0.f, 0.f, 0.f, 1.f);
+            c1[j] = make_float4(INFINITY, 0.f, INFINITY, 0.f);  // no reach
+            if (j < nl && k < S.n_tri_opaque) {
+                const float4* rec = cone + cstride * j + 2 * k;
+                c0[j] = rec[0];
+                c1[j] = rec[1];
+            }
+        }
         unsigned long long mj[kLightBatch], m = 0;
 #pragma unroll
         for (int j = 0; j < kLightBatch; ++j) {
             mj[j] = 0;
             if (j < nl && wc[j].ok) {
-                bool reach = false;
-                if (k < S.n_tri_opaque) {
-                    const float4 c0 = cone[cstride * j + 2 * k], c1 = cone[cstride * j + 2 * k + 1];
-                    reach = ((c1.x < dmax[j]) & cone_overlap(wc[j], c0, c1.w, dmax[j] * 1e-6f * c1.y)) |
-                            (dmax[j] > c1.z);
-                }
+                const float ang = dmax[j] * 1e-6f * c1[j].y;
+                bool reach = (c1[j].x < dmax[j]) & cone_overlap(wc[j], c0[j], c1[j].w, ang);
+                // edge records only for sphere survivors
+                if (RT_EDGES && S.use_edges && reach)
+                    reach = edges_open(wc[j], cone + cstride * j + 2 * (size_t)S.n_tri + 3 * k, ang);
+                reach |= dmax[j] > c1[j].z;
                 mj[j] = __ballot(reach);
                 m |= mj[j];
             }
@@ -1218,8 +1299,13 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
     }
 }
 
+// Occupancy floor: 7 waves per SIMD (<= 72 VGPRs); the culled loops are
+// latency-bound (C3: 6 -> 7 waves -12%).
+#ifndef RT_WAVES_PER_EU
+#define RT_WAVES_PER_EU 7
+#endif
 template <int MAXD, int LB, bool PF, bool WAVE>
-__global__ __launch_bounds__(256) void rt_trace_kernel(const SceneDev S, const FrameDev F, unsigned* __restrict__ rgba,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MAXD == 0 ? RT_WAVES_PER_EU : 1))) void rt_trace_kernel(const SceneDev S, const FrameDev F, unsigned* __restrict__ rgba,
                                                        float* __restrict__ rgbf, StatsDev* __restrict__ stats)
 {
     const int lane = threadIdx.x & 63;
@@ -1545,8 +1631,8 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
     HIP_TRY(c, up((void**)&c->d_trisph, sph.data(), sph.size() * sizeof(float)));
     HIP_TRY(c, up((void**)&c->d_trinrm, nrm.data(), nrm.size() * sizeof(float)));
     HIP_TRY(c, up((void**)&c->d_tricoef, coef.data(), coef.size() * sizeof(float)));
-    HIP_TRY(c, hipMalloc((void**)&c->d_cone_cam, std::max<size_t>(ntr, 1) * 2 * sizeof(float4)));
-    HIP_TRY(c, hipMalloc((void**)&c->d_cone_light, std::max<size_t>(ntr * nl, 1) * 2 * sizeof(float4)));
+    HIP_TRY(c, hipMalloc((void**)&c->d_cone_cam, std::max<size_t>(ntr, 1) * kConeRec * sizeof(float4)));
+    HIP_TRY(c, hipMalloc((void**)&c->d_cone_light, std::max<size_t>(ntr * nl, 1) * kConeRec * sizeof(float4)));
     for (int j = 0; j < nl && ntr > 0; ++j) {
         const float* l = s->lights + 7 * (size_t)j;
         // shadow rays are culled up to 4x the light's farthest triangle
@@ -1558,7 +1644,7 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
         }
         hipLaunchKernelGGL(rt_cone_prepass, dim3((unsigned)((ntr + 255) / 256)), dim3(256), 0, 0, c->d_tri, c->d_trisph,
                            c->d_trinrm, c->d_tricoef, (int)ntr, l[0], l[1], l[2], 0, (float)(4.0 * far),
-                           c->d_cone_light + 2 * ntr * j);
+                           c->d_cone_light + kConeRec * ntr * j);
         HIP_TRY(c, hipGetLastError());
     }
     HIP_TRY(c, hipDeviceSynchronize());
@@ -1605,6 +1691,7 @@ static int reachable_depth(const rt_ctx* c, const rt_frame* f)
 
 // 256 camera records = 16 KB, the scalar data cache.
 static constexpr int kTricamMaxTriangles = 256;
+static constexpr int kEdgeMaxTriangles = 1024;
 
 typedef void (*kernel_fn)(const SceneDev, const FrameDev, unsigned*, float*, StatsDev*);
 
@@ -1661,7 +1748,7 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
     }
     const int use_tricam = c->n_tri > 0 && c->n_tri <= kTricamMaxTriangles;
     SceneDev S{c->d_geom, c->d_mat, c->d_lights, c->d_tri, c->d_plane, c->d_quad, c->d_translucent, c->d_tricam,
-               use_tricam, c->d_cone_cam, c->d_cone_light, c->n_surf, c->n_lights, c->n_tri, c->n_plane, c->n_quad,
+               use_tricam, c->n_tri <= kEdgeMaxTriangles, c->d_cone_cam, c->d_cone_light, c->n_surf, c->n_lights, c->n_tri, c->n_plane, c->n_quad,
                c->n_tri_opaque, c->n_plane_opaque, c->n_quad_opaque, c->n_translucent, c->shadow_split};
     FrameDev F;
     std::memcpy(F.cam, f->cam_pos, sizeof F.cam);
