@@ -1083,7 +1083,16 @@ __device__ __forceinline__ void add_light(Color& res, const Mat& m, const float4
 {
     const Color LC = Color{l1.x, l1.y, l1.z} * F;
     const float g = l0.w * m.kd * dot(N, L);
+    // Exact shortcuts: a term that evaluates to +-0 leaves every non-zero
+    // component of res bit-identical, so it is skipped when res has none.
+    // The Phong term is +-0 when shin == 0 (pw = 1) and I * ks == 0; the
+    // Lambert term when the light is filtered to 0 and g is finite
+    // (colours are finite by construction: integers / 255).
+    const bool zero_phong = (m.shin == 0.0f) & (l0.w * m.ks == 0.0f);
+    const bool dark = (F.r == 0.0f) & (F.g == 0.0f) & (F.b == 0.0f);
+    if (zero_phong & dark & (fabsf(g) <= 3.4e38f) & (res.r != 0.0f) & (res.g != 0.0f) & (res.b != 0.0f)) return;
     res += (m.color * g) * LC;
+    if (zero_phong & (res.r != 0.0f) & (res.g != 0.0f) & (res.b != 0.0f)) return;
     const Vec3 rf = reflect(L, N);
     const float ps = dot(rf, D);
     if (ps > 0) {
@@ -1150,8 +1159,10 @@ __device__ __forceinline__ Color shade_local(const SceneDev& S, const Mat& m, co
                 }
             }
         }
+#ifndef RT_ABLATE_SHADOW  // timing-only build: no shadow rays
         if (use_wave) shadow_opaque_wave<kLightBatch>(S, lb, nl, P, L, dist, occ, wc, dmax);
         else shadow_opaque_batch<kLightBatch, PF>(S, lb, nl, P, L, dist, occ);
+#endif
 #pragma unroll
         for (int j = 0; j < kLightBatch; ++j) {
             if (j < nl && gate[j]) {

@@ -24,7 +24,7 @@ for s in $STEPS; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 400 python bench.py ;;
     bench_all)
-      for c in c1 c2 c3 c4 c4s7 c4s9; do run bench_$c 400 python bench.py --config $c --steps 10 --cpu-seconds 5; done ;;
+      for c in c1 c2 c3 c4 c4s7 c4s9 c5; do run bench_$c 400 python bench.py --config $c --steps 10 --cpu-seconds 5; done ;;
     listpmc) run list_counters 120 rocprofv3 -L ;;
     pmc)
       B="python bench.py --steps 5 --warmup 1 --no-cpu-baseline --config ${CONFIG:-c2}"
