@@ -57,11 +57,20 @@ def scene_path(name: str) -> str:
 
 
 def algorithmic_flops(types, primary, bounce, shadow):
+    """The reference algorithm's volume: every ray against every surface."""
     import numpy as np
 
     per_ray = (int(np.sum(types == 0)) * OPS_TRI + int(np.sum(types == 1)) * OPS_PLANE +
                int(np.sum(types == 2)) * OPS_QUAD)
     return (primary + bounce + shadow) * per_ray + primary * OPS_RAY_SETUP + shadow * OPS_SHADE_PER_LIT_LIGHT
+
+
+def executed_flops(st):
+    """tests the kernel actually executed (rt_stats, a wave-level
+    test counted once per lane of the wave) x ops per test, plus ray set-up and
+    shading per lit light."""
+    return (st.triangle_tests * OPS_TRI + st.plane_tests * OPS_PLANE + st.quadric_tests * OPS_QUAD +
+            st.primary_rays * OPS_RAY_SETUP + st.shadow_rays * OPS_SHADE_PER_LIT_LIGHT)
 
 
 def cpu_baseline(path, w, h, depth, seconds):
@@ -157,7 +166,10 @@ def main():
     sf.flags = rt_amd.FLAG_STATS
     ctx.render(sf)
     st = ctx.stats()
-    flops = algorithmic_flops(types, st.primary_rays, st.bounce_rays, st.shadow_rays)
+    brute = algorithmic_flops(types, st.primary_rays, st.bounce_rays, st.shadow_rays)
+    flops = executed_flops(st)
+    brute_tests = (st.primary_rays + st.bounce_rays + st.shadow_rays) * int(types.shape[0])
+    run_tests = st.triangle_tests + st.plane_tests + st.quadric_tests
 
     counter = [0]
 
@@ -245,7 +257,10 @@ def main():
             "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
                          "frac_vs_nofma_issue_peak": round(achieved / PEAK_NOFMA_TOPS, 4),
-                         "flops_per_launch": int(flops), "kernel": f"rt_trace_kernel<{st.stack_depth},{st.light_batch}>"},
+                         "flops_per_launch": int(flops), "kernel": f"rt_trace_kernel<{st.stack_depth},{st.light_batch}>",
+                         "work": "exact ray-primitive tests executed (after culling) x SURVEY 8(d) ops + set-up + shading",
+                         "tests_executed": int(run_tests), "tests_brute_force": int(brute_tests),
+                         "brute_force_equiv_tflops": round(brute / (kernel_ms * 1e-3) / 1e12, 3)},
         }
         if world == 1 and not args.no_cpu_baseline:
             cb = cpu_baseline(path, W, H, depth, args.cpu_seconds)

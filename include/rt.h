@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+#define RT_ABI_VERSION 2
 
 enum {
     RT_OK = 0,
@@ -98,6 +98,11 @@ typedef struct rt_stats {
     float kernel_ms;       /* last render's kernel time (hipEvent)          */
     int32_t stack_depth;   /* compiled bounce-stack depth that ran          */
     int32_t light_batch;   /* lights sharing one shadow pass in that kernel */
+    /* exact ray-primitive tests executed (ABI 2): a test a wave runs counts
+       once per lane of the wave, culled tests not at all                    */
+    uint64_t triangle_tests;
+    uint64_t plane_tests;
+    uint64_t quadric_tests;
 } rt_stats;
 
 /* ------------------------------------------------------------ host scene */

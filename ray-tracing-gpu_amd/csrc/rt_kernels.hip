@@ -125,7 +125,14 @@ struct FrameDev {
 };
 
 struct StatsDev {
-    unsigned long long primary, bounce, shadow, skipped;
+    unsigned long long primary, bounce, shadow, skipped, tri, pla, qua;
+};
+
+// Per-lane tallies (RT_FLAG_STATS): rays, and the exact ray-primitive tests
+// the lane's wave executed (a wave-level test counts once per lane).
+struct Counters {
+    unsigned primary = 0, bounce = 0, shadow = 0, skipped = 0;
+    unsigned tri = 0, pla = 0, qua = 0;
 };
 
 // ----------------------------------------------------- exact fast reciprocal
@@ -296,7 +303,7 @@ __device__ __forceinline__ TriRec load_tri(const SceneDev& S, int k)
 // Scene.cpp:1705-1715: closest hit over every surface.  Returns the winning
 // FILE index (-1 = miss) and its distance.
 template <bool CAMERA>
-__device__ __forceinline__ int closest_hit(const SceneDev& S, const Vec3 O, const Vec3 D, float& best_t)
+__device__ __forceinline__ int closest_hit(const SceneDev& S, const Vec3 O, const Vec3 D, float& best_t, Counters& cnt)
 {
     float bt = -1.0f;
     int bi = -1;
@@ -307,6 +314,7 @@ __device__ __forceinline__ int closest_hit(const SceneDev& S, const Vec3 O, cons
             if (!__any(dot(D, make3(c.x, c.y, c.z)) >= c.w)) continue;
         }
         const TriRec tr = load_tri(S, k);
+        ++cnt.tri;
         const TriU r = tri_u(tr.p0, tr.e1, tr.e2, O, D);
         if (!__any(r.ok)) continue;
         float t;
@@ -316,6 +324,7 @@ __device__ __forceinline__ int closest_hit(const SceneDev& S, const Vec3 O, cons
     for (int k = 0; k < S.n_plane; ++k) {
         const float4 a = S.plane[2 * k], b = S.plane[2 * k + 1];
         float t;
+        ++cnt.pla;
         const bool ok = hit_plane(make_float4(0.f, a.x, a.y, a.z), make_float4(a.w, 0.f, 0.f, 0.f), O, D, t);
         take_min(ok, t, __float_as_int(b.x), bt, bi);
     }
@@ -323,6 +332,7 @@ __device__ __forceinline__ int closest_hit(const SceneDev& S, const Vec3 O, cons
         const float4* r = S.quad + 3 * k;
         const float4 a = r[0], b = r[1], c = r[2];
         float t;
+        ++cnt.qua;
         // repack into the file-order record layout hit_quadric reads
         const bool ok = hit_quadric(make_float4(0.f, a.x, a.y, a.z), make_float4(a.w, b.x, b.y, b.z),
                                     make_float4(b.w, c.x, c.y, 0.f), O, D, t);
@@ -399,8 +409,9 @@ __device__ __forceinline__ float4 f4(const u32x16 v, int q)
 // One camera-ray triangle test: exact u first, the rest only if some lane of
 // the wave is inside the u bounds.
 __device__ __forceinline__ void camera_tri(const float4 a, const float4 b, const float4 c, const float4 d,
-                                           const Vec3 D, float& bt, int& bi)
+                                           const Vec3 D, float& bt, int& bi, Counters& cnt)
 {
+    ++cnt.tri;
     const Vec3 e1 = make3(a.x, a.y, a.z), e2 = make3(a.w, b.x, b.y);
     const Vec3 Sv = make3(b.z, b.w, c.x), Q = make3(c.y, c.z, c.w);
     const Vec3 P = cross(D, e2);
@@ -418,7 +429,8 @@ __device__ __forceinline__ void camera_tri(const float4 a, const float4 b, const
 // per-triangle values that depend only on the origin come from tricam[].
 // Records are fetched RT_GROUP at a time so the scalar loads of a group are
 // all in flight before its first test.
-__device__ __forceinline__ int closest_hit_camera(const SceneDev& S, const Vec3 O, const Vec3 D, float& best_t)
+__device__ __forceinline__ int closest_hit_camera(const SceneDev& S, const Vec3 O, const Vec3 D, float& best_t,
+                                                  Counters& cnt)
 {
     float bt = -1.0f;
     int bi = -1;
@@ -434,7 +446,7 @@ __device__ __forceinline__ int closest_hit_camera(const SceneDev& S, const Vec3 
             u32x16 rec_n = rt_sload16(S.tricam + 4 * kn);
             const float4 cc = f4(cone);
             if (__any(dot(D, make3(cc.x, cc.y, cc.z)) >= cc.w))
-                camera_tri(f4(rec, 0), f4(rec, 1), f4(rec, 2), f4(rec, 3), D, bt, bi);
+                camera_tri(f4(rec, 0), f4(rec, 1), f4(rec, 2), f4(rec, 3), D, bt, bi, cnt);
             rt_swait(cone_n, rec_n);
             cone = cone_n;
             rec = rec_n;
@@ -445,12 +457,13 @@ __device__ __forceinline__ int closest_hit_camera(const SceneDev& S, const Vec3 
         const float4 cc = S.cone_cam[2 * k];
         if (!__any(dot(D, make3(cc.x, cc.y, cc.z)) >= cc.w)) continue;
         const float4* r = S.tricam + 4 * k;
-        camera_tri(r[0], r[1], r[2], r[3], D, bt, bi);
+        camera_tri(r[0], r[1], r[2], r[3], D, bt, bi, cnt);
     }
 #endif
     for (int k = 0; k < S.n_plane; ++k) {
         const float4 a = S.plane[2 * k], b = S.plane[2 * k + 1];
         float t;
+        ++cnt.pla;
         const bool ok = hit_plane(make_float4(0.f, a.x, a.y, a.z), make_float4(a.w, 0.f, 0.f, 0.f), O, D, t);
         take_min(ok, t, __float_as_int(b.x), bt, bi);
     }
@@ -458,6 +471,7 @@ __device__ __forceinline__ int closest_hit_camera(const SceneDev& S, const Vec3 
         const float4* r = S.quad + 3 * k;
         const float4 a = r[0], b = r[1], c = r[2];
         float t;
+        ++cnt.qua;
         const bool ok = hit_quadric(make_float4(0.f, a.x, a.y, a.z), make_float4(a.w, b.x, b.y, b.z),
                                     make_float4(b.w, c.x, c.y, 0.f), O, D, t);
         take_min(ok, t, __float_as_int(c.z), bt, bi);
@@ -554,7 +568,7 @@ __device__ __forceinline__ bool edges_open(const WaveCone& wc, const float4* e, 
 
 // Closest hit for camera rays, wave-culled (full wave, cone ok).
 __device__ __forceinline__ int closest_hit_camera_wave(const SceneDev& S, const WaveCone& wc, const Vec3 O,
-                                                       const Vec3 D, float& best_t)
+                                                       const Vec3 D, float& best_t, Counters& cnt)
 {
     float bt = -1.0f;
     int bi = -1;
@@ -575,9 +589,10 @@ __device__ __forceinline__ int closest_hit_camera_wave(const SceneDev& S, const 
             m &= m - 1;
             if (S.use_tricam) {
                 const float4* r = S.tricam + 4 * kk;
-                camera_tri(r[0], r[1], r[2], r[3], D, bt, bi);
+                camera_tri(r[0], r[1], r[2], r[3], D, bt, bi, cnt);
             } else {
                 const TriRec tr = load_tri(S, kk);
+                ++cnt.tri;
                 const TriU r = tri_u(tr.p0, tr.e1, tr.e2, O, D);
                 if (!__any(r.ok)) continue;
                 float t;
@@ -589,6 +604,7 @@ __device__ __forceinline__ int closest_hit_camera_wave(const SceneDev& S, const 
     for (int k = 0; k < S.n_plane; ++k) {
         const float4 a = S.plane[2 * k], b = S.plane[2 * k + 1];
         float t;
+        ++cnt.pla;
         const bool ok = hit_plane(make_float4(0.f, a.x, a.y, a.z), make_float4(a.w, 0.f, 0.f, 0.f), O, D, t);
         take_min(ok, t, __float_as_int(b.x), bt, bi);
     }
@@ -596,6 +612,7 @@ __device__ __forceinline__ int closest_hit_camera_wave(const SceneDev& S, const 
         const float4* r = S.quad + 3 * k;
         const float4 a = r[0], b = r[1], c = r[2];
         float t;
+        ++cnt.qua;
         const bool ok = hit_quadric(make_float4(0.f, a.x, a.y, a.z), make_float4(a.w, b.x, b.y, b.z),
                                     make_float4(b.w, c.x, c.y, 0.f), O, D, t);
         take_min(ok, t, __float_as_int(c.z), bt, bi);
@@ -606,13 +623,14 @@ __device__ __forceinline__ int closest_hit_camera_wave(const SceneDev& S, const 
 
 // Primary rays: wave-culled when the whole wave is here, else per lane.
 template <bool WAVE>
-__device__ __forceinline__ int closest_hit_primary(const SceneDev& S, const Vec3 O, const Vec3 D, float& t)
+__device__ __forceinline__ int closest_hit_primary(const SceneDev& S, const Vec3 O, const Vec3 D, float& t,
+                                                   Counters& cnt)
 {
     if (WAVE && wave_full()) {
         const WaveCone wc = wave_cone(D, true);
-        if (wc.ok) return closest_hit_camera_wave(S, wc, O, D, t);
+        if (wc.ok) return closest_hit_camera_wave(S, wc, O, D, t, cnt);
     }
-    return S.use_tricam ? closest_hit_camera(S, O, D, t) : closest_hit<true>(S, O, D, t);
+    return S.use_tricam ? closest_hit_camera(S, O, D, t, cnt) : closest_hit<true>(S, O, D, t, cnt);
 }
 
 // tricam[] for camera position C (one thread per triangle).
@@ -781,15 +799,22 @@ __device__ __forceinline__ Mat load_mat(const SceneDev& S, int idx)
 
 // One file-order surface record against a shadow ray (generic path).
 __device__ __forceinline__ bool shadow_hit_record(const float4* rec, const Vec3 P, const Vec3 L, float dist,
-                                                  Color& fc)
+                                                  Color& fc, Counters& cnt)
 {
     const float4 a = rec[0], b = rec[1], c = rec[2], d = rec[3];
     float t;
     bool ok;
     const int kind = kind_of(a);
-    if (kind == RT_TRIANGLE) ok = hit_triangle(a, b, c, P, L, t);
-    else if (kind == RT_PLANE) ok = hit_plane(a, b, P, L, t);
-    else ok = hit_quadric(a, b, c, P, L, t);
+    if (kind == RT_TRIANGLE) {
+        ++cnt.tri;
+        ok = hit_triangle(a, b, c, P, L, t);
+    } else if (kind == RT_PLANE) {
+        ++cnt.pla;
+        ok = hit_plane(a, b, P, L, t);
+    } else {
+        ++cnt.qua;
+        ok = hit_quadric(a, b, c, P, L, t);
+    }
     fc = Color{d.y, d.z, d.w};
     return ok & (t > kEps) & (t < dist);
 }
@@ -797,7 +822,7 @@ __device__ __forceinline__ bool shadow_hit_record(const float4* rec, const Vec3 
 // Scene.cpp:1842-1861 ObtenirFiltreDeSurface.  L is the UNNORMALISED light
 // vector; it is normalised here exactly like the reference (in place).
 __device__ __forceinline__ Color shadow_filter(const SceneDev& S, int light, const Vec3 P, Vec3& L,
-                                               unsigned& skipped)
+                                               Counters& cnt)
 {
     Color F{1.0f, 1.0f, 1.0f};
     const float dist = norm(L);
@@ -806,7 +831,7 @@ __device__ __forceinline__ Color shadow_filter(const SceneDev& S, int light, con
         // General case: the product over every surface in file order.
         for (int i = 0; i < S.n_surf; ++i) {
             Color fc;
-            if (shadow_hit_record(S.geom + 4 * i, P, L, dist, fc)) F *= fc;
+            if (shadow_hit_record(S.geom + 4 * i, P, L, dist, fc, cnt)) F *= fc;
         }
         return F;
     }
@@ -826,6 +851,7 @@ __device__ __forceinline__ Color shadow_filter(const SceneDev& S, int light, con
         const bool reach = !occluded & light_reach(c0, c1, L, dist, slack);
         if (!__any(reach)) continue;
         const TriRec tr = load_tri(S, k);
+        ++cnt.tri;
         const TriU r = tri_u(tr.p0, tr.e1, tr.e2, P, L);
         if (!__any(r.ok && !occluded)) continue;
         float t;
@@ -837,6 +863,7 @@ __device__ __forceinline__ Color shadow_filter(const SceneDev& S, int light, con
         ++done;
         const float4 a = S.plane[2 * k];
         float t;
+        ++cnt.pla;
         const bool ok = hit_plane(make_float4(0.f, a.x, a.y, a.z), make_float4(a.w, 0.f, 0.f, 0.f), P, L, t);
         occluded |= ok & (t > kEps) & (t < dist);
     }
@@ -846,24 +873,22 @@ __device__ __forceinline__ Color shadow_filter(const SceneDev& S, int light, con
         const float4* r = S.quad + 3 * k;
         const float4 a = r[0], b = r[1], c = r[2];
         float t;
+        ++cnt.qua;
         const bool ok = hit_quadric(make_float4(0.f, a.x, a.y, a.z), make_float4(a.w, b.x, b.y, b.z),
                                     make_float4(b.w, c.x, c.y, 0.f), P, L, t);
         occluded |= ok & (t > kEps) & (t < dist);
     }
-    skipped += (unsigned)(total - done);
+    cnt.skipped += (unsigned)(total - done);
     if (occluded) return Color{0.0f, 0.0f, 0.0f};
     // Translucent surfaces, file order (the relative order of the factors the
     // reference multiplies is preserved; unhit opaque surfaces contribute none).
     for (int j = 0; j < S.n_translucent; ++j) {
         Color fc;
-        if (shadow_hit_record(S.geom + 4 * S.translucent[j], P, L, dist, fc)) F *= fc;
+        if (shadow_hit_record(S.geom + 4 * S.translucent[j], P, L, dist, fc, cnt)) F *= fc;
     }
     return F;
 }
 
-struct Counters {
-    unsigned primary = 0, bounce = 0, shadow = 0, skipped = 0;
-};
 
 // Scene.cpp:1742-1777: ambient + every light (N.L gate on the unnormalised
 // light vector, filter, Lambert "Gouraud" term, Phong term).
@@ -879,7 +904,7 @@ struct Counters {
 template <int kLightBatch, bool PF>
 __device__ __forceinline__ void shadow_opaque_batch(const SceneDev& S, int l0, int nl, const Vec3 P,
                                                     const Vec3 (&L)[kLightBatch], const float (&dist)[kLightBatch],
-                                                    bool (&occ)[kLightBatch])
+                                                    bool (&occ)[kLightBatch], Counters& cnt)
 {
     const float4* cone = S.cone_light + kConeRec * (size_t)S.n_tri * l0;
     const size_t cstride = kConeRec * (size_t)S.n_tri;
@@ -935,6 +960,7 @@ __device__ __forceinline__ void shadow_opaque_batch(const SceneDev& S, int l0, i
 #pragma unroll
             for (int j = 0; j < kLightBatch; ++j) {
                 if (j < nl && __any(reach[j])) {
+                    ++cnt.tri;
                     const Vec3 Pv = cross(L[j], tr.e2);
                     const float det = dot(tr.e1, Pv);
                     const float inv = recip_det(det);
@@ -960,6 +986,7 @@ __device__ __forceinline__ void shadow_opaque_batch(const SceneDev& S, int l0, i
         for (int j = 0; j < kLightBatch; ++j) {
             if (j < nl && __any(!occ[j])) {
                 float t;
+                ++cnt.pla;
                 const bool ok = hit_plane(make_float4(0.f, a.x, a.y, a.z), make_float4(a.w, 0.f, 0.f, 0.f), P, L[j], t);
                 occ[j] |= ok & (t > kEps) & (t < dist[j]);
             }
@@ -972,6 +999,7 @@ __device__ __forceinline__ void shadow_opaque_batch(const SceneDev& S, int l0, i
         for (int j = 0; j < kLightBatch; ++j) {
             if (j < nl && __any(!occ[j])) {
                 float t;
+                ++cnt.qua;
                 const bool ok = hit_quadric(make_float4(0.f, a.x, a.y, a.z), make_float4(a.w, b.x, b.y, b.z),
                                             make_float4(b.w, c.x, c.y, 0.f), P, L[j], t);
                 occ[j] |= ok & (t > kEps) & (t < dist[j]);
@@ -988,7 +1016,7 @@ template <int kLightBatch>
 __device__ __forceinline__ void shadow_opaque_wave(const SceneDev& S, int l0, int nl, const Vec3 P,
                                                    const Vec3 (&L)[kLightBatch], const float (&dist)[kLightBatch],
                                                    bool (&occ)[kLightBatch], const WaveCone (&wc)[kLightBatch],
-                                                   const float (&dmax)[kLightBatch])
+                                                   const float (&dmax)[kLightBatch], Counters& cnt)
 {
     const float4* cone = S.cone_light + kConeRec * (size_t)S.n_tri * l0;
     const size_t cstride = kConeRec * (size_t)S.n_tri;
@@ -1036,6 +1064,7 @@ __device__ __forceinline__ void shadow_opaque_wave(const SceneDev& S, int l0, in
 #pragma unroll
             for (int j = 0; j < kLightBatch; ++j) {
                 if (((mj[j] >> b) & 1ull) && __any(!occ[j])) {
+                    ++cnt.tri;
                     const Vec3 Pv = cross(L[j], tr.e2);
                     const float det = dot(tr.e1, Pv);
                     const float inv = recip_det(det);
@@ -1054,6 +1083,7 @@ __device__ __forceinline__ void shadow_opaque_wave(const SceneDev& S, int l0, in
         for (int j = 0; j < kLightBatch; ++j) {
             if (j < nl && __any(!occ[j])) {
                 float t;
+                ++cnt.pla;
                 const bool ok = hit_plane(make_float4(0.f, a.x, a.y, a.z), make_float4(a.w, 0.f, 0.f, 0.f), P, L[j], t);
                 occ[j] |= ok & (t > kEps) & (t < dist[j]);
             }
@@ -1066,6 +1096,7 @@ __device__ __forceinline__ void shadow_opaque_wave(const SceneDev& S, int l0, in
         for (int j = 0; j < kLightBatch; ++j) {
             if (j < nl && __any(!occ[j])) {
                 float t;
+                ++cnt.qua;
                 const bool ok = hit_quadric(make_float4(0.f, a.x, a.y, a.z), make_float4(a.w, b.x, b.y, b.z),
                                             make_float4(b.w, c.x, c.y, 0.f), P, L[j], t);
                 occ[j] |= ok & (t > kEps) & (t < dist[j]);
@@ -1118,7 +1149,7 @@ __device__ __forceinline__ Color shade_local(const SceneDev& S, const Mat& m, co
             Vec3 L = make3(l0.x, l0.y, l0.z) - P;
             if (active && dot(L, N) > 0) {
                 ++cnt.shadow;
-                const Color F = shadow_filter(S, li, P, L, cnt.skipped);
+                const Color F = shadow_filter(S, li, P, L, cnt);
                 add_light(res, m, l0, l1, N, L, D, F);
             }
         }
@@ -1160,8 +1191,8 @@ __device__ __forceinline__ Color shade_local(const SceneDev& S, const Mat& m, co
             }
         }
 #ifndef RT_ABLATE_SHADOW  // timing-only build: no shadow rays
-        if (use_wave) shadow_opaque_wave<kLightBatch>(S, lb, nl, P, L, dist, occ, wc, dmax);
-        else shadow_opaque_batch<kLightBatch, PF>(S, lb, nl, P, L, dist, occ);
+        if (use_wave) shadow_opaque_wave<kLightBatch>(S, lb, nl, P, L, dist, occ, wc, dmax, cnt);
+        else shadow_opaque_batch<kLightBatch, PF>(S, lb, nl, P, L, dist, occ, cnt);
 #endif
 #pragma unroll
         for (int j = 0; j < kLightBatch; ++j) {
@@ -1172,7 +1203,7 @@ __device__ __forceinline__ Color shade_local(const SceneDev& S, const Mat& m, co
                     F = Color{1.0f, 1.0f, 1.0f};
                     for (int q = 0; q < S.n_translucent; ++q) {
                         Color fc;
-                        if (shadow_hit_record(S.geom + 4 * S.translucent[q], P, L[j], dist[j], fc)) F *= fc;
+                        if (shadow_hit_record(S.geom + 4 * S.translucent[q], P, L[j], dist[j], fc, cnt)) F *= fc;
                     }
                 }
                 add_light(res, m, l0, l1, N, L[j], D, F);
@@ -1200,7 +1231,7 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
         return Color{D.x, D.y, D.z};
 #endif
         float t;
-        const int idx = closest_hit_primary<WAVE>(S, O, D, t);
+        const int idx = closest_hit_primary<WAVE>(S, O, D, t, cnt);
         // Lanes that miss (or lie outside the frame) stay in step through the
         // shading so the wave stays whole for wave-level shadow culling.
         const bool hit = idx >= 0;
@@ -1223,7 +1254,7 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
         for (;;) {
             if (trace) {
                 float t;
-                const int idx = camera_ray ? closest_hit_primary<WAVE>(S, O, D, t) : closest_hit<false>(S, O, D, t);
+                const int idx = camera_ray ? closest_hit_primary<WAVE>(S, O, D, t, cnt) : closest_hit<false>(S, O, D, t, cnt);
                 camera_ray = false;
                 ret = bg;
                 if (idx >= 0) {
@@ -1315,7 +1346,9 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
 #ifndef RT_WAVES_PER_EU
 #define RT_WAVES_PER_EU 7
 #endif
-template <int MAXD, int LB, bool PF, bool WAVE>
+// COUNT: also tally the exact tests executed (the RT_FLAG_STATS launch); in
+// the timed kernels the tallies are dead and compile away.
+template <int MAXD, int LB, bool PF, bool WAVE, bool COUNT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MAXD == 0 ? RT_WAVES_PER_EU : 1))) void rt_trace_kernel(const SceneDev S, const FrameDev F, unsigned* __restrict__ rgba,
                                                        float* __restrict__ rgbf, StatsDev* __restrict__ stats)
 {
@@ -1356,7 +1389,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MAXD == 0 ?
         atomicAdd(&stats->primary, (unsigned long long)cnt.primary);
         atomicAdd(&stats->bounce, (unsigned long long)cnt.bounce);
         atomicAdd(&stats->shadow, (unsigned long long)cnt.shadow);
-        atomicAdd(&stats->skipped, (unsigned long long)cnt.skipped * 1ull);
+        atomicAdd(&stats->skipped, (unsigned long long)cnt.skipped);
+        if constexpr (COUNT) {
+            atomicAdd(&stats->tri, (unsigned long long)cnt.tri);
+            atomicAdd(&stats->pla, (unsigned long long)cnt.pla);
+            atomicAdd(&stats->qua, (unsigned long long)cnt.qua);
+        }
     }
 }
 
@@ -1714,23 +1752,24 @@ typedef void (*kernel_fn)(const SceneDev, const FrameDev, unsigned*, float*, Sta
 #ifndef RT_WAVE_LB
 #define RT_WAVE_LB 2
 #endif
+template <bool COUNT>
 static kernel_fn pick_kernel(int depth, int n_tri, int n_lights, int& cap, int& lb)
 {
     lb = 1;
     if (depth == 0 && n_tri > 0) {
         cap = 0;
         lb = RT_WAVE_LB;
-        return (kernel_fn)&rt_trace_kernel<0, RT_WAVE_LB, false, true>;
+        return (kernel_fn)&rt_trace_kernel<0, RT_WAVE_LB, false, true, COUNT>;
     }
     if (depth == 0 && n_lights > 1) {
         cap = 0;
         lb = 3;
-        return (kernel_fn)&rt_trace_kernel<0, 3, false, false>;
+        return (kernel_fn)&rt_trace_kernel<0, 3, false, false, COUNT>;
     }
-#define RT_PICK(N)                                                 \
-    if (depth <= N) {                                              \
-        cap = N;                                                   \
-        return (kernel_fn)&rt_trace_kernel<N, 1, false, false>;    \
+#define RT_PICK(N)                                                        \
+    if (depth <= N) {                                                     \
+        cap = N;                                                          \
+        return (kernel_fn)&rt_trace_kernel<N, 1, false, false, COUNT>;    \
     }
     RT_STACK_DEPTHS(RT_PICK)
 #undef RT_PICK
@@ -1752,7 +1791,8 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
     }
     const int depth = reachable_depth(c, f);
     int cap = 0, lb = 1;
-    kernel_fn k = pick_kernel(depth, c->n_tri, c->n_lights, cap, lb);
+    kernel_fn k = (f->flags & RT_FLAG_STATS) ? pick_kernel<true>(depth, c->n_tri, c->n_lights, cap, lb)
+                                              : pick_kernel<false>(depth, c->n_tri, c->n_lights, cap, lb);
     if (!k) {
         c->err = "reachable bounce depth " + std::to_string(depth) + " exceeds the compiled stack (32)";
         return RT_E_UNSUPPORTED;
@@ -1821,6 +1861,9 @@ static int finish_sync(rt_ctx* c, const rt_frame* f, hipStream_t st, bool timed)
         c->last.bounce_rays = h.bounce;
         c->last.shadow_rays = h.shadow;
         c->last.shadow_tests_skipped = h.skipped;
+        c->last.triangle_tests = h.tri;
+        c->last.plane_tests = h.pla;
+        c->last.quadric_tests = h.qua;
     }
     return RT_OK;
 }

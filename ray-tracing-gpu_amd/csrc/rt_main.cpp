@@ -91,10 +91,12 @@ int main(int argc, char** argv)
     std::printf("[ETAT]: Termine! --> Temps total de rendu : %.6f secondes (%d frame(s), kernel %.3f ms)\n",
                 total, frames, st.kernel_ms);
     if (stats)
-        std::printf("[STATS]: primary=%llu bounce=%llu shadow=%llu shadow_tests_skipped=%llu stack=%d\n",
+        std::printf("[STATS]: primary=%llu bounce=%llu shadow=%llu shadow_tests_skipped=%llu stack=%d "
+                    "tests: triangle=%llu plane=%llu quadric=%llu\n",
                     (unsigned long long)st.primary_rays, (unsigned long long)st.bounce_rays,
                     (unsigned long long)st.shadow_rays, (unsigned long long)st.shadow_tests_skipped,
-                    st.stack_depth);
+                    st.stack_depth, (unsigned long long)st.triangle_tests, (unsigned long long)st.plane_tests,
+                    (unsigned long long)st.quadric_tests);
     if (out) {
         FILE* f = std::fopen(out, "wb");
         if (!f) return fail("fopen", -1, out);

@@ -68,7 +68,8 @@ class Stats(ctypes.Structure):
     _fields_ = [("primary_rays", ctypes.c_uint64), ("bounce_rays", ctypes.c_uint64),
                 ("shadow_rays", ctypes.c_uint64), ("shadow_tests_skipped", ctypes.c_uint64),
                 ("kernel_ms", ctypes.c_float), ("stack_depth", ctypes.c_int32),
-                ("light_batch", ctypes.c_int32)]
+                ("light_batch", ctypes.c_int32), ("triangle_tests", ctypes.c_uint64),
+                ("plane_tests", ctypes.c_uint64), ("quadric_tests", ctypes.c_uint64)]
 
 
 _lib: Optional[ctypes.CDLL] = None

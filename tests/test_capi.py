@@ -36,7 +36,7 @@ def test_header_symbols_exported():
 
 
 def test_abi_version():
-    assert rt_amd.lib().rt_abi_version() == 1
+    assert rt_amd.lib().rt_abi_version() == 2
 
 
 def test_struct_layouts_match_header():
@@ -45,8 +45,9 @@ def test_struct_layouts_match_header():
 #include <stddef.h>
 #include "rt.h"
 int main(void){
-  printf("%zu %zu %zu %zu %zu %zu\n", sizeof(rt_scene_flat), sizeof(rt_frame), sizeof(rt_stats),
-         offsetof(rt_frame, width), offsetof(rt_frame, flags), offsetof(rt_stats, kernel_ms));
+  printf("%zu %zu %zu %zu %zu %zu %zu\n", sizeof(rt_scene_flat), sizeof(rt_frame), sizeof(rt_stats),
+         offsetof(rt_frame, width), offsetof(rt_frame, flags), offsetof(rt_stats, kernel_ms),
+         offsetof(rt_stats, triangle_tests));
   return 0; }
 """
     import tempfile
@@ -58,7 +59,8 @@ int main(void){
         subprocess.run(["gcc", "-I", os.path.join(REPO, "include"), c, "-o", exe], check=True)
         vals = list(map(int, subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split()))
     assert vals == [ctypes.sizeof(rt_amd.SceneFlat), ctypes.sizeof(rt_amd.Frame), ctypes.sizeof(rt_amd.Stats),
-                    rt_amd.Frame.width.offset, rt_amd.Frame.flags.offset, rt_amd.Stats.kernel_ms.offset]
+                    rt_amd.Frame.width.offset, rt_amd.Frame.flags.offset, rt_amd.Stats.kernel_ms.offset,
+                    rt_amd.Stats.triangle_tests.offset]
 
 
 def test_null_arguments_are_errors():

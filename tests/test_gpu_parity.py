@@ -102,6 +102,20 @@ def test_scene2_1080p_digest_and_counts(ctx, digests):
     assert st.bounce_rays == 0
 
 
+@pytest.mark.parametrize("i,depth", [(2, 0), (7, 3), (1, 0)])
+def test_counted_kernel_renders_the_same(ctx, i, depth):
+    """The RT_FLAG_STATS launch runs the COUNT kernel variant: same image, and
+    its test tallies lie between 0 and the brute-force count."""
+    plain = render(ctx, scene(i), 320, 200, depth)
+    counted = render(ctx, scene(i), 320, 200, depth, flags=rt_amd.FLAG_STATS)
+    st = ctx.stats()
+    assert bits_equal(plain, counted)
+    s = rt_amd.Scene(scene(i), 320, 200, depth)
+    n = s.n_surfaces
+    tests = st.triangle_tests + st.plane_tests + st.quadric_tests
+    assert 0 < tests <= (st.primary_rays + st.bounce_rays + st.shadow_rays) * n * 64
+
+
 def test_scene2_depth_inert_full_size(ctx):
     """C4 property at full size: scene2 has no Kr/Kt, so depth 5 == depth 0."""
     a = render(ctx, scene(2), 3840, 2160, 5, as_float=False)
