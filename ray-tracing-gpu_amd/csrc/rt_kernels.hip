@@ -521,6 +521,19 @@ __device__ __forceinline__ float wave_max(float v)
     v = fmaxf(v, dppf<0x140>(v));
     return fmaxf(fmaxf(readlanef(v, 0), readlanef(v, 16)), fmaxf(readlanef(v, 32), readlanef(v, 48)));
 }
+// Sum over all 64 lanes (full exec only), for the stats tallies.
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
+{
+    // the stats launch is untimed: 64 scalar reads are simple and exact
+    unsigned long long t = 0;
+    for (int l = 0; l < 64; ++l) {
+        const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, l);
+        const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), l);
+        t += ((unsigned long long)hi << 32) | lo;
+    }
+    return t;
+}
+
 struct WaveCone {
     Vec3 w;
     float cosW, sinW;
@@ -1341,8 +1354,11 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
     }
 }
 
-// Occupancy floor: 7 waves per SIMD (<= 72 VGPRs); the culled loops are
-// latency-bound (C3: 6 -> 7 waves -12%).
+// Occupancy floor (waves per SIMD) for the depth-0 kernels: 7 (<= 72
+// VGPRs).  It costs 4 VGPR spills (scratch: ~7 MB of HBM writes per C2
+// frame, far below any bandwidth limit) and wins C2 by 4% over the
+// unconstrained 81 VGPRs / 5 waves; 6 and 8 waves are slower
+// (tools/ab_variants.py, MI355X).
 #ifndef RT_WAVES_PER_EU
 #define RT_WAVES_PER_EU 7
 #endif
@@ -1386,14 +1402,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MAXD == 0 ?
         }
     }
     if (F.flags & RT_FLAG_STATS) {
-        atomicAdd(&stats->primary, (unsigned long long)cnt.primary);
-        atomicAdd(&stats->bounce, (unsigned long long)cnt.bounce);
-        atomicAdd(&stats->shadow, (unsigned long long)cnt.shadow);
-        atomicAdd(&stats->skipped, (unsigned long long)cnt.skipped);
-        if constexpr (COUNT) {
-            atomicAdd(&stats->tri, (unsigned long long)cnt.tri);
-            atomicAdd(&stats->pla, (unsigned long long)cnt.pla);
-            atomicAdd(&stats->qua, (unsigned long long)cnt.qua);
+        unsigned long long v[7] = {cnt.primary, cnt.bounce, cnt.shadow, cnt.skipped, cnt.tri, cnt.pla, cnt.qua};
+        unsigned long long* dst[7] = {&stats->primary, &stats->bounce, &stats->shadow, &stats->skipped,
+                                      &stats->tri, &stats->pla, &stats->qua};
+        const int nv = COUNT ? 7 : 4;
+        if (wave_full()) {  // one atomic per counter per wave
+#pragma unroll
+            for (int i = 0; i < 7; ++i)
+                if (i < nv) {
+                    const unsigned long long w = wave_sum_u64(v[i]);
+                    if ((threadIdx.x & 63) == 0) atomicAdd(dst[i], w);
+                }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 7; ++i)
+                if (i < nv) atomicAdd(dst[i], v[i]);
         }
     }
 }

@@ -44,8 +44,9 @@ for s in $STEPS; do
       done ;;
     fastmath) run fastmath_check 600 tools/fastmath_check ;;
 
-    prof) run rocprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 200 --no-cpu-baseline --config ${CONFIG:-c2}
-          python tools/prof_summary.py gpurun_out/prof/run_kernel_trace.csv > gpurun_out/prof/summary.json ;;
+    prof) P=gpurun_out/prof_${CONFIG:-c2}
+          run rocprof_${CONFIG:-c2} 400 rocprofv3 --kernel-trace --stats --output-format csv -d $P -o run -- python bench.py --steps ${PROF_STEPS:-200} --no-cpu-baseline --config ${CONFIG:-c2}
+          python tools/prof_summary.py $P/run_kernel_trace.csv > $P/summary.json ;;
   esac
 done
 exit 0
