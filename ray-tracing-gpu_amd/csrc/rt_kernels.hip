@@ -125,8 +125,11 @@ struct FrameDev {
 };
 
 struct StatsDev {
-    unsigned long long primary, bounce, shadow, skipped, tri, pla, qua;
+    unsigned long long primary, bounce, shadow, skipped, tri, pla, qua, pad;
 };
+// Stats tallies land in kStatSlots copies (by block) so the atomics of a
+// launch spread over many addresses instead of serialising on one.
+constexpr int kStatSlots = 256;
 
 // Per-lane tallies (RT_FLAG_STATS): rays, and the exact ray-primitive tests
 // the lane's wave executed (a wave-level test counts once per lane).
@@ -1403,8 +1406,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MAXD == 0 ?
     }
     if (F.flags & RT_FLAG_STATS) {
         unsigned long long v[7] = {cnt.primary, cnt.bounce, cnt.shadow, cnt.skipped, cnt.tri, cnt.pla, cnt.qua};
-        unsigned long long* dst[7] = {&stats->primary, &stats->bounce, &stats->shadow, &stats->skipped,
-                                      &stats->tri, &stats->pla, &stats->qua};
+        StatsDev* sl = stats + ((blockIdx.x + blockIdx.y * gridDim.x) % kStatSlots);
+        unsigned long long* dst[7] = {&sl->primary, &sl->bounce, &sl->shadow, &sl->skipped,
+                                      &sl->tri, &sl->pla, &sl->qua};
         const int nv = COUNT ? 7 : 4;
         if (wave_full()) {  // one atomic per counter per wave
 #pragma unroll
@@ -1495,7 +1499,7 @@ RT_EXPORT int rt_create(int32_t dev, rt_ctx** out)
     HIP_TRY(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIP_TRY(c, hipEventCreate(&c->ev0));
     HIP_TRY(c, hipEventCreate(&c->ev1));
-    HIP_TRY(c, hipMalloc(&c->d_stats, sizeof(StatsDev)));
+    HIP_TRY(c, hipMalloc(&c->d_stats, kStatSlots * sizeof(StatsDev)));
     return RT_OK;
 }
 
@@ -1845,7 +1849,7 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
     c->last.stack_depth = cap;
     c->last.light_batch = lb;
     if (rows == 0) return RT_OK;
-    if (f->flags & RT_FLAG_STATS) HIP_TRY(c, hipMemsetAsync(c->d_stats, 0, sizeof(StatsDev), st));
+    if (f->flags & RT_FLAG_STATS) HIP_TRY(c, hipMemsetAsync(c->d_stats, 0, kStatSlots * sizeof(StatsDev), st));
     // Camera-ray triangle values: recomputed only when the camera moves.
     if (c->n_tri > 0 && (!c->cam_valid || std::memcmp(c->cam_key, f->cam_pos, sizeof c->cam_key) != 0)) {
         const float* cp = f->cam_pos;
@@ -1878,8 +1882,18 @@ static int finish_sync(rt_ctx* c, const rt_frame* f, hipStream_t st, bool timed)
         c->last.kernel_ms = ms;
     }
     if (f->flags & RT_FLAG_STATS) {
+        std::vector<StatsDev> slots(kStatSlots);
+        HIP_TRY(c, hipMemcpy(slots.data(), c->d_stats, kStatSlots * sizeof(StatsDev), hipMemcpyDeviceToHost));
         StatsDev h{};
-        HIP_TRY(c, hipMemcpy(&h, c->d_stats, sizeof h, hipMemcpyDeviceToHost));
+        for (const StatsDev& q : slots) {
+            h.primary += q.primary;
+            h.bounce += q.bounce;
+            h.shadow += q.shadow;
+            h.skipped += q.skipped;
+            h.tri += q.tri;
+            h.pla += q.pla;
+            h.qua += q.qua;
+        }
         c->last.primary_rays = h.primary;
         c->last.bounce_rays = h.bounce;
         c->last.shadow_rays = h.shadow;
