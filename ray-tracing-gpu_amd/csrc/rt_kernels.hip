@@ -101,6 +101,12 @@ struct SceneDev {
     // camera (cone_cam) or light l (cone_light + kConeRec*n_tri*l).
     const float4* __restrict__ cone_cam;
     const float4* __restrict__ cone_light;
+    // Two-level culling for big lists: one [c0 c1] record per apex and
+    // 64-triangle cluster (tri[] is Morton-ordered at upload), built by
+    // rt_cluster_prepass from its members' records; n_clu = 0: off.
+    const float4* __restrict__ clu_cam;
+    const float4* __restrict__ clu_light;
+    int n_clu;
     int n_surf, n_lights;
     int n_tri, n_plane, n_quad;
     int n_tri_opaque, n_plane_opaque, n_quad_opaque;
@@ -561,9 +567,10 @@ __device__ __forceinline__ WaveCone wave_cone(const Vec3 d, bool live)
 }
 // May some ray of the wave cone reach the triangle cone [c0.xyz, c0.w; c1.w]?
 // ang = extra angular slack.
-__device__ __forceinline__ bool cone_overlap(const WaveCone& wc, const float4 c0, float sinT, float ang)
+__device__ __forceinline__ bool cone_overlap(const WaveCone& wc, const float4 c0, float sinT, float ang,
+                                             float margin = 2e-6f)
 {
-    const float lim = wc.cosW * c0.w - wc.sinW * sinT - 2e-6f - ang;
+    const float lim = wc.cosW * c0.w - wc.sinW * sinT - margin - ang;
     return !(c0.w > 0.0f) | (dot(wc.w, make3(c0.x, c0.y, c0.z)) >= lim);
 }
 
@@ -582,40 +589,65 @@ __device__ __forceinline__ bool edges_open(const WaveCone& wc, const float4* e, 
     return edge_open(wc, e[0], ang) & edge_open(wc, e[1], ang) & edge_open(wc, e[2], ang);
 }
 
+// One batch of 64 triangles [k0, k0 + 64) for the wave's camera rays: one
+// lane per triangle against the wave cone, exact tests on the survivors.
+__device__ __forceinline__ void camera_wave_batch(const SceneDev& S, const WaveCone& wc, int k0, const Vec3 O,
+                                                  const Vec3 D, float& bt, int& bi, Counters& cnt)
+{
+    const int k = k0 + (int)(threadIdx.x & 63);
+    float4 c0 = make_float4(0.f, 0.f, 0.f, 1.f), c1 = make_float4(0.f, 0.f, 0.f, 0.f);  // no reach
+    if (k < S.n_tri) {
+        c0 = S.cone_cam[2 * k];
+        c1 = S.cone_cam[2 * k + 1];
+    }
+    bool reach = cone_overlap(wc, c0, c1.w, 0.0f);
+    // edge records only for sphere survivors
+    if (RT_EDGES && S.use_edges && reach) reach = edges_open(wc, S.cone_cam + 2 * S.n_tri + 3 * k, 0.0f);
+    unsigned long long m = __ballot(reach);
+    while (m) {
+        const int kk = k0 + (int)__builtin_ctzll(m);
+        m &= m - 1;
+        if (S.use_tricam) {
+            const float4* r = S.tricam + 4 * kk;
+            camera_tri(r[0], r[1], r[2], r[3], D, bt, bi, cnt);
+        } else {
+            const TriRec tr = load_tri(S, kk);
+            ++cnt.tri;
+            const TriU r = tri_u(tr.p0, tr.e1, tr.e2, O, D);
+            if (!__any(r.ok)) continue;
+            float t;
+            const bool ok = tri_vt(r, tr.e1, tr.e2, D, t);
+            take_min(ok, t, tr.idx, bt, bi);
+        }
+    }
+}
+
 // Closest hit for camera rays, wave-culled (full wave, cone ok).
+template <bool CLU>
 __device__ __forceinline__ int closest_hit_camera_wave(const SceneDev& S, const WaveCone& wc, const Vec3 O,
                                                        const Vec3 D, float& best_t, Counters& cnt)
 {
     float bt = -1.0f;
     int bi = -1;
     const int lane = (int)(threadIdx.x & 63);
-    for (int k0 = 0; k0 < S.n_tri; k0 += 64) {
-        const int k = k0 + lane;
-        float4 c0 = make_float4(0.f, 0.f, 0.f, 1.f), c1 = make_float4(0.f, 0.f, 0.f, 0.f);  // no reach
-        if (k < S.n_tri) {
-            c0 = S.cone_cam[2 * k];
-            c1 = S.cone_cam[2 * k + 1];
-        }
-        bool reach = cone_overlap(wc, c0, c1.w, 0.0f);
-        // edge records only for sphere survivors
-        if (RT_EDGES && S.use_edges && reach) reach = edges_open(wc, S.cone_cam + 2 * S.n_tri + 3 * k, 0.0f);
-        unsigned long long m = __ballot(reach);
-        while (m) {
-            const int kk = k0 + (int)__builtin_ctzll(m);
-            m &= m - 1;
-            if (S.use_tricam) {
-                const float4* r = S.tricam + 4 * kk;
-                camera_tri(r[0], r[1], r[2], r[3], D, bt, bi, cnt);
-            } else {
-                const TriRec tr = load_tri(S, kk);
-                ++cnt.tri;
-                const TriU r = tri_u(tr.p0, tr.e1, tr.e2, O, D);
-                if (!__any(r.ok)) continue;
-                float t;
-                const bool ok = tri_vt(r, tr.e1, tr.e2, D, t);
-                take_min(ok, t, tr.idx, bt, bi);
+    if constexpr (CLU) {
+        // clusters of 64 first (cluster record implies every member's test)
+        for (int c0i = 0; c0i < S.n_clu; c0i += 64) {
+            const int cl = c0i + lane;
+            float4 q0 = make_float4(0.f, 0.f, 0.f, 1.f), q1 = make_float4(0.f, 0.f, 0.f, 0.f);  // no reach
+            if (cl < S.n_clu) {
+                q0 = S.clu_cam[2 * cl];
+                q1 = S.clu_cam[2 * cl + 1];
+            }
+            unsigned long long cm = __ballot(cone_overlap(wc, q0, q1.w, 0.0f, 4e-6f));
+            while (cm) {
+                const int k0 = 64 * (c0i + (int)__builtin_ctzll(cm));
+                cm &= cm - 1;
+                camera_wave_batch(S, wc, k0, O, D, bt, bi, cnt);
             }
         }
+    } else {
+        for (int k0 = 0; k0 < S.n_tri; k0 += 64) camera_wave_batch(S, wc, k0, O, D, bt, bi, cnt);
     }
     for (int k = 0; k < S.n_plane; ++k) {
         const float4 a = S.plane[2 * k], b = S.plane[2 * k + 1];
@@ -638,13 +670,15 @@ __device__ __forceinline__ int closest_hit_camera_wave(const SceneDev& S, const 
 }
 
 // Primary rays: wave-culled when the whole wave is here, else per lane.
-template <bool WAVE>
+// WAVE: 0 per lane only, 1 wave-level culling, 2 wave-level two-level
+// (clustered) culling.
+template <int WAVE>
 __device__ __forceinline__ int closest_hit_primary(const SceneDev& S, const Vec3 O, const Vec3 D, float& t,
                                                    Counters& cnt)
 {
-    if (WAVE && wave_full()) {
+    if (WAVE > 0 && wave_full()) {
         const WaveCone wc = wave_cone(D, true);
-        if (wc.ok) return closest_hit_camera_wave(S, wc, O, D, t, cnt);
+        if (wc.ok) return closest_hit_camera_wave<WAVE == 2>(S, wc, O, D, t, cnt);
     }
     return S.use_tricam ? closest_hit_camera(S, O, D, t, cnt) : closest_hit<true>(S, O, D, t, cnt);
 }
@@ -783,6 +817,57 @@ __global__ void rt_cone_prepass(const float4* __restrict__ tri, const float4* __
     oe[0] = ce[0];
     oe[1] = ce[1];
     oe[2] = ce[2];
+}
+
+// Cluster records for one apex (one thread per 64-triangle cluster, in
+// double), from the members' [c0 c1] records.  The wave-level member test is
+//   w . v_k >= lim_k - M,   lim_k = cosW cosT_k - sinW sinT_k,
+// and w . a >= w . v_k - |a - v_k| for any unit-ish a, so every member test
+// that passes implies
+//   w . a >= cosW C - sinW S - M,  C = min cosT_k - 2 max |a - v_k|,
+//   S = max sinT_k   (cosW >= 1/2 in every wave cone),
+// which is the cluster test (same form, a larger rounding margin).  A member
+// that is always tested (cosT <= 0) makes the cluster always tested.  For
+// lights: dmin = min, 2/dmin = max, dcap = min over the members.
+__global__ void rt_cluster_prepass(const float4* __restrict__ cone, int n, int nclu, float4* __restrict__ out)
+{
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= nclu) return;
+    const int k0 = 64 * c, k1 = min(n, k0 + 64);
+    double ax = 0, ay = 0, az = 0, cmin = 2.0, smax = 0.0, dmin = INFINITY, inv = 0.0, dcap = INFINITY;
+    bool always = false;
+    for (int k = k0; k < k1; ++k) {
+        const float4 c0 = cone[2 * k], c1 = cone[2 * k + 1];
+        always |= !(c0.w > 0.0f);
+        ax += c0.x;
+        ay += c0.y;
+        az += c0.z;
+        cmin = fmin(cmin, (double)c0.w);
+        smax = fmax(smax, (double)c1.w);
+        dmin = fmin(dmin, (double)c1.x);
+        inv = fmax(inv, (double)c1.y);
+        dcap = fmin(dcap, (double)c1.z);
+    }
+    const double an = sqrt(ax * ax + ay * ay + az * az);
+    float4 q0 = make_float4(0.f, 0.f, 0.f, -2.0f);
+    float4 q1 = make_float4(-INFINITY, 0.f, -INFINITY, 2.0f);
+    if (!always && an > 0.0 && isfinite(an)) {
+        const float4 a = make_float4((float)(ax / an), (float)(ay / an), (float)(az / an), 0.f);
+        double chord = 0.0;  // max |a - v_k| with the float a the test uses
+        for (int k = k0; k < k1; ++k) {
+            const float4 c0 = cone[2 * k];
+            const double dx = (double)a.x - c0.x, dy = (double)a.y - c0.y, dz = (double)a.z - c0.z;
+            chord = fmax(chord, sqrt(dx * dx + dy * dy + dz * dz));
+        }
+        const double C = cmin - 2.0 * chord * (1.0 + 1e-9) - 1e-7;
+        if (C > 0.0) {
+            q0 = make_float4(a.x, a.y, a.z, (float)(C * (1.0 - 1e-6)));
+            q1 = make_float4((float)(dmin * (1.0 - 1e-6)), (float)(inv * (1.0 + 1e-6)), (float)(dcap * (1.0 - 1e-6)),
+                             (float)(smax * (1.0 + 1e-6) + 1e-7));
+        }
+    }
+    out[2 * c] = q0;
+    out[2 * c + 1] = q1;
 }
 
 // Shadow-ray cull predicate (L normalised towards the light, dist to it):
@@ -1024,11 +1109,74 @@ __device__ __forceinline__ void shadow_opaque_batch(const SceneDev& S, int l0, i
     }
 }
 
+// One batch of 64 opaque triangles [k0, k0 + 64) for the lights in the bit
+// set `lights`: one lane per triangle against each light's wave cone, then
+// exact any-hit tests on the survivors; the light-independent part of the
+// test (S = P - p0, Q = S x e1, e2 . Q) is shared by the lights.
+template <int kLightBatch>
+__device__ __forceinline__ void shadow_wave_batch(const SceneDev& S, const float4* cone, size_t cstride, int k0,
+                                                  unsigned lights, const Vec3 P, const Vec3 (&L)[kLightBatch],
+                                                  const float (&dist)[kLightBatch], bool (&occ)[kLightBatch],
+                                                  const WaveCone (&wc)[kLightBatch],
+                                                  const float (&dmax)[kLightBatch], Counters& cnt)
+{
+    const int k = k0 + (int)(threadIdx.x & 63);
+    // every record load of the batch first (one wait), then the tests
+    float4 c0[kLightBatch], c1[kLightBatch];
+#pragma unroll
+    for (int j = 0; j < kLightBatch; ++j) {
+        c0[j] = make_float4(0.f, 0.f, 0.f, 1.f);
+        c1[j] = make_float4(INFINITY, 0.f, INFINITY, 0.f);  // no reach
+        if (((lights >> j) & 1u) && k < S.n_tri_opaque) {
+            const float4* rec = cone + cstride * j + 2 * k;
+            c0[j] = rec[0];
+            c1[j] = rec[1];
+        }
+    }
+    unsigned long long mj[kLightBatch], m = 0;
+#pragma unroll
+    for (int j = 0; j < kLightBatch; ++j) {
+        mj[j] = 0;
+        if (((lights >> j) & 1u) && wc[j].ok) {
+            const float ang = dmax[j] * 1e-6f * c1[j].y;
+            bool reach = (c1[j].x < dmax[j]) & cone_overlap(wc[j], c0[j], c1[j].w, ang);
+            // edge records only for sphere survivors
+            if (RT_EDGES && S.use_edges && reach)
+                reach = edges_open(wc[j], cone + cstride * j + 2 * (size_t)S.n_tri + 3 * k, ang);
+            reach |= dmax[j] > c1[j].z;
+            mj[j] = __ballot(reach);
+            m |= mj[j];
+        }
+    }
+    while (m) {
+        const int b = (int)__builtin_ctzll(m);
+        m &= m - 1;
+        const TriRec tr = load_tri(S, k0 + b);
+        const Vec3 Sv = P - tr.p0;
+        const Vec3 Q = cross(Sv, tr.e1);
+        const float tq = dot(tr.e2, Q);
+#pragma unroll
+        for (int j = 0; j < kLightBatch; ++j) {
+            if (((mj[j] >> b) & 1ull) && __any(!occ[j])) {
+                ++cnt.tri;
+                const Vec3 Pv = cross(L[j], tr.e2);
+                const float det = dot(tr.e1, Pv);
+                const float inv = recip_det(det);
+                const float u = dot(Sv, Pv) * inv;
+                const float v = dot(L[j], Q) * inv;
+                const float t = tq * inv;
+                const bool ok = !(fabsf(det) < kEps) & !((u < 0) | (u > 1)) & !((v < 0) | (u + v > 1));
+                occ[j] |= ok & (t > kEps) & (t < dist[j]);
+            }
+        }
+    }
+}
+
 // shadow_opaque_batch with wave-level culling (full wave; every light of the
 // batch with a live lane must have ok cones — else the caller uses the
 // per-lane form).  Same any-hit results: a triangle no lane of the wave can
 // reach is skipped, the rest are tested exactly per lane.
-template <int kLightBatch>
+template <int kLightBatch, bool CLU>
 __device__ __forceinline__ void shadow_opaque_wave(const SceneDev& S, int l0, int nl, const Vec3 P,
                                                    const Vec3 (&L)[kLightBatch], const float (&dist)[kLightBatch],
                                                    bool (&occ)[kLightBatch], const WaveCone (&wc)[kLightBatch],
@@ -1037,60 +1185,48 @@ __device__ __forceinline__ void shadow_opaque_wave(const SceneDev& S, int l0, in
     const float4* cone = S.cone_light + kConeRec * (size_t)S.n_tri * l0;
     const size_t cstride = kConeRec * (size_t)S.n_tri;
     const int lane = (int)(threadIdx.x & 63);
-    for (int k0 = 0; k0 < S.n_tri_opaque; k0 += 64) {
-        bool live = false;
+    if constexpr (CLU) {
+        const float4* clu = S.clu_light + 2 * (size_t)S.n_clu * l0;
+        const int ncl = (S.n_tri_opaque + 63) / 64;
+        for (int c0i = 0; c0i < ncl; c0i += 64) {
+            bool live = false;
 #pragma unroll
-        for (int j = 0; j < kLightBatch; ++j) live |= (j < nl) & !occ[j];
-        if (!__any(live)) break;
-        const int k = k0 + lane;
-        // every record load of the batch first (one wait), then the tests
-        float4 c0[kLightBatch], c1[kLightBatch];
-#pragma unroll
-        for (int j = 0; j < kLightBatch; ++j) {
-            c0[j] = make_float4(0.f, 0.f, 0.f, 1.f);
-            c1[j] = make_float4(INFINITY, 0.f, INFINITY, 0.f);  // no reach
-            if (j < nl && k < S.n_tri_opaque) {
-                const float4* rec = cone + cstride * j + 2 * k;
-                c0[j] = rec[0];
-                c1[j] = rec[1];
-            }
-        }
-        unsigned long long mj[kLightBatch], m = 0;
-#pragma unroll
-        for (int j = 0; j < kLightBatch; ++j) {
-            mj[j] = 0;
-            if (j < nl && wc[j].ok) {
-                const float ang = dmax[j] * 1e-6f * c1[j].y;
-                bool reach = (c1[j].x < dmax[j]) & cone_overlap(wc[j], c0[j], c1[j].w, ang);
-                // edge records only for sphere survivors
-                if (RT_EDGES && S.use_edges && reach)
-                    reach = edges_open(wc[j], cone + cstride * j + 2 * (size_t)S.n_tri + 3 * k, ang);
-                reach |= dmax[j] > c1[j].z;
-                mj[j] = __ballot(reach);
-                m |= mj[j];
-            }
-        }
-        while (m) {
-            const int b = (int)__builtin_ctzll(m);
-            m &= m - 1;
-            const TriRec tr = load_tri(S, k0 + b);
-            const Vec3 Sv = P - tr.p0;
-            const Vec3 Q = cross(Sv, tr.e1);
-            const float tq = dot(tr.e2, Q);
+            for (int j = 0; j < kLightBatch; ++j) live |= (j < nl) & !occ[j];
+            if (!__any(live)) break;
+            const int cl = c0i + lane;
+            unsigned long long cj[kLightBatch], cm = 0;
 #pragma unroll
             for (int j = 0; j < kLightBatch; ++j) {
-                if (((mj[j] >> b) & 1ull) && __any(!occ[j])) {
-                    ++cnt.tri;
-                    const Vec3 Pv = cross(L[j], tr.e2);
-                    const float det = dot(tr.e1, Pv);
-                    const float inv = recip_det(det);
-                    const float u = dot(Sv, Pv) * inv;
-                    const float v = dot(L[j], Q) * inv;
-                    const float t = tq * inv;
-                    const bool ok = !(fabsf(det) < kEps) & !((u < 0) | (u > 1)) & !((v < 0) | (u + v > 1));
-                    occ[j] |= ok & (t > kEps) & (t < dist[j]);
+                cj[j] = 0;
+                if (j < nl && wc[j].ok) {
+                    bool reach = false;
+                    if (cl < ncl) {
+                        const float4 q0 = clu[2 * (size_t)S.n_clu * j + 2 * cl];
+                        const float4 q1 = clu[2 * (size_t)S.n_clu * j + 2 * cl + 1];
+                        const float ang = dmax[j] * 1e-6f * q1.y;
+                        reach = ((q1.x < dmax[j]) & cone_overlap(wc[j], q0, q1.w, ang, 4e-6f)) | (dmax[j] > q1.z);
+                    }
+                    cj[j] = __ballot(reach);
+                    cm |= cj[j];
                 }
             }
+            while (cm) {
+                const int b = (int)__builtin_ctzll(cm);
+                cm &= cm - 1;
+                unsigned lights = 0;
+#pragma unroll
+                for (int j = 0; j < kLightBatch; ++j) lights |= (unsigned)((cj[j] >> b) & 1ull) << j;
+                shadow_wave_batch<kLightBatch>(S, cone, cstride, 64 * (c0i + b), lights, P, L, dist, occ, wc, dmax,
+                                               cnt);
+            }
+        }
+    } else {
+        for (int k0 = 0; k0 < S.n_tri_opaque; k0 += 64) {
+            bool live = false;
+#pragma unroll
+            for (int j = 0; j < kLightBatch; ++j) live |= (j < nl) & !occ[j];
+            if (!__any(live)) break;
+            shadow_wave_batch<kLightBatch>(S, cone, cstride, k0, (1u << nl) - 1u, P, L, dist, occ, wc, dmax, cnt);
         }
     }
     for (int k = 0; k < S.n_plane_opaque; ++k) {
@@ -1152,7 +1288,7 @@ __device__ __forceinline__ void add_light(Color& res, const Mat& m, const float4
     }
 }
 
-template <int kLightBatch, bool PF, bool WAVE>
+template <int kLightBatch, bool PF, int WAVE>
 __device__ __forceinline__ Color shade_local(const SceneDev& S, const Mat& m, const Vec3 P, const Vec3 N,
                                              const Vec3 D, Counters& cnt, bool active = true)
 {
@@ -1191,7 +1327,7 @@ __device__ __forceinline__ Color shade_local(const SceneDev& S, const Mat& m, co
             }
             occ[j] = !gate[j];
         }
-        bool use_wave = WAVE && wave_full();
+        bool use_wave = WAVE > 0 && wave_full();
         WaveCone wc[kLightBatch];
         float dmax[kLightBatch];
         if (use_wave) {
@@ -1207,7 +1343,7 @@ __device__ __forceinline__ Color shade_local(const SceneDev& S, const Mat& m, co
             }
         }
 #ifndef RT_ABLATE_SHADOW  // timing-only build: no shadow rays
-        if (use_wave) shadow_opaque_wave<kLightBatch>(S, lb, nl, P, L, dist, occ, wc, dmax, cnt);
+        if (use_wave) shadow_opaque_wave<kLightBatch, WAVE == 2>(S, lb, nl, P, L, dist, occ, wc, dmax, cnt);
         else shadow_opaque_batch<kLightBatch, PF>(S, lb, nl, P, L, dist, occ, cnt);
 #endif
 #pragma unroll
@@ -1238,7 +1374,7 @@ struct Frame {
     int surf, stage;
 };
 
-template <int MAXD, int LB, bool PF, bool WAVE>
+template <int MAXD, int LB, bool PF, int WAVE>
 __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, Counters& cnt, bool live)
 {
     const Color bg{F.bg[0], F.bg[1], F.bg[2]};
@@ -1367,7 +1503,7 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
 #endif
 // COUNT: also tally the exact tests executed (the RT_FLAG_STATS launch); in
 // the timed kernels the tallies are dead and compile away.
-template <int MAXD, int LB, bool PF, bool WAVE, bool COUNT>
+template <int MAXD, int LB, bool PF, int WAVE, bool COUNT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MAXD == 0 ? RT_WAVES_PER_EU : 1))) void rt_trace_kernel(const SceneDev S, const FrameDev F, unsigned* __restrict__ rgba,
                                                        float* __restrict__ rgbf, StatsDev* __restrict__ stats)
 {
@@ -1451,6 +1587,9 @@ struct rt_ctx {
     float4* d_cone_light = nullptr;
     float4* d_trinrm = nullptr;
     float4* d_tricoef = nullptr;
+    float4* d_clu_cam = nullptr;
+    float4* d_clu_light = nullptr;
+    int n_clu = 0;
     float cam_key[3] = {0.f, 0.f, 0.f};
     bool cam_valid = false;
     StatsDev* d_stats = nullptr;
@@ -1523,6 +1662,8 @@ RT_EXPORT void rt_destroy(rt_ctx* c)
     hipFree(c->d_cone_light);
     hipFree(c->d_trinrm);
     hipFree(c->d_tricoef);
+    hipFree(c->d_clu_cam);
+    hipFree(c->d_clu_light);
     hipFree(c->d_stats);
     hipFree(c->d_scratch);
     if (c->ev0) hipEventDestroy(c->ev0);
@@ -1532,6 +1673,56 @@ RT_EXPORT void rt_destroy(rt_ctx* c)
 }
 
 static bool nonneg_finite(float v) { return std::isfinite(v) && !std::signbit(v); }
+
+// 256 camera records = 16 KB, the scalar data cache.
+static constexpr int kTricamMaxTriangles = 256;
+static constexpr int kEdgeMaxTriangles = 1024;
+// two-level (clustered) culling above this many triangles
+static constexpr int kClusterMinTriangles = 1024;
+
+static uint32_t spread10(uint32_t v)
+{
+    v &= 1023u;
+    v = (v | (v << 16)) & 0x030000FFu;
+    v = (v | (v << 8)) & 0x0300F00Fu;
+    v = (v | (v << 4)) & 0x030C30C3u;
+    v = (v | (v << 2)) & 0x09249249u;
+    return v;
+}
+// Sort 12-float triangle records by the Morton code of their centroid, the
+// ranges [0, n_opaque) and [n_opaque, n) separately (stable).
+static void morton_order(std::vector<float>& tri, int n_opaque)
+{
+    const size_t n = tri.size() / 12;
+    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    std::vector<double> cen(3 * n);
+    for (size_t k = 0; k < n; ++k)
+        for (int a = 0; a < 3; ++a) {
+            const double p0 = tri[12 * k + a];
+            const double v = p0 + (tri[12 * k + 3 + a] + (double)tri[12 * k + 6 + a]) / 3.0;
+            cen[3 * k + a] = std::isfinite(v) ? v : 0.0;
+            lo[a] = std::min(lo[a], cen[3 * k + a]);
+            hi[a] = std::max(hi[a], cen[3 * k + a]);
+        }
+    // one scale for all axes: cubic cells, so a flat mesh is not cut along
+    // its thin axis
+    const double ext = std::max({hi[0] - lo[0], hi[1] - lo[1], hi[2] - lo[2]});
+    std::vector<uint32_t> key(n);
+    for (size_t k = 0; k < n; ++k) {
+        uint32_t q[3];
+        for (int a = 0; a < 3; ++a)
+            q[a] = ext > 0 ? (uint32_t)std::min(1023.0, std::floor((cen[3 * k + a] - lo[a]) / ext * 1024.0)) : 0u;
+        key[k] = spread10(q[0]) | (spread10(q[1]) << 1) | (spread10(q[2]) << 2);
+    }
+    std::vector<size_t> ord(n);
+    for (size_t k = 0; k < n; ++k) ord[k] = k;
+    auto cmp = [&](size_t x, size_t y) { return key[x] < key[y]; };
+    std::stable_sort(ord.begin(), ord.begin() + n_opaque, cmp);
+    std::stable_sort(ord.begin() + n_opaque, ord.end(), cmp);
+    std::vector<float> out(tri.size());
+    for (size_t k = 0; k < n; ++k) std::memcpy(&out[12 * k], &tri[12 * ord[k]], 12 * sizeof(float));
+    tri.swap(out);
+}
 
 RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
 {
@@ -1610,6 +1801,11 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
     }
     for (int i = 0; i < n; ++i)
         if (!opaque_at(i)) translucent.push_back(i);
+    // Big lists: Morton order (of the centroid) inside the opaque and the
+    // translucent ranges, so 64 consecutive triangles form a compact cluster
+    // for the two-level culling.  The order is free: closest hit is the
+    // lexicographic (t, file index) minimum and opaque shadow tests are any-hit.
+    if (tri.size() / 12 > (size_t)kClusterMinTriangles) morton_order(tri, n_tri_o);
     const int cnt_tri = (int)(tri.size() / 12), cnt_pla = (int)(pla.size() / 8), cnt_qua = (int)(qua.size() / 12);
     const int cnt_translucent = (int)translucent.size();
     tri.resize(std::max<size_t>(tri.size(), 12));
@@ -1635,7 +1831,11 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
     hipFree(c->d_cone_light);
     hipFree(c->d_trinrm);
     hipFree(c->d_tricoef);
+    hipFree(c->d_clu_cam);
+    hipFree(c->d_clu_light);
     c->d_tricam = c->d_trisph = c->d_cone_cam = c->d_cone_light = c->d_trinrm = c->d_tricoef = nullptr;
+    c->d_clu_cam = c->d_clu_light = nullptr;
+    c->n_clu = 0;
     c->cam_valid = false;
     c->d_geom = c->d_mat = c->d_lights = c->d_tri = c->d_plane = c->d_quad = nullptr;
     c->d_translucent = nullptr;
@@ -1723,6 +1923,17 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
                            c->d_cone_light + kConeRec * ntr * j);
         HIP_TRY(c, hipGetLastError());
     }
+    if (ntr > (size_t)kClusterMinTriangles) {
+        c->n_clu = (int)((ntr + 63) / 64);
+        HIP_TRY(c, hipMalloc((void**)&c->d_clu_cam, (size_t)c->n_clu * 2 * sizeof(float4)));
+        HIP_TRY(c, hipMalloc((void**)&c->d_clu_light, std::max<size_t>((size_t)c->n_clu * nl, 1) * 2 * sizeof(float4)));
+        for (int j = 0; j < nl; ++j) {
+            hipLaunchKernelGGL(rt_cluster_prepass, dim3((unsigned)((c->n_clu + 63) / 64)), dim3(64), 0, 0,
+                               c->d_cone_light + kConeRec * ntr * j, (int)ntr, c->n_clu,
+                               c->d_clu_light + 2 * (size_t)c->n_clu * j);
+            HIP_TRY(c, hipGetLastError());
+        }
+    }
     HIP_TRY(c, hipDeviceSynchronize());
     HIP_TRY(c, hipMalloc(&c->d_geom, geom.size() * sizeof(float)));
     HIP_TRY(c, hipMalloc(&c->d_mat, mat.size() * sizeof(float)));
@@ -1765,10 +1976,6 @@ static int reachable_depth(const rt_ctx* c, const rt_frame* f)
     return levels;
 }
 
-// 256 camera records = 16 KB, the scalar data cache.
-static constexpr int kTricamMaxTriangles = 256;
-static constexpr int kEdgeMaxTriangles = 1024;
-
 typedef void (*kernel_fn)(const SceneDev, const FrameDev, unsigned*, float*, StatsDev*);
 
 // Kernel variants (tools/ab_variants.py, MI355X).  Without bounces and with
@@ -1783,20 +1990,25 @@ template <bool COUNT>
 static kernel_fn pick_kernel(int depth, int n_tri, int n_lights, int& cap, int& lb)
 {
     lb = 1;
+    if (depth == 0 && n_tri > kClusterMinTriangles) {
+        cap = 0;
+        lb = RT_WAVE_LB;
+        return (kernel_fn)&rt_trace_kernel<0, RT_WAVE_LB, false, 2, COUNT>;
+    }
     if (depth == 0 && n_tri > 0) {
         cap = 0;
         lb = RT_WAVE_LB;
-        return (kernel_fn)&rt_trace_kernel<0, RT_WAVE_LB, false, true, COUNT>;
+        return (kernel_fn)&rt_trace_kernel<0, RT_WAVE_LB, false, 1, COUNT>;
     }
     if (depth == 0 && n_lights > 1) {
         cap = 0;
         lb = 3;
-        return (kernel_fn)&rt_trace_kernel<0, 3, false, false, COUNT>;
+        return (kernel_fn)&rt_trace_kernel<0, 3, false, 0, COUNT>;
     }
 #define RT_PICK(N)                                                        \
     if (depth <= N) {                                                     \
         cap = N;                                                          \
-        return (kernel_fn)&rt_trace_kernel<N, 1, false, false, COUNT>;    \
+        return (kernel_fn)&rt_trace_kernel<N, 1, false, 0, COUNT>;        \
     }
     RT_STACK_DEPTHS(RT_PICK)
 #undef RT_PICK
@@ -1826,7 +2038,8 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
     }
     const int use_tricam = c->n_tri > 0 && c->n_tri <= kTricamMaxTriangles;
     SceneDev S{c->d_geom, c->d_mat, c->d_lights, c->d_tri, c->d_plane, c->d_quad, c->d_translucent, c->d_tricam,
-               use_tricam, c->n_tri <= kEdgeMaxTriangles, c->d_cone_cam, c->d_cone_light, c->n_surf, c->n_lights, c->n_tri, c->n_plane, c->n_quad,
+               use_tricam, c->n_tri <= kEdgeMaxTriangles, c->d_cone_cam, c->d_cone_light, c->d_clu_cam,
+               c->d_clu_light, c->n_clu, c->n_surf, c->n_lights, c->n_tri, c->n_plane, c->n_quad,
                c->n_tri_opaque, c->n_plane_opaque, c->n_quad_opaque, c->n_translucent, c->shadow_split};
     FrameDev F;
     std::memcpy(F.cam, f->cam_pos, sizeof F.cam);
@@ -1861,6 +2074,11 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
         hipLaunchKernelGGL(rt_cone_prepass, dim3((c->n_tri + 255) / 256), dim3(256), 0, st, c->d_tri, c->d_trisph,
                            c->d_trinrm, c->d_tricoef, c->n_tri, cp[0], cp[1], cp[2], 1, 0.0f, c->d_cone_cam);
         HIP_TRY(c, hipGetLastError());
+        if (c->n_clu > 0) {
+            hipLaunchKernelGGL(rt_cluster_prepass, dim3((unsigned)((c->n_clu + 63) / 64)), dim3(64), 0, st,
+                               c->d_cone_cam, c->n_tri, c->n_clu, c->d_clu_cam);
+            HIP_TRY(c, hipGetLastError());
+        }
         std::memcpy(c->cam_key, f->cam_pos, sizeof c->cam_key);
         c->cam_valid = true;
     }

@@ -20,7 +20,7 @@ def _unit(v):
     return v / np.linalg.norm(v)
 
 
-def cull_stress_dat(seed: int, reflect: float = 0.0) -> str:
+def cull_stress_dat(seed: int, reflect: float = 0.0, n_small: int = 40) -> str:
     rng = np.random.default_rng(seed)
     out = ["* cull stress scene (tests/cull_scenes.py)", "        background: 0 0 150",
            "        origin: %.3f %.3f %.3f" % tuple(CAMERA), "        eye: 0.0 0.0 0.0", "        up:  0.0 1.0 0.0"]
@@ -46,7 +46,7 @@ def cull_stress_dat(seed: int, reflect: float = 0.0) -> str:
     for _ in range(12):  # large triangles (longest edge up to ~400: never culled past 110)
         c = rng.uniform([-60, -20, -150], [60, 40, -40])
         tris.append([c + rng.normal(size=3) * rng.uniform(30, 160) for _ in range(3)])
-    for _ in range(40):  # small ones
+    for _ in range(n_small):  # small ones (> 1,024 triangles in all: the clustered culling)
         c = rng.uniform([-30, -15, -30], [30, 25, 20])
         tris.append([c + rng.normal(size=3) * rng.uniform(0.05, 4.0) for _ in range(3)])
     for _ in range(12):  # slivers
@@ -66,7 +66,12 @@ def cull_stress_dat(seed: int, reflect: float = 0.0) -> str:
     return text
 
 
-def write(path, seed: int, reflect: float = 0.0) -> str:
+def write(path, seed: int, reflect: float = 0.0, n_small: int = 40) -> str:
     with open(path, "w") as f:
-        f.write(cull_stress_dat(seed, reflect))
+        f.write(cull_stress_dat(seed, reflect, n_small))
     return path
+
+
+# seeds >= 10: big lists (two-level culling, Morton-ordered triangles)
+def n_small_for(seed: int) -> int:
+    return 1500 if seed >= 10 else 40

@@ -37,7 +37,8 @@ CASES = _cases()
 
 
 def _path(tmp_path, seed, depth):
-    return cull_scenes.write(str(tmp_path / f"cs{seed}_{depth}.dat"), seed, 0.3 if depth else 0.0)
+    return cull_scenes.write(str(tmp_path / f"cs{seed}_{depth}.dat"), seed, 0.3 if depth else 0.0,
+                             cull_scenes.n_small_for(seed))
 
 
 @pytest.mark.parametrize("name,seed,w,h,depth", [c for c in CASES if c[2] <= 160])
