@@ -592,7 +592,8 @@ __device__ __forceinline__ bool edges_open(const WaveCone& wc, const float4* e, 
 // One batch of 64 triangles [k0, k0 + 64) for the wave's camera rays: one
 // lane per triangle against the wave cone, exact tests on the survivors.
 __device__ __forceinline__ void camera_wave_batch(const SceneDev& S, const WaveCone& wc, int k0, const Vec3 O,
-                                                  const Vec3 D, float& bt, int& bi, Counters& cnt)
+                                                  const Vec3 D, float& bt, int& bi, Counters& cnt,
+                                                  float far = INFINITY)
 {
     const int k = k0 + (int)(threadIdx.x & 63);
     float4 c0 = make_float4(0.f, 0.f, 0.f, 1.f), c1 = make_float4(0.f, 0.f, 0.f, 0.f);  // no reach
@@ -600,7 +601,9 @@ __device__ __forceinline__ void camera_wave_batch(const SceneDev& S, const WaveC
         c0 = S.cone_cam[2 * k];
         c1 = S.cone_cam[2 * k + 1];
     }
-    bool reach = cone_overlap(wc, c0, c1.w, 0.0f);
+    // far: every lane already holds a hit nearer than this, so a triangle
+    // whose hits all lie at t >= dmin > far cannot win
+    bool reach = cone_overlap(wc, c0, c1.w, 0.0f) & !(far < c1.x);
     // edge records only for sphere survivors
     if (RT_EDGES && S.use_edges && reach) reach = edges_open(wc, S.cone_cam + 2 * S.n_tri + 3 * k, 0.0f);
     unsigned long long m = __ballot(reach);
@@ -630,31 +633,40 @@ __device__ __forceinline__ int closest_hit_camera_wave(const SceneDev& S, const 
     float bt = -1.0f;
     int bi = -1;
     const int lane = (int)(threadIdx.x & 63);
-    if constexpr (CLU) {
-        // clusters of 64 first (cluster record implies every member's test)
-        for (int c0i = 0; c0i < S.n_clu; c0i += 64) {
-            const int cl = c0i + lane;
-            float4 q0 = make_float4(0.f, 0.f, 0.f, 1.f), q1 = make_float4(0.f, 0.f, 0.f, 0.f);  // no reach
-            if (cl < S.n_clu) {
-                q0 = S.clu_cam[2 * cl];
-                q1 = S.clu_cam[2 * cl + 1];
-            }
-            unsigned long long cm = __ballot(cone_overlap(wc, q0, q1.w, 0.0f, 4e-6f));
-            while (cm) {
-                const int k0 = 64 * (c0i + (int)__builtin_ctzll(cm));
-                cm &= cm - 1;
-                camera_wave_batch(S, wc, k0, O, D, bt, bi, cnt);
-            }
-        }
-    } else {
-        for (int k0 = 0; k0 < S.n_tri; k0 += 64) camera_wave_batch(S, wc, k0, O, D, bt, bi, cnt);
-    }
+    // planes first: their hits bound the early exit below (the minimum over
+    // (t, index) does not depend on the order)
     for (int k = 0; k < S.n_plane; ++k) {
         const float4 a = S.plane[2 * k], b = S.plane[2 * k + 1];
         float t;
         ++cnt.pla;
         const bool ok = hit_plane(make_float4(0.f, a.x, a.y, a.z), make_float4(a.w, 0.f, 0.f, 0.f), O, D, t);
         take_min(ok, t, __float_as_int(b.x), bt, bi);
+    }
+    if constexpr (CLU) {
+        // Clusters of 64 first (a cluster record implies every member's
+        // test), nearest first (rt_cluster_sort: by dmin, the id in q1.y):
+        // once every lane holds a hit nearer than the next cluster's dmin,
+        // nothing farther can win.
+        for (int c0i = 0; c0i < S.n_clu; c0i += 64) {
+            const float far = wave_max(bi >= 0 ? bt : INFINITY);
+            if (far < S.clu_cam[2 * c0i + 1].x) break;
+            const int cl = c0i + lane;
+            float4 q0 = make_float4(0.f, 0.f, 0.f, 1.f), q1 = make_float4(INFINITY, 0.f, 0.f, 0.f);  // no reach
+            if (cl < S.n_clu) {
+                q0 = S.clu_cam[2 * cl];
+                q1 = S.clu_cam[2 * cl + 1];
+            }
+            const int id = __float_as_int(q1.y);
+            unsigned long long cm = __ballot(cone_overlap(wc, q0, q1.w, 0.0f, 4e-6f) & !(far < q1.x));
+            while (cm) {
+                const int b = (int)__builtin_ctzll(cm);
+                cm &= cm - 1;
+                const int cid = __builtin_amdgcn_readlane(id, b);
+                camera_wave_batch(S, wc, 64 * cid, O, D, bt, bi, cnt, wave_max(bi >= 0 ? bt : INFINITY));
+            }
+        }
+    } else {
+        for (int k0 = 0; k0 < S.n_tri; k0 += 64) camera_wave_batch(S, wc, k0, O, D, bt, bi, cnt);
     }
     for (int k = 0; k < S.n_quad; ++k) {
         const float4* r = S.quad + 3 * k;
@@ -726,7 +738,7 @@ __global__ void rt_camera_prepass(const float4* __restrict__ tri, int n, float c
 // a sphere behind the light.  Rounding of the cull test itself: radius
 // + 2e-5 dv, cosine - 2e-5.
 //
-//   camera: c0 = [dir to centre, cosT]   c1 = [0, 0, 0, sinT]
+//   camera: c0 = [dir to centre, cosT]   c1 = [dmin, 0, 0, sinT]
 //   light : c0 = [dir to centre, cosT]   c1 = [dmin, 2/dmin, dcap, sinT]
 //   edges : [n_e, lim] for the three edges (wave-level test only; stored
 //           after the n_tri [c0 c1] pairs)
@@ -768,8 +780,11 @@ __global__ void rt_cone_prepass(const float4* __restrict__ tri, const float4* __
         const float sinT = (float)(sqrt(fmax(0.0, 1.0 - (double)cone.w * cone.w)) + 1e-7);
         if (camera) {
             if (h_eff >= (gS * (dv + r0) + gL) * phi) {
+                // dmin: no reported hit of this triangle has t < dmin (the
+                // near-regime t error is <= m/3) — the closest-hit early exit
+                const double dmin = (dv - rc - m / 3.0) * (1.0 - 1e-5);
                 c0 = cone;
-                c1 = make_float4(0.f, 0.f, 0.f, sinT);
+                c1 = make_float4((float)dmin, 0.f, 0.f, sinT);
             }
         } else {
             const double dmin = (dv - rc - m / 3.0) * (1.0 - 1e-5);
@@ -868,6 +883,24 @@ __global__ void rt_cluster_prepass(const float4* __restrict__ cone, int n, int n
     }
     out[2 * c] = q0;
     out[2 * c + 1] = q1;
+}
+
+// Camera cluster records in increasing dmin (rank sort, one thread per
+// cluster; ties by id), the cluster id in q1.y (unused by camera tests).
+__global__ void rt_cluster_sort(const float4* __restrict__ in, int nclu, float4* __restrict__ out)
+{
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= nclu) return;
+    const float key = in[2 * c + 1].x;
+    int rank = 0;
+    for (int j = 0; j < nclu; ++j) {
+        const float kj = in[2 * j + 1].x;
+        rank += (kj < key) | ((kj == key) & (j < c));
+    }
+    float4 q1 = in[2 * c + 1];
+    q1.y = __int_as_float(c);
+    out[2 * rank] = in[2 * c];
+    out[2 * rank + 1] = q1;
 }
 
 // Shadow-ray cull predicate (L normalised towards the light, dist to it):
@@ -1925,7 +1958,7 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
     }
     if (ntr > (size_t)kClusterMinTriangles) {
         c->n_clu = (int)((ntr + 63) / 64);
-        HIP_TRY(c, hipMalloc((void**)&c->d_clu_cam, (size_t)c->n_clu * 2 * sizeof(float4)));
+        HIP_TRY(c, hipMalloc((void**)&c->d_clu_cam, (size_t)c->n_clu * 4 * sizeof(float4)));
         HIP_TRY(c, hipMalloc((void**)&c->d_clu_light, std::max<size_t>((size_t)c->n_clu * nl, 1) * 2 * sizeof(float4)));
         for (int j = 0; j < nl; ++j) {
             hipLaunchKernelGGL(rt_cluster_prepass, dim3((unsigned)((c->n_clu + 63) / 64)), dim3(64), 0, 0,
@@ -2075,8 +2108,12 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
                            c->d_trinrm, c->d_tricoef, c->n_tri, cp[0], cp[1], cp[2], 1, 0.0f, c->d_cone_cam);
         HIP_TRY(c, hipGetLastError());
         if (c->n_clu > 0) {
+            float4* tmp = c->d_clu_cam + 2 * (size_t)c->n_clu;  // second half: unsorted
             hipLaunchKernelGGL(rt_cluster_prepass, dim3((unsigned)((c->n_clu + 63) / 64)), dim3(64), 0, st,
-                               c->d_cone_cam, c->n_tri, c->n_clu, c->d_clu_cam);
+                               c->d_cone_cam, c->n_tri, c->n_clu, tmp);
+            HIP_TRY(c, hipGetLastError());
+            hipLaunchKernelGGL(rt_cluster_sort, dim3((unsigned)((c->n_clu + 255) / 256)), dim3(256), 0, st, tmp,
+                               c->n_clu, c->d_clu_cam);
             HIP_TRY(c, hipGetLastError());
         }
         std::memcpy(c->cam_key, f->cam_pos, sizeof c->cam_key);
