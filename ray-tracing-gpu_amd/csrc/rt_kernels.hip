@@ -142,7 +142,24 @@ constexpr int kStatSlots = 256;
 struct Counters {
     unsigned primary = 0, bounce = 0, shadow = 0, skipped = 0;
     unsigned tri = 0, pla = 0, qua = 0;
+#ifdef RT_PROF  // diagnostic build (tools/prof_sections.py): shader clocks per section
+    unsigned long long pt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long last = 0;
+#endif
 };
+#ifdef RT_PROF
+#define RT_MARK(cnt, i)                                           \
+    do {                                                          \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+        (cnt).pt[i] += t_ - (cnt).last;                           \
+        (cnt).last = t_;                                          \
+    } while (0)
+__device__ unsigned long long rt_prof_acc[8];
+#else
+#define RT_MARK(cnt, i) \
+    do {                \
+    } while (0)
+#endif
 
 // ----------------------------------------------------- exact fast reciprocal
 // IEEE 1.0f/x in 3 VALU instead of the ~10-instruction division expansion:
@@ -1354,12 +1371,15 @@ __device__ __forceinline__ Color shade_local(const SceneDev& S, const Mat& m, co
                 const float4 l0 = S.lights[2 * (lb + j)];
                 const Vec3 Lr = make3(l0.x, l0.y, l0.z) - P;
                 gate[j] = active & (dot(Lr, N) > 0);  // Scene.cpp:1756, unnormalised
-                dist[j] = norm(Lr);                // Scene.cpp:1847-1848
-                L[j] = div_recip(Lr, dist[j]);
+                // Scene.cpp:1847-1848: norm + one reciprocal, by the exact
+                // fast sequences (rt_fastmath.h) when the whole wave is in range
+                dist[j] = sqrt_w(Lr.x * Lr.x + Lr.y * Lr.y + Lr.z * Lr.z);
+                L[j] = Lr * recip_w(dist[j]);
                 cnt.shadow += gate[j];
             }
             occ[j] = !gate[j];
         }
+        RT_MARK(cnt, 2);
         bool use_wave = WAVE > 0 && wave_full();
         WaveCone wc[kLightBatch];
         float dmax[kLightBatch];
@@ -1376,9 +1396,11 @@ __device__ __forceinline__ Color shade_local(const SceneDev& S, const Mat& m, co
             }
         }
 #ifndef RT_ABLATE_SHADOW  // timing-only build: no shadow rays
+        RT_MARK(cnt, 3);
         if (use_wave) shadow_opaque_wave<kLightBatch, WAVE == 2>(S, lb, nl, P, L, dist, occ, wc, dmax, cnt);
         else shadow_opaque_batch<kLightBatch, PF>(S, lb, nl, P, L, dist, occ, cnt);
 #endif
+        RT_MARK(cnt, 4);
 #pragma unroll
         for (int j = 0; j < kLightBatch; ++j) {
             if (j < nl && gate[j]) {
@@ -1394,6 +1416,7 @@ __device__ __forceinline__ Color shade_local(const SceneDev& S, const Mat& m, co
                 add_light(res, m, l0, l1, N, L[j], D, F);
             }
         }
+        RT_MARK(cnt, 5);
     }
     return res;
 }
@@ -1416,7 +1439,9 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
         return Color{D.x, D.y, D.z};
 #endif
         float t;
+        RT_MARK(cnt, 0);
         const int idx = closest_hit_primary<WAVE>(S, O, D, t, cnt);
+        RT_MARK(cnt, 1);
         // Lanes that miss (or lie outside the frame) stay in step through the
         // shading so the wave stays whole for wave-level shadow culling.
         const bool hit = idx >= 0;
@@ -1425,8 +1450,18 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
         return Color{t, (float)idx, 0.f};
 #endif
         const int sidx = hit ? idx : 0;
-        const Vec3 N = hit_normal(S, sidx, O, D, t);
-        const Mat m = load_mat(S, sidx);
+        // A tile usually sees one surface: then its normal and material
+        // records come by scalar (broadcast) loads instead of a per-lane gather.
+        const int s0 = __builtin_amdgcn_readfirstlane(sidx);
+        Vec3 N;
+        Mat m;
+        if (__all(sidx == s0)) {
+            N = hit_normal(S, s0, O, D, t);
+            m = load_mat(S, s0);
+        } else {
+            N = hit_normal(S, sidx, O, D, t);
+            m = load_mat(S, sidx);
+        }
         const Vec3 P = O + t * D;
         const Color c = shade_local<LB, PF, WAVE>(S, m, P, N, D, cnt, hit & live);
         return hit ? c : bg;
@@ -1548,6 +1583,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MAXD == 0 ?
     const bool valid = px < F.width && py < F.row_end;
 
     Counters cnt;
+#ifdef RT_PROF
+    cnt.last = __builtin_amdgcn_s_memtime();
+#endif
     Color c{0.f, 0.f, 0.f};
     // Without bounces every lane runs (lanes outside the frame on a clamped
     // pixel, result dropped) so edge waves stay whole for wave-level culling.
@@ -1573,6 +1611,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MAXD == 0 ?
             if (rgba) rgba[o] = unorm8(c.r) | (unorm8(c.g) << 8) | (unorm8(c.b) << 16) | 0xFF000000u;
         }
     }
+#ifdef RT_PROF
+    RT_MARK(cnt, 6);
+    if ((threadIdx.x & 63) == 0)
+        for (int i = 0; i < 8; ++i) atomicAdd(&rt_prof_acc[i], cnt.pt[i]);
+#endif
     if (F.flags & RT_FLAG_STATS) {
         unsigned long long v[7] = {cnt.primary, cnt.bounce, cnt.shadow, cnt.skipped, cnt.tri, cnt.pla, cnt.qua};
         StatsDev* sl = stats + ((blockIdx.x + blockIdx.y * gridDim.x) % kStatSlots);
@@ -2216,3 +2259,16 @@ RT_EXPORT int rt_last_stats(rt_ctx* c, rt_stats* out)
     *out = c->last;
     return RT_OK;
 }
+
+#ifdef RT_PROF
+// Diagnostic builds only (not in include/rt.h): read and clear the per-section
+// shader-clock totals (summed over waves).
+extern "C" __attribute__((visibility("default"))) int rt_debug_prof(unsigned long long* out8)
+{
+    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(rt::rt_prof_acc), 8 * sizeof(unsigned long long)) != hipSuccess)
+        return RT_E_HIP;
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(rt::rt_prof_acc), z, sizeof z) != hipSuccess) return RT_E_HIP;
+    return RT_OK;
+}
+#endif

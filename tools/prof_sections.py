@@ -1,0 +1,55 @@
+"""Per-section shader-clock breakdown of the trace kernel (diagnostic).
+
+Builds with -DRT_PROF accumulate s_memtime deltas per wave into 8 sections
+(0 set-up, 1 primary closest hit, 2 shading set-up + light vectors, 3 wave
+cones, 4 shadow tests, 5 translucent filter + Lambert/Phong, 6 store/stats);
+this renders a config K times with such a build and prints each section's
+share of the summed wave time.
+
+    python tools/prof_sections.py ray-tracing-gpu_amd/lib/var/prof.so --config c2
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "ray-tracing-gpu_amd"))
+sys.path.insert(0, REPO)
+
+NAMES = ["setup", "primary", "shade_setup", "wave_cones", "shadow_tests", "lambert_phong", "store"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("lib")
+    ap.add_argument("--config", default="c2")
+    ap.add_argument("--frames", type=int, default=20)
+    a = ap.parse_args()
+    os.environ["RT_AMD_LIB"] = os.path.abspath(a.lib)
+    import torch  # noqa: F401  (one HIP runtime)
+
+    import bench
+    import rt_amd
+
+    L = rt_amd.lib()
+    L.rt_debug_prof.argtypes = [ctypes.c_void_p]
+    name, W, H, depth = bench.CONFIGS[a.config]
+    s = rt_amd.Scene(bench.scene_path(name), W, H, depth)
+    ctx = rt_amd.Context(0)
+    ctx.upload(s)
+    ctx.render(s.frame)
+    buf = (ctypes.c_ulonglong * 8)()
+    L.rt_debug_prof(buf)  # clear
+    for _ in range(a.frames):
+        ctx.render(s.frame)
+    L.rt_debug_prof(buf)
+    tot = sum(buf[:7]) or 1
+    print(json.dumps({"config": a.config, "frames": a.frames,
+                      "share": {n: round(buf[i] / tot, 4) for i, n in enumerate(NAMES)},
+                      "wave_clocks_per_frame": {n: buf[i] // a.frames for i, n in enumerate(NAMES)}}))
+
+
+if __name__ == "__main__":
+    main()
