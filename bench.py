@@ -121,6 +121,45 @@ def cpu_baseline(path, w, h, depth, seconds):
                       f"{w}x{h} depth={depth} frame, {el:.1f} s, serial like the reference loop"}
 
 
+def cpu_allcores(path, w, h, depth, seconds):
+    """the C restatement (oracle/liboracle.so, OpenMP over
+    rows, bit-identical to the reference) on all the host cores this job may
+    use, over 64x64 windows spread over the frame until `seconds` elapse."""
+    import numpy as np
+
+    port = os.path.join(REPO, "oracle", "liboracle.so")
+    if not os.path.exists(port):
+        import subprocess
+
+        subprocess.run(["make", "-s", "-C", os.path.join(REPO, "oracle")], check=True)
+    L = ctypes.CDLL(port)
+    VP = ctypes.c_void_p
+    L.oracle_load.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(VP)]
+    L.oracle_render_window.argtypes = [VP, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, VP, ctypes.c_int]
+    L.oracle_free.argtypes = [VP]
+    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)), os.cpu_count() or 1))
+    p = VP()
+    assert L.oracle_load(path.encode(), w, h, depth, ctypes.byref(p)) == 0
+    n = 64
+    buf = np.zeros((n, n, 3), np.float32)
+    wins = [(r, c) for r in range(0, max(1, h - n + 1), max(n, h // 8)) for c in range(0, max(1, w - n + 1), max(n, w // 8))]
+    order = np.random.default_rng(4321).permutation(len(wins))
+    px, k = 0, 0
+    t0 = time.perf_counter()
+    while True:
+        r, c = wins[order[k % len(wins)]]
+        L.oracle_render_window(p, r, min(h, r + n), c, min(w, c + n), buf.ctypes.data, threads)
+        px += (min(h, r + n) - r) * (min(w, c + n) - c)
+        k += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    L.oracle_free(p)
+    return {"value": round(px / el / 1e6, 4), "unit": "Mray/s", "cores": threads, "kind": "port",
+            "sample": f"{k} 64x64 windows ({px} primary rays) of the {w}x{h} depth={depth} frame, "
+                      f"{el:.1f} s, OpenMP over rows"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -266,6 +305,9 @@ def main():
             cb = cpu_baseline(path, W, H, depth, args.cpu_seconds)
             cb["gpu_over_cpu"] = round(value / cb["value"], 1) if cb["value"] else None
             out["cpu_baseline"] = cb
+            ca = cpu_allcores(path, W, H, depth, max(2.0, args.cpu_seconds / 2))
+            ca["gpu_over_cpu"] = round(value / ca["value"], 1) if ca["value"] else None
+            out["cpu_baseline_allcores"] = ca
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
