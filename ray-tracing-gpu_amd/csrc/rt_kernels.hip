@@ -1423,11 +1423,17 @@ __device__ __forceinline__ Color shade_local(const SceneDev& S, const Mat& m, co
 
 // One pixel's colour.  MAXD = compile-time bounce-stack capacity (0 = no
 // bounces: the reference as shipped).
+// A pushed node: its colour so far, its surface, and which child runs:
+// 0 reflected (no refraction to follow), 2 reflected (the refracted ray is
+// waiting in Refr), 1 refracted.  5 dwords; the 8-dword Refr is written only
+// by nodes that spawn both children.
 struct Frame {
     Color acc;
-    Vec3 P, N, D;
-    float rior, energy;
     int surf, stage;
+};
+struct Refr {
+    Vec3 P, D;
+    float rior, energy;
 };
 
 template <int MAXD, int LB, bool PF, int WAVE>
@@ -1467,6 +1473,7 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
         return hit ? c : bg;
     } else {
         Frame stk[MAXD];
+        Refr rf[MAXD];
         int sp = 0;
         float rior = 1.0f, energy = 1.0f;
         Color ret{0.f, 0.f, 0.f};
@@ -1489,36 +1496,42 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
                     const bool doR = er > F.min_energy && can;
                     const bool doT = et > F.min_energy && can;
                     if (doR || doT) {
-                        Frame& fr = stk[sp++];
+                        Frame& fr = stk[sp];
                         fr.acc = acc;
-                        fr.P = P;
-                        fr.N = N;
-                        fr.D = D;
-                        fr.rior = rior;
-                        fr.energy = energy;
                         fr.surf = idx;
                         ++cnt.bounce;
+                        // The refracted ray (Scene.cpp:1793-1822), from this
+                        // node's incoming ray — the same values whether it
+                        // is traced now or after the reflected subtree.
+                        Vec3 Dt = D;
+                        float rior_t = rior;
+                        if (doT) {
+                            Vec3 n = N;
+                            float ratio;
+                            if (rior == m.ior) {  // Scene.cpp:1797-1803 inside -> out
+                                rior_t = F.scene_ior;
+                                ratio = m.ior / F.scene_ior;
+                                n = -n;
+                            } else {
+                                rior_t = m.ior;
+                                ratio = F.scene_ior / m.ior;
+                            }
+                            Dt = refract(D, n, ratio);
+                        }
                         O = P;
                         if (doR) {  // Scene.cpp:1782-1788: IOR left at CRayon's default 0
-                            fr.stage = 0;
+                            fr.stage = doT ? 2 : 0;
+                            if (doT) rf[sp] = Refr{P, Dt, rior_t, et};
                             D = reflect(D, N);
                             rior = 0.0f;
                             energy = er;
                         } else {
                             fr.stage = 1;
-                            Vec3 n = N;
-                            float ratio;
-                            if (rior == m.ior) {  // Scene.cpp:1797-1803 inside -> out
-                                rior = F.scene_ior;
-                                ratio = m.ior / F.scene_ior;
-                                n = -n;
-                            } else {
-                                rior = m.ior;
-                                ratio = F.scene_ior / m.ior;
-                            }
-                            D = refract(D, n, ratio);
+                            D = Dt;
+                            rior = rior_t;
                             energy = et;
                         }
+                        ++sp;
                         continue;
                     }
                     ret = acc;
@@ -1528,25 +1541,16 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
             if (sp == 0) return ret;
             Frame& fr = stk[sp - 1];
             const Mat m = load_mat(S, fr.surf);
-            if (fr.stage == 0) {
+            if (fr.stage != 1) {
                 fr.acc += ret * m.kr;  // Scene.cpp:1787
-                const float et = m.kt * fr.energy;
-                if (et > F.min_energy && (sp - 1) < F.max_bounces) {
+                if (fr.stage == 2) {   // the refracted child (Scene.cpp:1790)
                     fr.stage = 1;
                     ++cnt.bounce;
-                    Vec3 n = fr.N;
-                    float ratio;
-                    if (fr.rior == m.ior) {
-                        rior = F.scene_ior;
-                        ratio = m.ior / F.scene_ior;
-                        n = -n;
-                    } else {
-                        rior = m.ior;
-                        ratio = F.scene_ior / m.ior;
-                    }
-                    O = fr.P;
-                    D = refract(fr.D, n, ratio);
-                    energy = et;
+                    const Refr r = rf[sp - 1];
+                    O = r.P;
+                    D = r.D;
+                    rior = r.rior;
+                    energy = r.energy;
                     trace = true;
                     continue;
                 }
