@@ -948,6 +948,24 @@ __device__ __forceinline__ Mat load_mat(const SceneDev& S, int idx)
     return Mat{{m0.x, m0.y, m0.z}, m0.w, m1.x, m1.y, m1.z, m1.w, m2.x, m2.y};
 }
 
+// An opaque plane against a shadow ray: Plan.cpp:128-144 and the filter's
+// window EPS < t < dist (Scene.cpp:1853).  t = -num / vd is only divided
+// out when some lane could pass: never when |vd| <= EPS, when num and vd
+// share a sign (t <= 0), or when |num| < 0.0099 |vd| (then |t| < EPS even
+// after rounding) — the common cases of points above a ground plane and of
+// points on it.
+__device__ __forceinline__ bool shadow_plane_hit(const float4 a, const Vec3 P, const Vec3 L, float dist)
+{
+    const Vec3 n = make3(a.x, a.y, a.z);
+    const float vd = dot(n, L);
+    const float num = dot(n, P) + a.w;
+    const bool maybe = (fabsf(vd) > kEps) & (((num < 0) & (vd > 0)) | ((num > 0) & (vd < 0))) &
+                       !(fabsf(num) < 0.0099f * fabsf(vd));
+    if (!__any(maybe)) return false;
+    const float t = -num / vd;
+    return (fabsf(vd) > kEps) & (t > kEps) & (t < dist);
+}
+
 // One file-order surface record against a shadow ray (generic path).
 __device__ __forceinline__ bool shadow_hit_record(const float4* rec, const Vec3 P, const Vec3 L, float dist,
                                                   Color& fc, Counters& cnt)
@@ -1136,10 +1154,8 @@ __device__ __forceinline__ void shadow_opaque_batch(const SceneDev& S, int l0, i
 #pragma unroll
         for (int j = 0; j < kLightBatch; ++j) {
             if (j < nl && __any(!occ[j])) {
-                float t;
                 ++cnt.pla;
-                const bool ok = hit_plane(make_float4(0.f, a.x, a.y, a.z), make_float4(a.w, 0.f, 0.f, 0.f), P, L[j], t);
-                occ[j] |= ok & (t > kEps) & (t < dist[j]);
+                occ[j] |= shadow_plane_hit(a, P, L[j], dist[j]);
             }
         }
     }
@@ -1284,10 +1300,8 @@ __device__ __forceinline__ void shadow_opaque_wave(const SceneDev& S, int l0, in
 #pragma unroll
         for (int j = 0; j < kLightBatch; ++j) {
             if (j < nl && __any(!occ[j])) {
-                float t;
                 ++cnt.pla;
-                const bool ok = hit_plane(make_float4(0.f, a.x, a.y, a.z), make_float4(a.w, 0.f, 0.f, 0.f), P, L[j], t);
-                occ[j] |= ok & (t > kEps) & (t < dist[j]);
+                occ[j] |= shadow_plane_hit(a, P, L[j], dist[j]);
             }
         }
     }
