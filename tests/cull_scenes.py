@@ -22,9 +22,15 @@ def _unit(v):
 
 def cull_stress_dat(seed: int, reflect: float = 0.0, n_small: int = 40) -> str:
     rng = np.random.default_rng(seed)
+    camera, lights = CAMERA, LIGHTS
+    if seed >= 100:  # randomised viewpoint and lights (tests/test_cull_stress.py vs the oracle)
+        camera = rng.uniform([-80, -10, 20], [80, 90, 120])
+        lights = [(rng.uniform([-150, -15, -150], [150, 300, 150]), 0.5),
+                  (rng.uniform([-60, -15, -60], [60, 60, 60]), 0.4),
+                  (rng.normal(size=3) * 3000.0, 0.3)]
     out = ["* cull stress scene (tests/cull_scenes.py)", "        background: 0 0 150",
-           "        origin: %.3f %.3f %.3f" % tuple(CAMERA), "        eye: 0.0 0.0 0.0", "        up:  0.0 1.0 0.0"]
-    for i, (p, inten) in enumerate(LIGHTS):
+           "        origin: %.3f %.3f %.3f" % tuple(camera), "        eye: 0.0 0.0 0.0", "        up:  0.0 1.0 0.0"]
+    for i, (p, inten) in enumerate(lights):
         out += [f"Lumiere: l{i}", "        position: %.3f %.3f %.3f" % tuple(p), f"        intens: {inten}"]
     out += ["Plane: ground", "        v_linear: 0.0 1.0 0.0", "        v_const:  20.0",
             "        color:   10 255 11", "        ambient: 0.3", "        diffus:  0.7"]
@@ -40,8 +46,8 @@ def cull_stress_dat(seed: int, reflect: float = 0.0, n_small: int = 40) -> str:
             pts = [q + s * (x * a + y * w) for x, y in rng.uniform(-1, 1, (3, 2))]
             tris.append(pts)
 
-    edge_on(CAMERA, 30, 12.0)
-    for p, _ in LIGHTS[:2]:
+    edge_on(camera, 30, 12.0)
+    for p, _ in lights[:2]:
         edge_on(p, 25, 12.0)
     for _ in range(12):  # large triangles (longest edge up to ~400: never culled past 110)
         c = rng.uniform([-60, -20, -150], [60, 40, -40])

@@ -59,3 +59,26 @@ def test_gpu_matches_reference(cull_golden, tmp_path, name, seed, w, h, depth):
     want = cull_golden[name]
     bad = np.argwhere(~(got.view(np.uint32) == want.view(np.uint32)).all(-1))
     assert bits_equal(got, want), f"{len(bad)} pixels differ, first {bad[:5].tolist()}"
+
+
+# Randomised viewpoints and lights (seeds >= 100), small frames: the GPU
+# against the oracle restatement (itself pinned bit-for-bit to the reference
+# above and in test_oracle.py).  Seeds 106+ add 1,200 small triangles (the
+# two-level culling); every third seed renders with bounces.
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(100, 112))
+def test_gpu_matches_oracle_random_views(oracle, tmp_path, seed):
+    import rt_amd
+
+    depth = 3 if seed % 3 == 0 else 0
+    n_small = 1200 if seed >= 106 else 60
+    path = cull_scenes.write(str(tmp_path / f"r{seed}.dat"), seed, 0.3 if depth else 0.0, n_small)
+    w, h = 96, 72
+    ctx = rt_amd.Context(0)
+    s = rt_amd.Scene(path, w, h, depth)
+    ctx.upload(s)
+    got = ctx.render_float(s.frame)
+    want = oracle.render(path, w, h, depth)
+    bad = np.argwhere(~(got.view(np.uint32) == want.view(np.uint32)).all(-1))
+    assert bits_equal(got, want), f"{len(bad)} pixels differ, first {bad[:5].tolist()}"
+
