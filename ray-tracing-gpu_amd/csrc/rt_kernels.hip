@@ -584,10 +584,17 @@ __device__ __forceinline__ WaveCone wave_cone(const Vec3 d, bool live)
 }
 // May some ray of the wave cone reach the triangle cone [c0.xyz, c0.w; c1.w]?
 // ang = extra angular slack.
+// ang = extra angular slack, applied as a wider wave cone W + ang:
+// cos(W + a) >= cosW - a sinW - a^2/2 and sin(W + a) <= sinW + a cosW, both
+// within a^2 of the true values, so the test is cos(W + a + T) minus the
+// rounding margin to within ~1e-10 — the angle-space form the cluster
+// records rely on (rt_cluster_prepass).
 __device__ __forceinline__ bool cone_overlap(const WaveCone& wc, const float4 c0, float sinT, float ang,
                                              float margin = 2e-6f)
 {
-    const float lim = wc.cosW * c0.w - wc.sinW * sinT - margin - ang;
+    const float cw = wc.cosW - ang * wc.sinW - 0.5f * ang * ang;
+    const float sw = wc.sinW + ang * wc.cosW;
+    const float lim = cw * c0.w - sw * sinT - margin;
     return !(c0.w > 0.0f) | (dot(wc.w, make3(c0.x, c0.y, c0.z)) >= lim);
 }
 
@@ -852,30 +859,30 @@ __global__ void rt_cone_prepass(const float4* __restrict__ tri, const float4* __
 }
 
 // Cluster records for one apex (one thread per 64-triangle cluster, in
-// double), from the members' [c0 c1] records.  The wave-level member test is
-//   w . v_k >= lim_k - M,   lim_k = cosW cosT_k - sinW sinT_k,
-// and w . a >= w . v_k - |a - v_k| for any unit-ish a, so every member test
-// that passes implies
-//   w . a >= cosW C - sinW S - M,  C = min cosT_k - 2 max |a - v_k|,
-//   S = max sinT_k   (cosW >= 1/2 in every wave cone),
-// which is the cluster test (same form, a larger rounding margin).  A member
-// that is always tested (cosT <= 0) makes the cluster always tested.  For
-// lights: dmin = min, 2/dmin = max, dcap = min over the members.
+// double), from the members' [c0 c1] records.  A member's wave test passes
+// only if  w . v_k >= cos(W' + T_k) - 3e-6  (W' = W widened by the angular
+// slack, T_k = acos(cosT_k), 2e-6 margin + 1e-6 rounding), i.e. only if
+// angle(w, v_k) <= W' + T_k + d0 with d0 = arccos(1 - 3e-6) < 2.5e-3.  Then
+// angle(w, a) <= W' + T_k + d0 + angle(a, v_k) <= W' + T_c for
+//   T_c = max_k (angle(a, v_k) + T_k) + 2.5e-3,
+// and the cluster test (the same form, its slack >= every member's) passes:
+// a surviving member always has a surviving cluster.  A member that is
+// always tested (cosT <= 0), or T_c >= 80 degrees, makes the cluster always
+// tested.  For lights: dmin = min, 2/dmin = max, dcap = min over the members.
 __global__ void rt_cluster_prepass(const float4* __restrict__ cone, int n, int nclu, float4* __restrict__ out)
 {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= nclu) return;
     const int k0 = 64 * c, k1 = min(n, k0 + 64);
-    double ax = 0, ay = 0, az = 0, cmin = 2.0, smax = 0.0, dmin = INFINITY, inv = 0.0, dcap = INFINITY;
+    double ax = 0, ay = 0, az = 0, dmin = INFINITY, inv = 0.0, dcap = INFINITY;
     bool always = false;
     for (int k = k0; k < k1; ++k) {
         const float4 c0 = cone[2 * k], c1 = cone[2 * k + 1];
         always |= !(c0.w > 0.0f);
-        ax += c0.x;
-        ay += c0.y;
-        az += c0.z;
-        cmin = fmin(cmin, (double)c0.w);
-        smax = fmax(smax, (double)c1.w);
+        const double vn = sqrt((double)c0.x * c0.x + (double)c0.y * c0.y + (double)c0.z * c0.z);
+        ax += c0.x / vn;
+        ay += c0.y / vn;
+        az += c0.z / vn;
         dmin = fmin(dmin, (double)c1.x);
         inv = fmax(inv, (double)c1.y);
         dcap = fmin(dcap, (double)c1.z);
@@ -884,18 +891,22 @@ __global__ void rt_cluster_prepass(const float4* __restrict__ cone, int n, int n
     float4 q0 = make_float4(0.f, 0.f, 0.f, -2.0f);
     float4 q1 = make_float4(-INFINITY, 0.f, -INFINITY, 2.0f);
     if (!always && an > 0.0 && isfinite(an)) {
+        // the float axis the test uses, normalised in double for the angles
         const float4 a = make_float4((float)(ax / an), (float)(ay / an), (float)(az / an), 0.f);
-        double chord = 0.0;  // max |a - v_k| with the float a the test uses
+        const double al = sqrt((double)a.x * a.x + (double)a.y * a.y + (double)a.z * a.z);
+        double Tc = 0.0;
         for (int k = k0; k < k1; ++k) {
             const float4 c0 = cone[2 * k];
-            const double dx = (double)a.x - c0.x, dy = (double)a.y - c0.y, dz = (double)a.z - c0.z;
-            chord = fmax(chord, sqrt(dx * dx + dy * dy + dz * dz));
+            const double vx = c0.x, vy = c0.y, vz = c0.z;
+            const double cx = a.y * vz - a.z * vy, cy = a.z * vx - a.x * vz, cz = a.x * vy - a.y * vx;
+            const double ang = atan2(sqrt(cx * cx + cy * cy + cz * cz), a.x * vx + a.y * vy + a.z * vz);
+            Tc = fmax(Tc, ang + acos(fmin(1.0, (double)c0.w)));
         }
-        const double C = cmin - 2.0 * chord * (1.0 + 1e-9) - 1e-7;
-        if (C > 0.0) {
-            q0 = make_float4(a.x, a.y, a.z, (float)(C * (1.0 - 1e-6)));
+        Tc = Tc * (1.0 + 1e-9) + 2.5e-3 + 1e-6 + 4.0 * fabs(al - 1.0);
+        if (Tc < 1.396) {  // 80 degrees
+            q0 = make_float4(a.x, a.y, a.z, (float)(cos(Tc) - 1e-7));
             q1 = make_float4((float)(dmin * (1.0 - 1e-6)), (float)(inv * (1.0 + 1e-6)), (float)(dcap * (1.0 - 1e-6)),
-                             (float)(smax * (1.0 + 1e-6) + 1e-7));
+                             (float)(sin(Tc) + 1e-7));
         }
     }
     out[2 * c] = q0;
