@@ -2,7 +2,10 @@
 
 Builds with -DRT_PROF accumulate s_memtime deltas per wave into 8 sections
 (0 set-up, 1 primary closest hit, 2 shading set-up + light vectors, 3 wave
-cones, 4 shadow tests, 5 translucent filter + Lambert/Phong, 6 store/stats);
+cones + shadow culling, 4 exact shadow triangle tests, 5 translucent filter +
+Lambert/Phong, 6 store/stats, 7 shadow plane tests; marks are scheduling
+barriers, so the build is slower than the product) and wave-level event
+counts (cluster batches, member batches, exact tests per wave);
 this renders a config K times with such a build and prints each section's
 share of the summed wave time.
 
@@ -18,7 +21,10 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "ray-tracing-gpu_amd"))
 sys.path.insert(0, REPO)
 
-NAMES = ["setup", "primary", "shade_setup", "wave_cones", "shadow_tests", "lambert_phong", "store"]
+# wave-level events (per wave): cluster batches, member batches, exact tests
+EVENTS = ["cam_cluster_batches", "cam_member_batches", "cam_exact", "shadow_cluster_ballots",
+          "shadow_member_batches", "shadow_exact", "shadow_clusters_by_dcap_only", "shadow_clusters_by_cone"]
+NAMES = ["setup", "primary", "shade_setup", "shadow_cull", "shadow_exact_tri", "lambert_phong", "store", "shadow_planes"]
 
 
 def main():
@@ -35,20 +41,26 @@ def main():
 
     L = rt_amd.lib()
     L.rt_debug_prof.argtypes = [ctypes.c_void_p]
+    L.rt_debug_prof_events.argtypes = [ctypes.c_void_p]
     name, W, H, depth = bench.CONFIGS[a.config]
     s = rt_amd.Scene(bench.scene_path(name), W, H, depth)
     ctx = rt_amd.Context(0)
     ctx.upload(s)
     ctx.render(s.frame)
     buf = (ctypes.c_ulonglong * 8)()
+    ev = (ctypes.c_ulonglong * 8)()
     L.rt_debug_prof(buf)  # clear
+    L.rt_debug_prof_events(ev)
     for _ in range(a.frames):
         ctx.render(s.frame)
     L.rt_debug_prof(buf)
-    tot = sum(buf[:7]) or 1
+    L.rt_debug_prof_events(ev)
+    waves = ((W + 7) // 8) * ((H + 7) // 8) * a.frames
+    tot = sum(buf[:8]) or 1
     print(json.dumps({"config": a.config, "frames": a.frames,
                       "share": {n: round(buf[i] / tot, 4) for i, n in enumerate(NAMES)},
-                      "wave_clocks_per_frame": {n: buf[i] // a.frames for i, n in enumerate(NAMES)}}))
+                      "wave_clocks_per_frame": {n: buf[i] // a.frames for i, n in enumerate(NAMES)},
+                      "events_per_wave": {n: round(ev[i] / waves, 2) for i, n in enumerate(EVENTS) if n}}))
 
 
 if __name__ == "__main__":
