@@ -568,7 +568,7 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
 
 struct WaveCone {
     Vec3 w;
-    float cosW, sinW;
+    float cosW, sinW, chord;  // chord = |d - w| bound = 2 sin(W/2)
     bool ok;
 };
 // Cone of the live lanes' unit directions d (apex shared).  ok = false when
@@ -586,6 +586,7 @@ __device__ __forceinline__ WaveCone wave_cone(const Vec3 d, bool live)
     c.cosW = wave_min(cd) - 1e-6f;
     c.ok = c.cosW >= 0.5f;
     c.sinW = __builtin_amdgcn_sqrtf(fmaxf(0.0f, 1.0f - c.cosW * c.cosW)) + 1e-6f;
+    c.chord = __builtin_amdgcn_sqrtf(2.0f * (1.0f - c.cosW)) + 1e-6f;
     return c;
 }
 // May some ray of the wave cone reach the triangle cone [c0.xyz, c0.w; c1.w]?
@@ -605,14 +606,12 @@ __device__ __forceinline__ bool cone_overlap(const WaveCone& wc, const float4 c0
 }
 
 // May some ray of the wave cone pass on the inner side (up to the margin
-// in e.w) of one edge plane [e.xyz, e.w]?  max over the cone of d . n is
-// 1 if the cone contains n, else cos(angle(w, n) - W).
+// in e.w) of one edge plane [e.xyz, e.w]?  For every d in the cone
+// d . n <= w . n + |d - w| <= w . n + chord(W) (+ ang for the widened cone).
 __device__ __forceinline__ bool edge_open(const WaveCone& wc, const float4 e, float ang)
 {
     const float c = dot(wc.w, make3(e.x, e.y, e.z));
-    const float sn = __builtin_amdgcn_sqrtf(fmaxf(0.0f, 1.0f - c * c)) + 1e-6f;
-    const float mx = c >= wc.cosW ? 1.0f : c * wc.cosW + sn * wc.sinW;
-    return !(mx + 2e-6f + ang < e.w);
+    return !(c + wc.chord + 2e-6f + ang < e.w);
 }
 __device__ __forceinline__ bool edges_open(const WaveCone& wc, const float4* e, float ang)
 {
