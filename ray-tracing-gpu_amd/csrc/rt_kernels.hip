@@ -1646,7 +1646,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MAXD == 0 ?
         Mat4 M;
 #pragma unroll
         for (int i = 0; i < 16; ++i) M.m[i >> 2][i & 3] = F.orient[i];
-        const Vec3 D = normalize(d0 * M);
+        // Vecteur3.h Normaliser (rt_math.h normalize) with the exact fast
+        // sqrt / reciprocal sequences (rt_fastmath.h) when the wave is in range
+        const Vec3 dm = d0 * M;
+        const float len = sqrt_w(dm.x * dm.x + dm.y * dm.y + dm.z * dm.z);
+        const Vec3 D = len > kEps ? dm * recip_w(len) : make3(0.f, 0.f, 0.f);
         const Vec3 O = make3(F.cam[0], F.cam[1], F.cam[2]);
         cnt.primary = valid ? 1u : 0u;
         c = radiance<MAXD, LB, PF, WAVE>(S, F, O, D, cnt, valid);
