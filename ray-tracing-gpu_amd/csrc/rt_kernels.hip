@@ -374,70 +374,6 @@ __device__ __forceinline__ int closest_hit(const SceneDev& S, const Vec3 O, cons
     return bi;
 }
 
-// ----------------------------------------------- scalar prefetch (s_load)
-// hipcc sinks a plain load of the next record below the culling branch, so
-// every iteration waits a full scalar-cache round trip.  These issue the
-// s_load in inline asm at the top of the iteration and retire it with an
-// s_waitcnt that also "redefines" the registers (so no use can be scheduled
-// before it).  Every path must reach rt_swait before the registers die, or a
-// late load could land in reallocated SGPRs.  hipcc's own SMEM waits are
-// always lgkmcnt(0) (SMEM returns out of order), so they stay correct.
-#ifndef RT_PF_CAMERA
-#define RT_PF_CAMERA 0
-#endif
-#ifndef RT_PF_SHADOW
-#define RT_PF_SHADOW 1
-#endif
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-typedef unsigned int u32x16 __attribute__((ext_vector_type(16)));
-__device__ __forceinline__ u32x4 rt_sload4(const void* p)
-{
-    u32x4 r;
-    asm volatile("s_load_dwordx4 %0, %1, 0x0" : "=s"(r) : "s"(p));
-    return r;
-}
-__device__ __forceinline__ u32x16 rt_sload16(const void* p)
-{
-    u32x16 r;
-    asm volatile("s_load_dwordx16 %0, %1, 0x0" : "=s"(r) : "s"(p));
-    return r;
-}
-typedef unsigned int u32x8 __attribute__((ext_vector_type(8)));
-__device__ __forceinline__ u32x8 rt_sload8(const void* p)
-{
-    u32x8 r;
-    asm volatile("s_load_dwordx8 %0, %1, 0x0" : "=s"(r) : "s"(p));
-    return r;
-}
-__device__ __forceinline__ void rt_swait(u32x8& a)
-{
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(a));
-}
-__device__ __forceinline__ float4 f4(const u32x8 v, int q)
-{
-    return make_float4(__uint_as_float(v[4 * q]), __uint_as_float(v[4 * q + 1]), __uint_as_float(v[4 * q + 2]),
-                       __uint_as_float(v[4 * q + 3]));
-}
-__device__ __forceinline__ void rt_swait(u32x4& a, u32x16& b)
-{
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(a), "+s"(b));
-}
-__device__ __forceinline__ float4 f4(const u32x4 v)
-{
-    return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
-}
-__device__ __forceinline__ float4 f4(const u32x16 v, int q)
-{
-    return make_float4(__uint_as_float(v[4 * q]), __uint_as_float(v[4 * q + 1]), __uint_as_float(v[4 * q + 2]),
-                       __uint_as_float(v[4 * q + 3]));
-}
-
-// Closest hit for camera rays (origin = the camera for every lane): the
-// per-triangle values that depend only on the origin come from tricam[].
-#ifndef RT_GROUP
-#define RT_GROUP 4
-#endif
-
 // One camera-ray triangle test: exact u first, the rest only if some lane of
 // the wave is inside the u bounds.
 __device__ __forceinline__ void camera_tri(const float4 a, const float4 b, const float4 c, const float4 d,
@@ -457,41 +393,20 @@ __device__ __forceinline__ void camera_tri(const float4 a, const float4 b, const
     take_min(okU & !((v < 0) | (u + v > 1)), t, __float_as_int(d.y), bt, bi);
 }
 
-// Closest hit for camera rays (origin = the camera for every lane): the
-// per-triangle values that depend only on the origin come from tricam[].
-// Records are fetched RT_GROUP at a time so the scalar loads of a group are
-// all in flight before its first test.
+// Closest hit for camera rays (origin = the camera for every lane), per-lane
+// culling (partial waves): the per-triangle values that depend only on the
+// origin come from tricam[].
 __device__ __forceinline__ int closest_hit_camera(const SceneDev& S, const Vec3 O, const Vec3 D, float& best_t,
                                                   Counters& cnt)
 {
     float bt = -1.0f;
     int bi = -1;
-#if RT_PF_CAMERA
-    if (S.n_tri > 0) {
-        // record k+1 (cone + camera record) is in flight while k is tested
-        u32x4 cone = rt_sload4(S.cone_cam);
-        u32x16 rec = rt_sload16(S.tricam);
-        rt_swait(cone, rec);
-        for (int k = 0; k < S.n_tri; ++k) {
-            const int kn = k + 1 < S.n_tri ? k + 1 : k;
-            u32x4 cone_n = rt_sload4(S.cone_cam + 2 * kn);
-            u32x16 rec_n = rt_sload16(S.tricam + 4 * kn);
-            const float4 cc = f4(cone);
-            if (__any(dot(D, make3(cc.x, cc.y, cc.z)) >= cc.w))
-                camera_tri(f4(rec, 0), f4(rec, 1), f4(rec, 2), f4(rec, 3), D, bt, bi, cnt);
-            rt_swait(cone_n, rec_n);
-            cone = cone_n;
-            rec = rec_n;
-        }
-    }
-#else
     for (int k = 0; k < S.n_tri; ++k) {
         const float4 cc = S.cone_cam[2 * k];
         if (!__any(dot(D, make3(cc.x, cc.y, cc.z)) >= cc.w)) continue;
         const float4* r = S.tricam + 4 * k;
         camera_tri(r[0], r[1], r[2], r[3], D, bt, bi, cnt);
     }
-#endif
     for (int k = 0; k < S.n_plane; ++k) {
         const float4 a = S.plane[2 * k], b = S.plane[2 * k + 1];
         float t;
@@ -1086,10 +1001,9 @@ __device__ __forceinline__ Color shadow_filter(const SceneDev& S, int light, con
 // pass shares the record loads, the loop overhead and the light-independent
 // part of the triangle test (S = P - p0, Q = S x e1, e2 . Q — the same
 // values Triangle.cpp:143-158 computes for every light's ray from P).
-// LB (lights per pass) is a kernel template parameter: 3 wins on scenes whose
-// triangle list is small (C2: -2..5%), 1 on big lists, where the extra VGPRs
-// cost occupancy (C3: +5..16% for 2..4), tools/ab_variants.py.
-template <int kLightBatch, bool PF>
+// This is the per-lane-culled form (partial waves, bounce rays); full waves
+// of depth-0 kernels use shadow_opaque_wave.
+template <int kLightBatch>
 __device__ __forceinline__ void shadow_opaque_batch(const SceneDev& S, int l0, int nl, const Vec3 P,
                                                     const Vec3 (&L)[kLightBatch], const float (&dist)[kLightBatch],
                                                     bool (&occ)[kLightBatch], Counters& cnt)
@@ -1099,43 +1013,18 @@ __device__ __forceinline__ void shadow_opaque_batch(const SceneDev& S, int l0, i
     float slack[kLightBatch];
 #pragma unroll
     for (int j = 0; j < kLightBatch; ++j) slack[j] = dist[j] * 1e-6f;
-    // cone records of triangle k+1 (all lights of the batch) are in flight
-    // while triangle k is tested
-    u32x8 cn[kLightBatch];
-    if (PF && S.n_tri_opaque > 0) {
-#pragma unroll
-        for (int j = 0; j < kLightBatch; ++j) {
-            cn[j] = rt_sload8(cone + cstride * (j < nl ? j : 0));
-            rt_swait(cn[j]);
-        }
-    }
     for (int k = 0; k < S.n_tri_opaque; ++k) {
         bool live = false;
 #pragma unroll
         for (int j = 0; j < kLightBatch; ++j) live |= (j < nl) & !occ[j];
         if (!__any(live)) break;
-        const int kn = k + 1 < S.n_tri_opaque ? k + 1 : k;
-        u32x8 cnn[kLightBatch];
-        if constexpr (PF) {
-#pragma unroll
-            for (int j = 0; j < kLightBatch; ++j) cnn[j] = rt_sload8(cone + cstride * (j < nl ? j : 0) + 2 * kn);
-        } else {
-            (void)kn;
-        }
         bool reach[kLightBatch];
         bool any_reach = false;
 #pragma unroll
         for (int j = 0; j < kLightBatch; ++j) {
             reach[j] = false;
             if (j < nl) {
-                float4 c0, c1;
-                if constexpr (PF) {
-                    c0 = f4(cn[j], 0);
-                    c1 = f4(cn[j], 1);
-                } else {
-                    c0 = cone[cstride * j + 2 * k];
-                    c1 = cone[cstride * j + 2 * k + 1];
-                }
+                const float4 c0 = cone[cstride * j + 2 * k], c1 = cone[cstride * j + 2 * k + 1];
                 reach[j] = !occ[j] & light_reach(c0, c1, L[j], dist[j], slack[j]);
                 any_reach |= reach[j];
             }
@@ -1158,13 +1047,6 @@ __device__ __forceinline__ void shadow_opaque_batch(const SceneDev& S, int l0, i
                     const bool ok = !(fabsf(det) < kEps) & !((u < 0) | (u > 1)) & !((v < 0) | (u + v > 1));
                     occ[j] |= ok & (t > kEps) & (t < dist[j]);
                 }
-            }
-        }
-        if constexpr (PF) {
-#pragma unroll
-            for (int j = 0; j < kLightBatch; ++j) {
-                rt_swait(cnn[j]);
-                cn[j] = cnn[j];
             }
         }
     }
@@ -1383,7 +1265,7 @@ __device__ __forceinline__ void add_light(Color& res, const Mat& m, const float4
     }
 }
 
-template <int kLightBatch, bool PF, int WAVE>
+template <int kLightBatch, int WAVE>
 __device__ __forceinline__ Color shade_local(const SceneDev& S, const Mat& m, const Vec3 P, const Vec3 N,
                                              const Vec3 D, Counters& cnt, bool active = true)
 {
@@ -1443,7 +1325,7 @@ __device__ __forceinline__ Color shade_local(const SceneDev& S, const Mat& m, co
 #ifndef RT_ABLATE_SHADOW  // timing-only build: no shadow rays
         RT_MARK(cnt, 3);
         if (use_wave) shadow_opaque_wave<kLightBatch, WAVE == 2>(S, lb, nl, P, L, dist, occ, wc, dmax, cnt);
-        else shadow_opaque_batch<kLightBatch, PF>(S, lb, nl, P, L, dist, occ, cnt);
+        else shadow_opaque_batch<kLightBatch>(S, lb, nl, P, L, dist, occ, cnt);
 #endif
         RT_MARK(cnt, 4);
 #pragma unroll
@@ -1481,7 +1363,7 @@ struct Refr {
     float rior, energy;
 };
 
-template <int MAXD, int LB, bool PF, int WAVE>
+template <int MAXD, int LB, int WAVE>
 __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, Counters& cnt, bool live)
 {
     const Color bg{F.bg[0], F.bg[1], F.bg[2]};
@@ -1514,7 +1396,7 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
             m = load_mat(S, sidx);
         }
         const Vec3 P = O + t * D;
-        const Color c = shade_local<LB, PF, WAVE>(S, m, P, N, D, cnt, hit & live);
+        const Color c = shade_local<LB, WAVE>(S, m, P, N, D, cnt, hit & live);
         return hit ? c : bg;
     } else {
         Frame stk[MAXD];
@@ -1533,7 +1415,7 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
                     const Vec3 N = hit_normal(S, idx, O, D, t);
                     const Mat m = load_mat(S, idx);
                     const Vec3 P = O + t * D;
-                    const Color acc = shade_local<LB, PF, WAVE>(S, m, P, N, D, cnt);
+                    const Color acc = shade_local<LB, WAVE>(S, m, P, N, D, cnt);
                     // Scene.cpp:1779-1781 / :1790-1792 gates; bounces == sp
                     const float er = m.kr * energy;
                     const float et = m.kt * energy;
@@ -1620,7 +1502,7 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
 #endif
 // COUNT: also tally the exact tests executed (the RT_FLAG_STATS launch); in
 // the timed kernels the tallies are dead and compile away.
-template <int MAXD, int LB, bool PF, int WAVE, bool COUNT>
+template <int MAXD, int LB, int WAVE, bool COUNT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MAXD == 0 ? RT_WAVES_PER_EU : 1))) void rt_trace_kernel(const SceneDev S, const FrameDev F, unsigned* __restrict__ rgba,
                                                        float* __restrict__ rgbf, StatsDev* __restrict__ stats)
 {
@@ -1653,7 +1535,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MAXD == 0 ?
         const Vec3 D = len > kEps ? dm * recip_w(len) : make3(0.f, 0.f, 0.f);
         const Vec3 O = make3(F.cam[0], F.cam[1], F.cam[2]);
         cnt.primary = valid ? 1u : 0u;
-        c = radiance<MAXD, LB, PF, WAVE>(S, F, O, D, cnt, valid);
+        c = radiance<MAXD, LB, WAVE>(S, F, O, D, cnt, valid);
         if (valid) {
             const size_t o = (size_t)ly * F.width + px;
             if (rgbf) {
@@ -2113,10 +1995,10 @@ static int reachable_depth(const rt_ctx* c, const rt_frame* f)
 typedef void (*kernel_fn)(const SceneDev, const FrameDev, unsigned*, float*, StatsDev*);
 
 // Kernel variants (tools/ab_variants.py, MI355X).  Without bounces and with
-// triangles: wave-level culling, RT_WAVE_LB lights per shadow pass.  Without
-// triangles nothing is culled: small light batches as before.  Bounce
-// kernels: per-lane culling, one light per pass (LB 3 / prefetch each
-// regressed scene7 by 4%).
+// triangles: wave-level culling (two-level above kClusterMinTriangles),
+// RT_WAVE_LB lights per shadow pass (2: best of 1-3 on C2 and C3).  Without
+// triangles nothing is culled: light batches of 3.  Bounce kernels:
+// per-lane culling, one light per pass (LB 3 regressed scene7 by 4%).
 #ifndef RT_WAVE_LB
 #define RT_WAVE_LB 2
 #endif
@@ -2127,22 +2009,22 @@ static kernel_fn pick_kernel(int depth, int n_tri, int n_lights, int& cap, int& 
     if (depth == 0 && n_tri > kClusterMinTriangles) {
         cap = 0;
         lb = RT_WAVE_LB;
-        return (kernel_fn)&rt_trace_kernel<0, RT_WAVE_LB, false, 2, COUNT>;
+        return (kernel_fn)&rt_trace_kernel<0, RT_WAVE_LB, 2, COUNT>;
     }
     if (depth == 0 && n_tri > 0) {
         cap = 0;
         lb = RT_WAVE_LB;
-        return (kernel_fn)&rt_trace_kernel<0, RT_WAVE_LB, false, 1, COUNT>;
+        return (kernel_fn)&rt_trace_kernel<0, RT_WAVE_LB, 1, COUNT>;
     }
     if (depth == 0 && n_lights > 1) {
         cap = 0;
         lb = 3;
-        return (kernel_fn)&rt_trace_kernel<0, 3, false, 0, COUNT>;
+        return (kernel_fn)&rt_trace_kernel<0, 3, 0, COUNT>;
     }
 #define RT_PICK(N)                                                        \
     if (depth <= N) {                                                     \
         cap = N;                                                          \
-        return (kernel_fn)&rt_trace_kernel<N, 1, false, 0, COUNT>;        \
+        return (kernel_fn)&rt_trace_kernel<N, 1, 0, COUNT>;        \
     }
     RT_STACK_DEPTHS(RT_PICK)
 #undef RT_PICK
