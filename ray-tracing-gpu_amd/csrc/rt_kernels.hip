@@ -1579,6 +1579,45 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MAXD == 0 ?
 // covers the bounce depth the scene can actually reach.
 #define RT_STACK_DEPTHS(X) X(0) X(1) X(2) X(3) X(4) X(5) X(8) X(12) X(16) X(20) X(32)
 
+// Self-test of the wave primitives the culling relies on (rt_debug_selftest):
+// wave_min / wave_max / wave_sum_u64 against plain loops over the same lane
+// values, and wave_cone's cos W as a lower bound of every live lane's cosine.
+__global__ void rt_selftest_kernel(unsigned seed, unsigned* __restrict__ fails)
+{
+    const int lane = (int)(threadIdx.x & 63);
+    __shared__ float vals[256];
+    __shared__ unsigned long long uv[256];
+    unsigned h = (seed * 0x9E3779B9u) ^ (blockIdx.x * 0x85EBCA6Bu) ^ (threadIdx.x * 0xC2B2AE35u);
+    h ^= h >> 16;
+    h *= 0x7FEB352Du;
+    h ^= h >> 15;
+    const float x = (float)(h & 0xFFFFFF) / 16777216.0f * 2.0f - 1.0f;
+    const unsigned long long u = (unsigned long long)(h >> 8) * 977ull;
+    vals[threadIdx.x] = x;
+    uv[threadIdx.x] = u;
+    __syncthreads();
+    const float mn = wave_min(x), mx = wave_max(x);
+    const unsigned long long su = wave_sum_u64(u);
+    const int base = (int)(threadIdx.x & ~63u);
+    float rmn = vals[base], rmx = vals[base];
+    unsigned long long rsu = 0;
+    for (int i = 0; i < 64; ++i) {
+        rmn = fminf(rmn, vals[base + i]);
+        rmx = fmaxf(rmx, vals[base + i]);
+        rsu += uv[base + i];
+    }
+    // a random cone of directions: every live lane's cosine to the axis >= cos W
+    const float th = 0.05f * (float)((h >> 4) & 255) / 255.0f;
+    const float ph = 6.2831853f * (float)((h >> 12) & 1023) / 1024.0f;
+    const Vec3 d = make3(sinf(th) * cosf(ph), sinf(th) * sinf(ph), cosf(th));
+    const bool live = ((h >> 20) & 3) != 0;
+    const WaveCone wc = wave_cone(d, live);
+    bool bad = (mn != rmn) | (mx != rmx) | (su != rsu);
+    if (wc.ok && live) bad |= dot(d, wc.w) < wc.cosW;
+    if (bad) atomicAdd(fails, 1u);
+    (void)lane;
+}
+
 }  // namespace rt
 
 // ===================================================================== host
@@ -2221,3 +2260,24 @@ extern "C" __attribute__((visibility("default"))) int rt_debug_prof_events(unsig
     return RT_OK;
 }
 #endif
+
+// Diagnostic (not in include/rt.h): run rt_selftest_kernel over `blocks`
+// workgroups; *failures = lanes whose wave reduction or wave cone was wrong.
+RT_EXPORT int rt_debug_selftest(int device, int blocks, unsigned* failures)
+{
+    if (!failures || blocks <= 0) return RT_E_ARG;
+    if (hipSetDevice(device) != hipSuccess) return RT_E_HIP;
+    unsigned* d = nullptr;
+    if (hipMalloc(&d, sizeof(unsigned)) != hipSuccess) return RT_E_HIP;
+    int rc = RT_OK;
+    if (hipMemset(d, 0, sizeof(unsigned)) != hipSuccess) rc = RT_E_HIP;
+    if (rc == RT_OK) {
+        hipLaunchKernelGGL(rt_selftest_kernel, dim3((unsigned)blocks), dim3(256), 0, 0, 12345u, d);
+        if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
+            hipMemcpy(failures, d, sizeof(unsigned), hipMemcpyDeviceToHost) != hipSuccess)
+            rc = RT_E_HIP;
+    }
+    hipFree(d);
+    return rc;
+}
+

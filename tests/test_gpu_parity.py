@@ -176,3 +176,17 @@ def test_bad_frame_rejected(ctx):
     f.row_end = 17
     with pytest.raises(rt_amd.RtError):
         ctx.render(f)
+
+
+def test_wave_primitives_selftest(ctx):
+    """The DPP wave reductions and the wave cone the culling relies on, checked
+    on the device against plain loops (rt_debug_selftest, 4,096 workgroups)."""
+    import ctypes
+
+    L = rt_amd.lib()
+    f = L.rt_debug_selftest
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_uint)]
+    fails = ctypes.c_uint(99)
+    assert f(0, 4096, ctypes.byref(fails)) == 0
+    assert fails.value == 0
