@@ -28,6 +28,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdlib>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -117,6 +119,18 @@ struct SceneDev {
     //    test (stop at the first hit, by kind), and only the translucent ones
     //    are multiplied, in file order.  0: the file-order product over all.
     int shadow_split;
+    // Light buffer (shadow cells): per light, a cube map of lb_R x lb_R cells
+    // per face around the light; cell c lists (64-byte entries, nearest to
+    // the light first) every opaque triangle whose light cone record can
+    // reach a ray whose direction falls in c (rt_lb_* kernels).
+    // lb_off[meta.off + c] .. [+ c + 1] index lb_ent; lb_dcap holds, per
+    // light, the triangles whose cull is not valid up to meta.dcov (sorted by
+    // that distance cap).  lb_R = 0: off.
+    int lb_R;
+    const unsigned* __restrict__ lb_off;
+    const float4* __restrict__ lb_ent;
+    const float4* __restrict__ lb_dcap;
+    const float4* __restrict__ lb_meta;  // per light: [off base, dcap base, n dcap, dcov] (ints as float bits)
 };
 
 struct FrameDev {
@@ -160,6 +174,9 @@ struct Counters {
 __device__ unsigned long long rt_prof_acc[8];
 #define RT_EV(cnt, i) (++(cnt).ev[i])
 __device__ unsigned long long rt_prof_ev[8];
+// per-tile record (16 x u32: total clocks lo/hi, 8 section clocks >> 8, events 1 2 4 5 6 7)
+__device__ unsigned* rt_prof_tiles;
+__device__ int rt_prof_ntiles;
 #else
 #define RT_EV(cnt, i) ((void)0)
 #define RT_MARK(cnt, i) \
@@ -854,6 +871,216 @@ __global__ void rt_cluster_sort(const float4* __restrict__ in, int nclu, float4*
     out[2 * rank + 1] = q1;
 }
 
+// ------------------------------------------------------------ light buffer
+// Haines & Greenberg's light buffer, made exact: a cube map around each
+// light.  The direction d from the light to a shading point (d = -L) picks
+// the face of its largest |component| and the cell (i, j) of u = a/|m|,
+// v = b/|m| on that face (lb_cell).  Every cell has a cone [w, W] (lb_cone,
+// in double) containing every float direction the lookup can map to it,
+// with the invariants of a wave cone (exact w . d >= cosW + 2e-6 for every
+// such d; sinW, chord raised).  So the wave-level predicates cone_overlap and
+// edges_open applied to a CELL are the proven wave-level culling with the
+// wave's rays replaced by the cell's: a triangle they reject cannot be
+// reported by the reference for any ray of the cell whose length is at most
+// the distance dcov the angular slack was sized for (lanes beyond it, or
+// with a degenerate direction, take the per-lane path).  Cell lists hold the
+// kept triangles nearest-first (the per-lane dmin exit); pairs whose cull
+// is not valid up to dcov (dcap < dcov, or never culled) are in a separate
+// per-light list sorted by dcap, tested by the lanes with dist > dcap — the
+// per-lane predicate light_reach, split in two.
+constexpr int kLbGroup = 16;  // cells per supercell edge (two-level build)
+
+__device__ __forceinline__ int lb_cell(const Vec3 d, int R)
+{
+    const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
+    int face;
+    float m, a, b;
+    if ((ax >= ay) & (ax >= az)) {
+        face = d.x >= 0.0f ? 0 : 1;
+        m = ax; a = d.y; b = d.z;
+    } else if (ay >= az) {
+        face = d.y >= 0.0f ? 2 : 3;
+        m = ay; a = d.z; b = d.x;
+    } else {
+        face = d.z >= 0.0f ? 4 : 5;
+        m = az; a = d.x; b = d.y;
+    }
+    const float inv = __builtin_amdgcn_rcpf(m);  // ~1 ulp: the cells' 1e-5 margins cover it
+    const float h = 0.5f * (float)R;
+    int i = (int)floorf((a * inv + 1.0f) * h);
+    int j = (int)floorf((b * inv + 1.0f) * h);
+    i = min(max(i, 0), R - 1);
+    j = min(max(j, 0), R - 1);
+    return (face * R + j) * R + i;
+}
+
+__device__ __forceinline__ void lb_face_dir(int face, double u, double v, double* o)
+{
+    switch (face) {
+    case 0: o[0] = 1.0; o[1] = u; o[2] = v; break;
+    case 1: o[0] = -1.0; o[1] = u; o[2] = v; break;
+    case 2: o[0] = v; o[1] = 1.0; o[2] = u; break;
+    case 3: o[0] = v; o[1] = -1.0; o[2] = u; break;
+    case 4: o[0] = u; o[1] = v; o[2] = 1.0; break;
+    default: o[0] = u; o[1] = v; o[2] = -1.0; break;
+    }
+    const double n = sqrt(o[0] * o[0] + o[1] * o[1] + o[2] * o[2]);
+    o[0] /= n; o[1] /= n; o[2] /= n;
+}
+
+// Cone of the cells [i0, i1) x [j0, j1) of a face (u range widened by 1e-5
+// for the lookup's rounding), its half-angle grown by `widen` (supercells).
+// The farthest point of a small geodesically convex cell from its centre
+// direction is a corner.  Float |d| = 1 within 1e-6 (sqrt_w/recip_w), float
+// w within 1.2e-7 of the unit centre: cosW = cos(W)(1 - 2e-6) - 4e-6 keeps
+// exact w.d >= cosW + 2e-6 for every direction of the cells.
+__device__ WaveCone lb_cone(int face, int i0, int i1, int j0, int j1, int R, double widen)
+{
+    const double du = 1e-5;
+    const double u0 = 2.0 * i0 / R - 1.0 - du, u1 = 2.0 * i1 / R - 1.0 + du;
+    const double v0 = 2.0 * j0 / R - 1.0 - du, v1 = 2.0 * j1 / R - 1.0 + du;
+    double w[3];
+    lb_face_dir(face, 0.5 * (u0 + u1), 0.5 * (v0 + v1), w);
+    double W = 0.0;
+    for (int q = 0; q < 4; ++q) {
+        double c[3];
+        lb_face_dir(face, (q & 1) ? u1 : u0, (q & 2) ? v1 : v0, c);
+        const double x = w[1] * c[2] - w[2] * c[1], y = w[2] * c[0] - w[0] * c[2], z = w[0] * c[1] - w[1] * c[0];
+        W = fmax(W, atan2(sqrt(x * x + y * y + z * z), w[0] * c[0] + w[1] * c[1] + w[2] * c[2]));
+    }
+    W = W * (1.0 + 1e-9) + 1e-6 + widen;
+    WaveCone k;
+    k.w = make3((float)w[0], (float)w[1], (float)w[2]);
+    const double cw = cos(W) * (1.0 - 2e-6) - 4e-6;
+    float cf = (float)cw;
+    if ((double)cf > cw) cf = nextafterf(cf, -INFINITY);
+    const double sw = sqrt(fmax(0.0, 1.0 - (double)cf * (double)cf)) + 1e-6;
+    float sf = (float)sw;
+    if ((double)sf < sw) sf = nextafterf(sf, INFINITY);
+    const double ch = sqrt(2.0 * (1.0 - (double)cf)) + 1e-6;
+    float chf = (float)ch;
+    if ((double)chf < ch) chf = nextafterf(chf, INFINITY);
+    k.cosW = cf;
+    k.sinW = sf;
+    k.chord = chf;
+    k.ok = W < 1.0;  // cosW >= 0.54 like every wave cone (>= 0.5)
+    return k;
+}
+
+// May a ray of cone wc (up to length dcov) need light record k?  The shadow
+// wave batch's predicate with dmax = dcov, minus its dcap term (the dcap
+// list), with the edge planes always.  Never-culled pairs: the dcap list.
+__device__ __forceinline__ bool lb_keep(const WaveCone& wc, const float4 c0, const float4 c1, const float4* e,
+                                        float dcov)
+{
+    if (!(c0.w > 0.0f) || !(c1.x < dcov)) return false;
+    if (!wc.ok) return true;
+    const float ang = dcov * 1e-6f * c1.y;
+    return cone_overlap(wc, c0, c1.w, ang) && edges_open(wc, e, ang);
+}
+
+// Build pass 1: per supercell (16 x 16 cells, cone widened by 1e-3 rad so
+// that rejecting a triangle for it implies rejecting it for each of its
+// cells), the triangles of `perm` (nearest-first) it keeps, in order
+// (block-ordered compaction).  lists == nullptr: counts only.
+__global__ __launch_bounds__(256) void rt_lb_super(const float4* __restrict__ cone, int n, const int* __restrict__ perm,
+                                                   int np, int R, float dcov, const unsigned* __restrict__ offs,
+                                                   unsigned* __restrict__ counts, int* __restrict__ lists)
+{
+    const int G = R / kLbGroup;
+    const int s = blockIdx.x;
+    const int face = s / (G * G), rem = s % (G * G), sj = rem / G, si = rem % G;
+    const WaveCone wc = lb_cone(face, si * kLbGroup, si * kLbGroup + kLbGroup, sj * kLbGroup, sj * kLbGroup + kLbGroup,
+                                R, 1e-3);
+    __shared__ unsigned wtot[4];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    unsigned total = 0;
+    const unsigned base = lists ? offs[s] : 0u;
+    for (int q0 = 0; q0 < np; q0 += 256) {
+        const int q = q0 + (int)threadIdx.x;
+        int k = -1;
+        bool keep = false;
+        if (q < np) {
+            k = perm[q];
+            keep = lb_keep(wc, cone[2 * k], cone[2 * k + 1], cone + 2 * (size_t)n + 3 * (size_t)k, dcov);
+        }
+        const unsigned long long b = __ballot(keep);
+        const unsigned pre = (unsigned)__popcll(b & ((1ull << lane) - 1ull));
+        if (lane == 0) wtot[wv] = (unsigned)__popcll(b);
+        __syncthreads();
+        unsigned off = 0;
+        for (int w = 0; w < wv; ++w) off += wtot[w];
+        const unsigned blk = wtot[0] + wtot[1] + wtot[2] + wtot[3];
+        if (lists && keep) lists[base + total + off + pre] = k;
+        total += blk;
+        __syncthreads();
+    }
+    if (!lists && threadIdx.x == 0) counts[s] = total;
+}
+
+// 64-byte light-buffer entry of triangle k (tri[] record + light record):
+//   [p0, key] [e1, e2.x] [e2.y e2.z, 2/dmin, 0] [c0 = dir to centre, cosT]
+// key = dmin (cell lists) or dcap (dcap list).
+__device__ __forceinline__ void lb_write(float4* o, const float4* __restrict__ tri, int k, const float4 c0,
+                                         const float4 c1, float key)
+{
+    const float4 a = tri[3 * k], b = tri[3 * k + 1], c = tri[3 * k + 2];
+    o[0] = make_float4(a.x, a.y, a.z, key);
+    o[1] = make_float4(a.w, b.x, b.y, b.z);
+    o[2] = make_float4(b.w, c.x, c1.y, 0.0f);
+    o[3] = c0;
+}
+
+// Build pass 2: one thread per cell of a supercell, over the supercell's
+// list (staged in LDS), in order.  ent == nullptr: counts only.
+__global__ __launch_bounds__(256) void rt_lb_cells(const float4* __restrict__ cone, int n, const float4* __restrict__ tri,
+                                                   int R, float dcov, const unsigned* __restrict__ soffs,
+                                                   const int* __restrict__ slists, const unsigned* __restrict__ coffs,
+                                                   unsigned* __restrict__ ccounts, float4* __restrict__ ent)
+{
+    const int G = R / kLbGroup;
+    const int s = blockIdx.x;
+    const int face = s / (G * G), rem = s % (G * G), sj = rem / G, si = rem % G;
+    const int i = si * kLbGroup + (int)(threadIdx.x & 15), j = sj * kLbGroup + (int)(threadIdx.x >> 4);
+    const int cell = (face * R + j) * R + i;
+    const WaveCone wc = lb_cone(face, i, i + 1, j, j + 1, R, 0.0);
+    __shared__ float4 rec[256 * kConeRec];
+    __shared__ int kid[256];
+    const unsigned b0 = soffs[s], b1 = soffs[s + 1];
+    unsigned cnt = 0, out = ent ? coffs[cell] : 0u;
+    for (unsigned q0 = b0; q0 < b1; q0 += 256) {
+        __syncthreads();
+        const unsigned q = q0 + threadIdx.x;
+        if (q < b1) {
+            const int k = slists[q];
+            kid[threadIdx.x] = k;
+            rec[kConeRec * threadIdx.x] = cone[2 * k];
+            rec[kConeRec * threadIdx.x + 1] = cone[2 * k + 1];
+            for (int e = 0; e < 3; ++e) rec[kConeRec * threadIdx.x + 2 + e] = cone[2 * (size_t)n + 3 * (size_t)k + e];
+        }
+        __syncthreads();
+        const int m = (int)min(256u, b1 - q0);
+        for (int x = 0; x < m; ++x) {
+            const float4 c0 = rec[kConeRec * x], c1 = rec[kConeRec * x + 1];
+            if (!lb_keep(wc, c0, c1, rec + kConeRec * x + 2, dcov)) continue;
+            if (ent) lb_write(ent + 4 * (size_t)out++, tri, kid[x], c0, c1, c1.x);
+            else ++cnt;
+        }
+    }
+    if (!ent) ccounts[cell] = cnt;
+}
+
+// The dcap list of one light: entries of perm (sorted by dcap), key = dcap.
+__global__ void rt_lb_dcap(const float4* __restrict__ cone, const float4* __restrict__ tri, const int* __restrict__ perm,
+                           int m, float4* __restrict__ out)
+{
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= m) return;
+    const int k = perm[q];
+    const float4 c0 = cone[2 * k], c1 = cone[2 * k + 1];
+    lb_write(out + 4 * (size_t)q, tri, k, c0, c1, c1.z == c1.z ? c1.z : -INFINITY);
+}
+
 // Shadow-ray cull predicate (L normalised towards the light, dist to it):
 // the segment reaches the sphere's distance and the cone, or the lane lies
 // beyond the distance the culling argument covers (c1.z).
@@ -1234,6 +1461,115 @@ __device__ __forceinline__ void shadow_opaque_wave(const SceneDev& S, int l0, in
     }
 }
 
+// One light's shadow rays against the OPAQUE surfaces with the light buffer
+// (shadow_split scenes).  occ: in = lanes without a shadow ray, out = also
+// the occluded ones (any-hit, so the order of the tests is free).  Each lane
+// walks its own cell's list (nearest first, leaving at the first entry that
+// lies beyond its point) with the per-lane cone test in front of the exact
+// test, then the dcap list while its dist exceeds the entries' caps; lanes
+// the buffer does not cover take the per-lane loop over every triangle.
+__device__ __forceinline__ void shadow_opaque_lb(const SceneDev& S, int l, const Vec3 P, const Vec3 L, float dist,
+                                                 bool& occ, Counters& cnt)
+{
+    for (int k = 0; k < S.n_plane_opaque; ++k) {
+        if (!__any(!occ)) return;
+        ++cnt.pla;
+        occ |= shadow_plane_hit(S.plane[2 * k], P, L, dist);
+    }
+    const float4 m0 = S.lb_meta[2 * l], m1 = S.lb_meta[2 * l + 1];
+    const unsigned obase = __float_as_uint(m0.x), dbase = __float_as_uint(m0.y), ndcap = __float_as_uint(m0.z);
+    const int R = __float_as_int(m0.w);
+    const float dcov = m1.x;
+    const Vec3 d = -L;
+    const float mx = fmaxf(fabsf(d.x), fmaxf(fabsf(d.y), fabsf(d.z)));
+    const bool use = !occ & (dist <= dcov) & (mx >= 0.5f) & (R > 0);
+    unsigned e = 0, end = 0;
+    if (use) {
+        const unsigned* o = S.lb_off + obase + lb_cell(d, R);
+        e = o[0];
+        end = o[1];
+    }
+    const float slack = dist * 1e-6f;
+    RT_MARK(cnt, 3);
+    for (;;) {
+        const bool act = (e < end) & !occ;
+        if (!__any(act)) break;
+        bool go = false;
+        float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0, r2 = r0;
+        if (act) {
+            const float4* r = S.lb_ent + 4 * (size_t)e;
+            r0 = r[0];
+            r1 = r[1];
+            r2 = r[2];
+            const float4 r3 = r[3];
+            if (!(r0.w < dist)) {
+                e = end;  // this and every later entry lie beyond P (dmin)
+            } else {
+                ++e;
+                go = -dot(L, make3(r3.x, r3.y, r3.z)) >= r3.w - slack * r2.z;
+            }
+        }
+        if (__any(go)) {
+            ++cnt.tri;
+            if (go) {
+                const Vec3 e1 = make3(r1.x, r1.y, r1.z), e2 = make3(r1.w, r2.x, r2.y);
+                const TriU u = tri_u(make3(r0.x, r0.y, r0.z), e1, e2, P, L);
+                float t;
+                const bool ok = tri_vt(u, e1, e2, L, t);
+                occ |= ok & (t > kEps) & (t < dist);
+            }
+        }
+    }
+    RT_MARK(cnt, 4);
+    // pairs not culled up to dcov: sorted by dcap, so once no live lane lies
+    // beyond an entry's cap none lies beyond a later one
+    for (unsigned q = 0; q < ndcap; ++q) {
+        const float4* r = S.lb_dcap + 4 * (size_t)(dbase + q);
+        const float4 r0 = r[0];
+        const bool need = use & !occ & (dist > r0.w);
+        if (!__any(need)) break;
+        ++cnt.tri;
+        const float4 r1 = r[1], r2 = r[2];
+        if (need) {
+            const Vec3 e1 = make3(r1.x, r1.y, r1.z), e2 = make3(r1.w, r2.x, r2.y);
+            const TriU u = tri_u(make3(r0.x, r0.y, r0.z), e1, e2, P, L);
+            float t;
+            const bool ok = tri_vt(u, e1, e2, L, t);
+            occ |= ok & (t > kEps) & (t < dist);
+        }
+    }
+    // lanes the buffer does not cover: every opaque triangle, culled per lane
+    if (__any(!occ & !use)) {
+        bool o2 = occ | use;
+        const float4* cone = S.cone_light + kConeRec * (size_t)S.n_tri * l;
+        for (int k = 0; k < S.n_tri_opaque; ++k) {
+            if (!__any(!o2)) break;
+            const float4 c0 = cone[2 * k], c1 = cone[2 * k + 1];
+            const bool reach = !o2 & light_reach(c0, c1, L, dist, slack);
+            if (!__any(reach)) continue;
+            const TriRec tr = load_tri(S, k);
+            ++cnt.tri;
+            const TriU r = tri_u(tr.p0, tr.e1, tr.e2, P, L);
+            if (!__any(r.ok && !o2)) continue;
+            float t;
+            const bool ok = tri_vt(r, tr.e1, tr.e2, L, t);
+            o2 |= ok & (t > kEps) & (t < dist);
+        }
+        occ = use ? occ : o2;
+    }
+    RT_MARK(cnt, 7);
+    for (int k = 0; k < S.n_quad_opaque; ++k) {
+        if (!__any(!occ)) break;
+        const float4* r = S.quad + 3 * k;
+        const float4 a = r[0], b = r[1], c = r[2];
+        float t;
+        ++cnt.qua;
+        const bool ok = hit_quadric(make_float4(0.f, a.x, a.y, a.z), make_float4(a.w, b.x, b.y, b.z),
+                                    make_float4(b.w, c.x, c.y, 0.f), P, L, t);
+        occ |= ok & (t > kEps) & (t < dist);
+    }
+}
+
 // Scene.cpp:1742-1777: ambient + every light (N.L gate on the unnormalised
 // light vector, filter, Lambert "Gouraud" term, Phong term).  Lights are
 // accumulated strictly in file order; only the filters of a batch of lights
@@ -1284,6 +1620,35 @@ __device__ __forceinline__ Color shade_local(const SceneDev& S, const Mat& m, co
         }
         return res;
     }
+    if constexpr ((WAVE & 4) != 0) {  // light buffer: one light at a time, file order
+        for (int li = 0; li < S.n_lights; ++li) {
+            const float4 l0 = S.lights[2 * li], l1 = S.lights[2 * li + 1];
+            const Vec3 Lr = make3(l0.x, l0.y, l0.z) - P;
+            const bool gate = active & (dot(Lr, N) > 0);  // Scene.cpp:1756, unnormalised
+            const float dist = sqrt_w(Lr.x * Lr.x + Lr.y * Lr.y + Lr.z * Lr.z);
+            const Vec3 L = Lr * recip_w(dist);
+            cnt.shadow += gate;
+            bool occ = !gate;
+            RT_MARK(cnt, 2);
+#ifndef RT_ABLATE_SHADOW
+            shadow_opaque_lb(S, li, P, L, dist, occ, cnt);
+#endif
+            RT_MARK(cnt, 7);
+            if (gate) {
+                Color F{0.0f, 0.0f, 0.0f};
+                if (!occ) {  // translucent surfaces, file order
+                    F = Color{1.0f, 1.0f, 1.0f};
+                    for (int q = 0; q < S.n_translucent; ++q) {
+                        Color fc;
+                        if (shadow_hit_record(S.geom + 4 * S.translucent[q], P, L, dist, fc, cnt)) F *= fc;
+                    }
+                }
+                add_light(res, m, l0, l1, N, L, D, F);
+            }
+            RT_MARK(cnt, 5);
+        }
+        return res;
+    }
     for (int lb = 0; lb < S.n_lights; lb += kLightBatch) {
         const int nl = S.n_lights - lb < kLightBatch ? S.n_lights - lb : kLightBatch;
         Vec3 L[kLightBatch];
@@ -1307,7 +1672,7 @@ __device__ __forceinline__ Color shade_local(const SceneDev& S, const Mat& m, co
             occ[j] = !gate[j];
         }
         RT_MARK(cnt, 2);
-        bool use_wave = WAVE > 0 && wave_full();
+        bool use_wave = (WAVE & 3) > 0 && wave_full();
         WaveCone wc[kLightBatch];
         float dmax[kLightBatch];
         if (use_wave) {
@@ -1324,7 +1689,7 @@ __device__ __forceinline__ Color shade_local(const SceneDev& S, const Mat& m, co
         }
 #ifndef RT_ABLATE_SHADOW  // timing-only build: no shadow rays
         RT_MARK(cnt, 3);
-        if (use_wave) shadow_opaque_wave<kLightBatch, WAVE == 2>(S, lb, nl, P, L, dist, occ, wc, dmax, cnt);
+        if (use_wave) shadow_opaque_wave<kLightBatch, (WAVE & 3) == 2>(S, lb, nl, P, L, dist, occ, wc, dmax, cnt);
         else shadow_opaque_batch<kLightBatch>(S, lb, nl, P, L, dist, occ, cnt);
 #endif
         RT_MARK(cnt, 4);
@@ -1373,7 +1738,7 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
 #endif
         float t;
         RT_MARK(cnt, 0);
-        const int idx = closest_hit_primary<WAVE>(S, O, D, t, cnt);
+        const int idx = closest_hit_primary<(WAVE & 3)>(S, O, D, t, cnt);
         RT_MARK(cnt, 1);
         // Lanes that miss (or lie outside the frame) stay in step through the
         // shading so the wave stays whole for wave-level shadow culling.
@@ -1408,7 +1773,7 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
         for (;;) {
             if (trace) {
                 float t;
-                const int idx = camera_ray ? closest_hit_primary<WAVE>(S, O, D, t, cnt) : closest_hit<false>(S, O, D, t, cnt);
+                const int idx = camera_ray ? closest_hit_primary<(WAVE & 3)>(S, O, D, t, cnt) : closest_hit<false>(S, O, D, t, cnt);
                 camera_ray = false;
                 ret = bg;
                 if (idx >= 0) {
@@ -1548,11 +1913,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MAXD == 0 ?
     }
 #ifdef RT_PROF
     RT_MARK(cnt, 6);
-    if ((threadIdx.x & 63) == 0)
+    if ((threadIdx.x & 63) == 0) {
+        unsigned long long tot = 0;
         for (int i = 0; i < 8; ++i) {
             atomicAdd(&rt_prof_acc[i], cnt.pt[i]);
             atomicAdd(&rt_prof_ev[i], (unsigned long long)cnt.ev[i]);
+            tot += cnt.pt[i];
         }
+        const int tile = (int)((blockIdx.y * 2 + (wave >> 1)) * (gridDim.x * 2) + blockIdx.x * 2 + (wave & 1));
+        if (rt_prof_tiles && tile < rt_prof_ntiles) {
+            unsigned* o = rt_prof_tiles + 16 * (size_t)tile;
+            o[0] = (unsigned)tot;
+            o[1] = (unsigned)(tot >> 32);
+            for (int i = 0; i < 8; ++i) o[2 + i] = (unsigned)(cnt.pt[i] >> 8);
+            const int evi[6] = {1, 2, 4, 5, 6, 7};  // cam member batches, cam exact, shadow member
+            for (int i = 0; i < 6; ++i) o[10 + i] = cnt.ev[evi[i]];  // batches, exact, by dcap, by cone
+        }
+    }
 #endif
     if (F.flags & RT_FLAG_STATS) {
         unsigned long long v[7] = {cnt.primary, cnt.bounce, cnt.shadow, cnt.skipped, cnt.tri, cnt.pla, cnt.qua};
@@ -1643,6 +2020,14 @@ struct rt_ctx {
     float4* d_clu_cam = nullptr;
     float4* d_clu_light = nullptr;
     int n_clu = 0;
+    // light buffer (shadow cells), rt_lb_build
+    unsigned* d_lb_off = nullptr;
+    float4* d_lb_ent = nullptr;
+    float4* d_lb_dcap = nullptr;
+    float4* d_lb_meta = nullptr;
+    bool lb_ready = false;
+    size_t lb_entries = 0;
+    double lb_build_ms = 0.0;
     float cam_key[3] = {0.f, 0.f, 0.f};
     bool cam_valid = false;
     StatsDev* d_stats = nullptr;
@@ -1717,6 +2102,10 @@ RT_EXPORT void rt_destroy(rt_ctx* c)
     hipFree(c->d_tricoef);
     hipFree(c->d_clu_cam);
     hipFree(c->d_clu_light);
+    hipFree(c->d_lb_off);
+    hipFree(c->d_lb_ent);
+    hipFree(c->d_lb_dcap);
+    hipFree(c->d_lb_meta);
     hipFree(c->d_stats);
     hipFree(c->d_scratch);
     if (c->ev0) hipEventDestroy(c->ev0);
@@ -1777,6 +2166,169 @@ static void cluster_order(std::vector<float>& tri, int n_opaque)
     std::vector<float> out(tri.size());
     for (size_t k = 0; k < n; ++k) std::memcpy(&out[12 * k], &tri[12 * ord[k]], 12 * sizeof(float));
     tri.swap(out);
+}
+
+// RT_AMD_LIGHTBUF (diagnostic/A-B switch): 0 = never build or use the light
+// buffer, 1 = use it for every depth-0 scene with triangles; unset = for
+// lists above kClusterMinTriangles.  RT_AMD_LB_SCALE scales the cell count.
+static int lb_mode()
+{
+    const char* v = getenv("RT_AMD_LIGHTBUF");
+    if (!v || !*v) return 2;
+    return atoi(v);
+}
+
+// Light buffer of every light (shadow_opaque_lb, lb_cone): resolution from
+// the median angular radius of the light's triangle cones (cell half-width
+// ~ that radius), nearest-first cell lists built on the device in two
+// levels (supercells of 16 x 16 cells, then cells), offsets by host scans.
+static int lb_build(rt_ctx* c, int ntr, int n_opaque, int nl, const std::vector<double>& dcov)
+{
+    const auto t0 = std::chrono::steady_clock::now();
+    const char* sc = getenv("RT_AMD_LB_SCALE");
+    const double scale = sc && *sc ? atof(sc) : 1.0;
+    struct Build {
+        int R = 16;
+        std::vector<int> dperm;
+        std::vector<unsigned> soff, ccount;
+        int* d_slists = nullptr;
+        unsigned* d_soff = nullptr;
+    };
+    std::vector<Build> B((size_t)nl);
+    std::vector<float4> h((size_t)ntr * 2);
+    int* d_perm = nullptr;
+    unsigned* d_cnt = nullptr;
+    int rc = RT_OK;
+    auto fail = [&](hipError_t e, const char* what) {
+        if (rc == RT_OK) rc = hip_fail(c, e, what);
+    };
+#define LB_TRY(call)                              \
+    do {                                          \
+        hipError_t e_ = (call);                   \
+        if (e_ != hipSuccess) { fail(e_, #call); goto done; } \
+    } while (0)
+    {
+        size_t total = 0, off_words = 0, dcap_total = 0;
+        LB_TRY(hipMalloc(&d_perm, std::max<size_t>(ntr, 1) * sizeof(int)));
+        for (int j = 0; j < nl; ++j) {
+            Build& b = B[j];
+            const float4* cone = c->d_cone_light + kConeRec * (size_t)ntr * j;
+            LB_TRY(hipMemcpy(h.data(), cone, h.size() * sizeof(float4), hipMemcpyDeviceToHost));
+            std::vector<double> T;
+            std::vector<int> perm;
+            for (int k = 0; k < n_opaque; ++k) {
+                const float4 c0 = h[2 * k], c1 = h[2 * k + 1];
+                if (c0.w > 0.0f) T.push_back(std::acos(std::min(1.0, (double)c0.w)));
+                if (c0.w > 0.0f && c1.x < (float)dcov[j]) perm.push_back(k);
+                if (!(c1.z >= (float)dcov[j])) b.dperm.push_back(k);
+            }
+            if (!T.empty()) {
+                std::nth_element(T.begin(), T.begin() + T.size() / 2, T.end());
+                const double med = std::max(T[T.size() / 2], 1e-4);
+                b.R = (int)std::lround(scale / (kLbGroup * med)) * kLbGroup;
+                b.R = std::min(1024, std::max(kLbGroup, b.R));
+            }
+            std::sort(perm.begin(), perm.end(), [&](int x, int y) {
+                return h[2 * x + 1].x < h[2 * y + 1].x || (h[2 * x + 1].x == h[2 * y + 1].x && x < y);
+            });
+            auto key = [&](int k) { const float z = h[2 * k + 1].z; return z == z ? z : -INFINITY; };
+            std::sort(b.dperm.begin(), b.dperm.end(),
+                      [&](int x, int y) { return key(x) < key(y) || (key(x) == key(y) && x < y); });
+            const int G = b.R / kLbGroup;
+            const unsigned nsup = 6u * G * G, ncell = 6u * b.R * b.R;
+            if (!perm.empty()) LB_TRY(hipMemcpy(d_perm, perm.data(), perm.size() * sizeof(int), hipMemcpyHostToDevice));
+            hipFree(d_cnt);
+            d_cnt = nullptr;
+            LB_TRY(hipMalloc(&d_cnt, std::max(nsup, ncell) * sizeof(unsigned)));
+            hipLaunchKernelGGL(rt_lb_super, dim3(nsup), dim3(256), 0, 0, cone, ntr, d_perm, (int)perm.size(), b.R,
+                               (float)dcov[j], nullptr, d_cnt, nullptr);
+            LB_TRY(hipGetLastError());
+            b.soff.assign(nsup + 1, 0u);
+            LB_TRY(hipMemcpy(b.soff.data() + 1, d_cnt, nsup * sizeof(unsigned), hipMemcpyDeviceToHost));
+            for (unsigned q = 0; q < nsup; ++q) b.soff[q + 1] += b.soff[q];
+            LB_TRY(hipMalloc(&b.d_soff, (nsup + 1) * sizeof(unsigned)));
+            LB_TRY(hipMemcpy(b.d_soff, b.soff.data(), (nsup + 1) * sizeof(unsigned), hipMemcpyHostToDevice));
+            LB_TRY(hipMalloc(&b.d_slists, std::max(b.soff[nsup], 1u) * sizeof(int)));
+            hipLaunchKernelGGL(rt_lb_super, dim3(nsup), dim3(256), 0, 0, cone, ntr, d_perm, (int)perm.size(), b.R,
+                               (float)dcov[j], b.d_soff, nullptr, b.d_slists);
+            LB_TRY(hipGetLastError());
+            hipLaunchKernelGGL(rt_lb_cells, dim3(nsup), dim3(256), 0, 0, cone, ntr, c->d_tri, b.R, (float)dcov[j],
+                               b.d_soff, b.d_slists, nullptr, d_cnt, nullptr);
+            LB_TRY(hipGetLastError());
+            b.ccount.resize(ncell);
+            LB_TRY(hipMemcpy(b.ccount.data(), d_cnt, ncell * sizeof(unsigned), hipMemcpyDeviceToHost));
+            for (unsigned q = 0; q < ncell; ++q) total += b.ccount[q];
+            off_words += ncell + 1;
+            dcap_total += b.dperm.size();
+        }
+        if (total >= 0xFFFFFFF0ull / 4) {  // entry indices are 32-bit
+            c->err = "light buffer too large";
+            goto done;
+        }
+        LB_TRY(hipMalloc(&c->d_lb_off, off_words * sizeof(unsigned)));
+        LB_TRY(hipMalloc(&c->d_lb_ent, std::max<size_t>(total, 1) * 4 * sizeof(float4)));
+        LB_TRY(hipMalloc(&c->d_lb_dcap, std::max<size_t>(dcap_total, 1) * 4 * sizeof(float4)));
+        LB_TRY(hipMalloc(&c->d_lb_meta, std::max(nl, 1) * 2 * sizeof(float4)));
+        std::vector<float4> meta((size_t)std::max(nl, 1) * 2);
+        size_t obase = 0, ebase = 0, dbase = 0;
+        for (int j = 0; j < nl; ++j) {
+            Build& b = B[j];
+            const float4* cone = c->d_cone_light + kConeRec * (size_t)ntr * j;
+            const unsigned G = b.R / kLbGroup, nsup = 6u * G * G, ncell = 6u * b.R * b.R;
+            std::vector<unsigned> off(ncell + 1);
+            size_t run = ebase;
+            for (unsigned q = 0; q < ncell; ++q) {
+                off[q] = (unsigned)run;
+                run += b.ccount[q];
+            }
+            off[ncell] = (unsigned)run;
+            LB_TRY(hipMemcpy(c->d_lb_off + obase, off.data(), off.size() * sizeof(unsigned), hipMemcpyHostToDevice));
+            hipLaunchKernelGGL(rt_lb_cells, dim3(nsup), dim3(256), 0, 0, cone, ntr, c->d_tri, b.R, (float)dcov[j],
+                               b.d_soff, b.d_slists, c->d_lb_off + obase, nullptr, c->d_lb_ent);
+            LB_TRY(hipGetLastError());
+            if (!b.dperm.empty()) {
+                LB_TRY(hipMemcpy(d_perm, b.dperm.data(), b.dperm.size() * sizeof(int), hipMemcpyHostToDevice));
+                hipLaunchKernelGGL(rt_lb_dcap, dim3((unsigned)((b.dperm.size() + 255) / 256)), dim3(256), 0, 0, cone,
+                                   c->d_tri, d_perm, (int)b.dperm.size(), c->d_lb_dcap + 4 * dbase);
+                LB_TRY(hipGetLastError());
+                LB_TRY(hipDeviceSynchronize());  // d_perm is reused by the next light
+            }
+            unsigned ob = (unsigned)obase, db = (unsigned)dbase, nd = (unsigned)b.dperm.size();
+            float4 m0, m1 = make_float4((float)dcov[j], 0.f, 0.f, 0.f);
+            std::memcpy(&m0.x, &ob, 4);
+            std::memcpy(&m0.y, &db, 4);
+            std::memcpy(&m0.z, &nd, 4);
+            std::memcpy(&m0.w, &b.R, 4);
+            meta[2 * j] = m0;
+            meta[2 * j + 1] = m1;
+            obase += ncell + 1;
+            ebase = run;
+            dbase += b.dperm.size();
+        }
+        LB_TRY(hipMemcpy(c->d_lb_meta, meta.data(), meta.size() * sizeof(float4), hipMemcpyHostToDevice));
+        LB_TRY(hipDeviceSynchronize());
+        c->lb_ready = true;
+        c->lb_entries = total;
+    }
+done:
+#undef LB_TRY
+    for (Build& b : B) {
+        hipFree(b.d_slists);
+        hipFree(b.d_soff);
+    }
+    hipFree(d_perm);
+    hipFree(d_cnt);
+    c->lb_build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (rc == RT_OK && !c->lb_ready) {  // too large: run without it
+        hipFree(c->d_lb_off);
+        hipFree(c->d_lb_ent);
+        hipFree(c->d_lb_dcap);
+        hipFree(c->d_lb_meta);
+        c->d_lb_off = nullptr;
+        c->d_lb_ent = c->d_lb_dcap = c->d_lb_meta = nullptr;
+        c->err.clear();
+    }
+    return rc;
 }
 
 RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
@@ -1891,6 +2443,14 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
     c->d_tricam = c->d_trisph = c->d_cone_cam = c->d_cone_light = c->d_trinrm = c->d_tricoef = nullptr;
     c->d_clu_cam = c->d_clu_light = nullptr;
     c->n_clu = 0;
+    hipFree(c->d_lb_off);
+    hipFree(c->d_lb_ent);
+    hipFree(c->d_lb_dcap);
+    hipFree(c->d_lb_meta);
+    c->d_lb_off = nullptr;
+    c->d_lb_ent = c->d_lb_dcap = c->d_lb_meta = nullptr;
+    c->lb_ready = false;
+    c->lb_entries = 0;
     c->cam_valid = false;
     c->d_geom = c->d_mat = c->d_lights = c->d_tri = c->d_plane = c->d_quad = nullptr;
     c->d_translucent = nullptr;
@@ -1964,6 +2524,7 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
     HIP_TRY(c, up((void**)&c->d_tricoef, coef.data(), coef.size() * sizeof(float)));
     HIP_TRY(c, hipMalloc((void**)&c->d_cone_cam, std::max<size_t>(ntr, 1) * kConeRec * sizeof(float4)));
     HIP_TRY(c, hipMalloc((void**)&c->d_cone_light, std::max<size_t>(ntr * nl, 1) * kConeRec * sizeof(float4)));
+    std::vector<double> lb_dcov((size_t)std::max(nl, 0), 0.0);
     for (int j = 0; j < nl && ntr > 0; ++j) {
         const float* l = s->lights + 7 * (size_t)j;
         // shadow rays are culled up to 4x the light's farthest triangle
@@ -1977,6 +2538,7 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
                            c->d_trinrm, c->d_tricoef, (int)ntr, l[0], l[1], l[2], 0, (float)(4.0 * far),
                            c->d_cone_light + kConeRec * ntr * j);
         HIP_TRY(c, hipGetLastError());
+        lb_dcov[j] = (double)(float)(4.0 * far);
     }
     if (ntr > (size_t)kClusterMinTriangles) {
         c->n_clu = (int)((ntr + 63) / 64);
@@ -1990,6 +2552,10 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
         }
     }
     HIP_TRY(c, hipDeviceSynchronize());
+    if (ntr > 0 && nl > 0 && n_tri_o > 0 && opaque && lb_mode() != 0) {
+        const int rc = lb_build(c, (int)ntr, n_tri_o, nl, lb_dcov);
+        if (rc) return rc;
+    }
     HIP_TRY(c, hipMalloc(&c->d_geom, geom.size() * sizeof(float)));
     HIP_TRY(c, hipMalloc(&c->d_mat, mat.size() * sizeof(float)));
     HIP_TRY(c, hipMalloc(&c->d_lights, lig.size() * sizeof(float)));
@@ -2042,9 +2608,14 @@ typedef void (*kernel_fn)(const SceneDev, const FrameDev, unsigned*, float*, Sta
 #define RT_WAVE_LB 2
 #endif
 template <bool COUNT>
-static kernel_fn pick_kernel(int depth, int n_tri, int n_lights, int& cap, int& lb)
+static kernel_fn pick_kernel(int depth, int n_tri, int n_lights, bool lbuf, int& cap, int& lb)
 {
     lb = 1;
+    if (depth == 0 && n_tri > 0 && lbuf) {  // light-buffer shadows, one light per pass
+        cap = 0;
+        if (n_tri > kClusterMinTriangles) return (kernel_fn)&rt_trace_kernel<0, 1, 6, COUNT>;
+        return (kernel_fn)&rt_trace_kernel<0, 1, 5, COUNT>;
+    }
     if (depth == 0 && n_tri > kClusterMinTriangles) {
         cap = 0;
         lb = RT_WAVE_LB;
@@ -2085,8 +2656,10 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
     }
     const int depth = reachable_depth(c, f);
     int cap = 0, lb = 1;
-    kernel_fn k = (f->flags & RT_FLAG_STATS) ? pick_kernel<true>(depth, c->n_tri, c->n_lights, cap, lb)
-                                              : pick_kernel<false>(depth, c->n_tri, c->n_lights, cap, lb);
+    const int mode = lb_mode();
+    const bool lbuf = c->lb_ready && (mode == 1 || (mode == 2 && c->n_tri > kClusterMinTriangles));
+    kernel_fn k = (f->flags & RT_FLAG_STATS) ? pick_kernel<true>(depth, c->n_tri, c->n_lights, lbuf, cap, lb)
+                                              : pick_kernel<false>(depth, c->n_tri, c->n_lights, lbuf, cap, lb);
     if (!k) {
         c->err = "reachable bounce depth " + std::to_string(depth) + " exceeds the compiled stack (32)";
         return RT_E_UNSUPPORTED;
@@ -2095,7 +2668,8 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
     SceneDev S{c->d_geom, c->d_mat, c->d_lights, c->d_tri, c->d_plane, c->d_quad, c->d_translucent, c->d_tricam,
                use_tricam, c->n_tri <= kEdgeMaxTriangles, c->d_cone_cam, c->d_cone_light, c->d_clu_cam,
                c->d_clu_light, c->n_clu, c->n_surf, c->n_lights, c->n_tri, c->n_plane, c->n_quad,
-               c->n_tri_opaque, c->n_plane_opaque, c->n_quad_opaque, c->n_translucent, c->shadow_split};
+               c->n_tri_opaque, c->n_plane_opaque, c->n_quad_opaque, c->n_translucent, c->shadow_split,
+               lbuf ? 1 : 0, c->d_lb_off, c->d_lb_ent, c->d_lb_dcap, c->d_lb_meta};
     FrameDev F;
     std::memcpy(F.cam, f->cam_pos, sizeof F.cam);
     std::memcpy(F.orient, f->orient, sizeof F.orient);
@@ -2248,6 +2822,14 @@ extern "C" __attribute__((visibility("default"))) int rt_debug_prof(unsigned lon
         return RT_E_HIP;
     unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(rt::rt_prof_acc), z, sizeof z) != hipSuccess) return RT_E_HIP;
+    return RT_OK;
+}
+// Per-tile records of the next renders (device buffer of 16 x u32 per 8x8
+// tile, tile = tile_row * (2 * grid.x) + tile_col); NULL turns it off.
+extern "C" __attribute__((visibility("default"))) int rt_debug_prof_tiles(unsigned* dev, int ntiles)
+{
+    if (hipMemcpyToSymbol(HIP_SYMBOL(rt::rt_prof_tiles), &dev, sizeof dev) != hipSuccess) return RT_E_HIP;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(rt::rt_prof_ntiles), &ntiles, sizeof ntiles) != hipSuccess) return RT_E_HIP;
     return RT_OK;
 }
 // Same for the wave-uniform event counts (summed over waves).
