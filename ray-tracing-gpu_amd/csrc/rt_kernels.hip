@@ -726,9 +726,11 @@ __global__ void rt_cone_prepass(const float4* __restrict__ tri, const float4* __
     const double dv = sqrt(vx * vx + vy * vy + vz * vz);
     const double r0 = s.w, L = nr.w, gS = cf.x, gL = cf.y, rho_cap = cf.z;
     const double h = fabs(nr.x * ((double)ax - p0.x) + nr.y * ((double)ay - p0.y) + nr.z * ((double)az - p0.z));
-    const double h_eff = 0.998 * h - 1e-6 * (dv + r0);  // float normal; shadow ray passes within 1e-3 h of A
+    // float normal (the additive term, and 1e-3 h); the shadow ray's line
+    // passes within 1e-6 dist of A, <= 1e-2 h while dist <= 1e4 h (the cap below)
+    const double h_eff = 0.989 * h - 1e-6 * (dv + r0);
     const double tau = 18.0 * 0x1p-24 * L;                // k <= 2
-    const double Rp = 1.001 * h + dv + r0 + 1e-6 * dv;
+    const double Rp = 1.011 * h + dv + r0 + 1e-6 * dv;
     // |S| bound and the G the margin must cover
     const double G = gS * ((camera ? 0.0 : (double)dtarget * 1.0001) + dv + r0) + gL;
     double m = 0.01 * r0;
@@ -736,10 +738,17 @@ __global__ void rt_cone_prepass(const float4* __restrict__ tri, const float4* __
     const double rc = r0 + m + 2e-5 * dv;  // cone radius
     float4 c0 = make_float4(0.f, 0.f, 0.f, -2.0f);
     float4 c1 = make_float4(-INFINITY, 0.f, -INFINITY, 2.0f);
+    bool never = false;
+    // m <= 10 r: wider cones cost more than the pairs they would cull
+    // (a wide member cone widens its cluster's cone and floods light-buffer
+    // cells; measured with m <= dv/2 for lights: C3 +7%, C5 +4%)
     if (rho_cap >= 0.0 && h_eff > 1.01 * G && m <= 10.0 * r0 && m > 2.0 * tau && dv - rc > m / 3.0 + 0.02 &&
         isfinite(dv) && isfinite(gS) && isfinite(gL)) {
         const double phi = 1.01 * (m + Rp) / (m - tau);
-        const double cosT = sqrt(1.0 - (rc / dv) * (rc / dv)) - 2e-5;
+        // cosine margin 2e-6 >= the per-lane test's rounding: float dot
+        // (3 x 2^-24), float unit c0 (1e-7), |L| - 1 (3 x 2^-24), float cosT
+        // (6e-8): 5.4e-7 in all
+        const double cosT = sqrt(1.0 - (rc / dv) * (rc / dv)) - 2e-6;
         const float4 cone = make_float4((float)(vx / dv), (float)(vy / dv), (float)(vz / dv), (float)cosT);
         const float sinT = (float)(sqrt(fmax(0.0, 1.0 - (double)cone.w * cone.w)) + 1e-7);
         if (camera) {
@@ -756,16 +765,42 @@ __global__ void rt_cone_prepass(const float4* __restrict__ tri, const float4* __
             const double rhoN = fmin(m / (3.0 * L), rho_cap);  // rho where well conditioned
             const double dcap2 =
                 rhoN > 0.0 ? ((dv - rc) * (1.0 - rhoN) - m / 3.0) / rhoN / 1.01 : INFINITY;
-            const double dcap = fmin(fmin(dcap1, dcap2), 1000.0 * h);
+            const double dcap = fmin(fmin(dcap1, dcap2), 1e4 * h);
             if (dcap > 0.0) {
                 c0 = cone;
                 c1 = make_float4((float)dmin, (float)(2.0 / dmin), (float)(dcap * (1.0 - 1e-6)), sinT);
             }
         }
     }
+    // Never reported: the reference rejects |det| < 0.01, so a hit needs
+    // a = |D . N^| >= amin = (0.01 - 7 eps L^2) / |N|, and then the line's
+    // crossing X with the plane lies within M = G/amin + tau of the triangle
+    // (the bound above, for every a >= amin).  The line passes within
+    // dl = 1e-6 |S| of the apex (exactly through it for camera rays), so
+    // |X - apex| <= (h + dl)/amin + dl: when that keeps X farther than
+    // r0 + M from the sphere centre, no ray from the apex (shadow rays up to
+    // the cap) can be reported — whatever its direction.  Such a pair gets a
+    // record no test passes (cosT 2, dmin +inf), also in place of a cone
+    // record whose cap falls short of dtarget.
+    const bool weak = !(c0.w > 0.0f) || (!camera && !(c1.z >= dtarget));
+    if (weak && rho_cap >= 0.0 && cf.w > 0.0f && isfinite(dv) && isfinite(gS) && isfinite(gL)) {
+        const double nn = cf.w;
+        const double amin = (0.0099999 - 7.07 * 0x1p-24 * L * L) / (nn * (1.0 + 1e-6));
+        if (amin > 0.0) {
+            const double smax = (camera ? 0.0 : (double)dtarget * 1.0001) + dv + r0;
+            const double M = 1.01 * ((gS * smax + gL) / amin + tau);
+            const double dl = camera ? 0.0 : 1e-6 * (double)dtarget * 1.0001;
+            const double hup = 1.01 * h + 1e-5 * (dv + r0);
+            if (dv - r0 - M - (hup + dl) / amin - dl > 1e-3 * dv + 0.01) {
+                never = true;
+                c0 = make_float4((float)(vx / dv), (float)(vy / dv), (float)(vz / dv), 2.0f);
+                c1 = make_float4(INFINITY, 0.f, camera ? 0.f : dtarget, 0.f);
+            }
+        }
+    }
     float4 ce[3];
     for (int e = 0; e < 3; ++e) ce[e] = make_float4(0.f, 0.f, 0.f, -4.0f);
-    if (c0.w > 0.0f) {  // a culled pair: add its edge planes
+    if (c0.w > 0.0f && !never) {  // a culled pair: add its edge planes
         const float4 b1 = tri[3 * k + 1], c2r = tri[3 * k + 2];
         const double V[3][3] = {{p0.x, p0.y, p0.z},
                                 {(double)p0.x + p0.w, (double)p0.y + b1.x, (double)p0.z + b1.y},
@@ -1494,6 +1529,7 @@ __device__ __forceinline__ void shadow_opaque_lb(const SceneDev& S, int l, const
     for (;;) {
         const bool act = (e < end) & !occ;
         if (!__any(act)) break;
+        RT_EV(cnt, 3);
         bool go = false;
         float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0, r2 = r0;
         if (act) {
@@ -1511,6 +1547,7 @@ __device__ __forceinline__ void shadow_opaque_lb(const SceneDev& S, int l, const
         }
         if (__any(go)) {
             ++cnt.tri;
+            RT_EV(cnt, 4);
             if (go) {
                 const Vec3 e1 = make3(r1.x, r1.y, r1.z), e2 = make3(r1.w, r2.x, r2.y);
                 const TriU u = tri_u(make3(r0.x, r0.y, r0.z), e1, e2, P, L);
@@ -1529,6 +1566,7 @@ __device__ __forceinline__ void shadow_opaque_lb(const SceneDev& S, int l, const
         const bool need = use & !occ & (dist > r0.w);
         if (!__any(need)) break;
         ++cnt.tri;
+        RT_EV(cnt, 5);
         const float4 r1 = r[1], r2 = r[2];
         if (need) {
             const Vec3 e1 = make3(r1.x, r1.y, r1.z), e2 = make3(r1.w, r2.x, r2.y);
@@ -1540,6 +1578,7 @@ __device__ __forceinline__ void shadow_opaque_lb(const SceneDev& S, int l, const
     }
     // lanes the buffer does not cover: every opaque triangle, culled per lane
     if (__any(!occ & !use)) {
+        RT_EV(cnt, 6);
         bool o2 = occ | use;
         const float4* cone = S.cone_light + kConeRec * (size_t)S.n_tri * l;
         for (int k = 0; k < S.n_tri_opaque; ++k) {
@@ -1549,6 +1588,7 @@ __device__ __forceinline__ void shadow_opaque_lb(const SceneDev& S, int l, const
             if (!__any(reach)) continue;
             const TriRec tr = load_tri(S, k);
             ++cnt.tri;
+            RT_EV(cnt, 7);
             const TriU r = tri_u(tr.p0, tr.e1, tr.e2, P, L);
             if (!__any(r.ok && !o2)) continue;
             float t;
@@ -2186,7 +2226,8 @@ static int lb_build(rt_ctx* c, int ntr, int n_opaque, int nl, const std::vector<
 {
     const auto t0 = std::chrono::steady_clock::now();
     const char* sc = getenv("RT_AMD_LB_SCALE");
-    const double scale = sc && *sc ? atof(sc) : 1.0;
+    // cells of ~1/4 the median cone radius: best of 0.5-6 on C3 and C5
+    const double scale = sc && *sc ? atof(sc) : 4.0;
     struct Build {
         int R = 16;
         std::vector<int> dperm;
@@ -2218,7 +2259,7 @@ static int lb_build(rt_ctx* c, int ntr, int n_opaque, int nl, const std::vector<
             std::vector<int> perm;
             for (int k = 0; k < n_opaque; ++k) {
                 const float4 c0 = h[2 * k], c1 = h[2 * k + 1];
-                if (c0.w > 0.0f) T.push_back(std::acos(std::min(1.0, (double)c0.w)));
+                if (c0.w > 0.0f && c0.w <= 1.0f) T.push_back(std::acos((double)c0.w));
                 if (c0.w > 0.0f && c1.x < (float)dcov[j]) perm.push_back(k);
                 if (!(c1.z >= (float)dcov[j])) b.dperm.push_back(k);
             }
@@ -2514,7 +2555,7 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
         coef[4 * k] = fine ? (float)(54.0 * kk * eps * L * L / nn * 1.01) : 0.f;
         coef[4 * k + 1] = fine ? (float)(21.0 * kk * eps * L * L * L / nn * 1.01) : 0.f;
         coef[4 * k + 2] = fine ? (float)(rho_cap * 1.01) : -1.0f;
-        coef[4 * k + 3] = 0.0f;
+        coef[4 * k + 3] = fine ? (float)nn : 0.0f;  // |N| = |e1 x e2| (never-hit bound)
     }
     sph.resize(std::max<size_t>(sph.size(), 4));
     nrm.resize(std::max<size_t>(nrm.size(), 4));
@@ -2842,6 +2883,30 @@ extern "C" __attribute__((visibility("default"))) int rt_debug_prof_events(unsig
     return RT_OK;
 }
 #endif
+
+// Diagnostic (not in include/rt.h): light-buffer summary of the uploaded
+// scene: out[0] = built (0/1), out[1] = entries, out[2] = build ms,
+// then per light (up to (n - 3) / 3): R, dcap-list length, dcov.
+RT_EXPORT int rt_debug_lb_info(rt_ctx* c, double* out, int n)
+{
+    if (!c || !out || n < 3) return RT_E_ARG;
+    out[0] = c->lb_ready ? 1.0 : 0.0;
+    out[1] = (double)c->lb_entries;
+    out[2] = c->lb_build_ms;
+    if (!c->lb_ready) return RT_OK;
+    std::vector<float4> meta((size_t)c->n_lights * 2);
+    HIP_TRY(c, hipMemcpy(meta.data(), c->d_lb_meta, meta.size() * sizeof(float4), hipMemcpyDeviceToHost));
+    for (int j = 0; j < c->n_lights && 3 + 3 * j + 2 < n; ++j) {
+        int R;
+        unsigned nd;
+        std::memcpy(&R, &meta[2 * j].w, 4);
+        std::memcpy(&nd, &meta[2 * j].z, 4);
+        out[3 + 3 * j] = R;
+        out[4 + 3 * j] = nd;
+        out[5 + 3 * j] = meta[2 * j + 1].x;
+    }
+    return RT_OK;
+}
 
 // Diagnostic (not in include/rt.h): run rt_selftest_kernel over `blocks`
 // workgroups; *failures = lanes whose wave reduction or wave cone was wrong.

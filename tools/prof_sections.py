@@ -24,6 +24,8 @@ sys.path.insert(0, REPO)
 # wave-level events (per wave): cluster batches, member batches, exact tests
 EVENTS = ["cam_cluster_batches", "cam_member_batches", "cam_exact", "shadow_cluster_ballots",
           "shadow_member_batches", "shadow_exact", "shadow_clusters_by_dcap_only", "shadow_clusters_by_cone"]
+# with the light buffer (shadow_opaque_lb), events 3-7 are its own
+EVENTS_LB = EVENTS[:3] + ["lb_walk_iters", "lb_walk_exact", "lb_dcap_iters", "lb_fallback_waves", "lb_fallback_exact"]
 NAMES = ["setup", "primary", "shade_setup", "shadow_cull", "shadow_exact_tri", "lambert_phong", "store", "shadow_planes"]
 
 
@@ -42,10 +44,14 @@ def main():
     L = rt_amd.lib()
     L.rt_debug_prof.argtypes = [ctypes.c_void_p]
     L.rt_debug_prof_events.argtypes = [ctypes.c_void_p]
+    L.rt_debug_lb_info.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
     name, W, H, depth = bench.CONFIGS[a.config]
     s = rt_amd.Scene(bench.scene_path(name), W, H, depth)
     ctx = rt_amd.Context(0)
     ctx.upload(s)
+    info = (ctypes.c_double * 30)()
+    L.rt_debug_lb_info(ctx._h, info, 30)
+    lbinfo = list(info)[: 3 + 3 * s.flat.n_lights] if info[0] else None
     ctx.render(s.frame)
     buf = (ctypes.c_ulonglong * 8)()
     ev = (ctypes.c_ulonglong * 8)()
@@ -56,11 +62,13 @@ def main():
     L.rt_debug_prof(buf)
     L.rt_debug_prof_events(ev)
     waves = ((W + 7) // 8) * ((H + 7) // 8) * a.frames
+    ev_names = EVENTS_LB if lbinfo and (a.config in ("c3", "c5") or os.environ.get("RT_AMD_LIGHTBUF") == "1") else EVENTS
     tot = sum(buf[:8]) or 1
     print(json.dumps({"config": a.config, "frames": a.frames,
                       "share": {n: round(buf[i] / tot, 4) for i, n in enumerate(NAMES)},
                       "wave_clocks_per_frame": {n: buf[i] // a.frames for i, n in enumerate(NAMES)},
-                      "events_per_wave": {n: round(ev[i] / waves, 2) for i, n in enumerate(EVENTS) if n}}))
+                      "events_per_wave": {n: round(ev[i] / waves, 2) for i, n in enumerate(ev_names) if n},
+                      "light_buffer": lbinfo}))
 
 
 if __name__ == "__main__":
