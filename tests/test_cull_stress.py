@@ -82,3 +82,49 @@ def test_gpu_matches_oracle_random_views(oracle, tmp_path, seed):
     bad = np.argwhere(~(got.view(np.uint32) == want.view(np.uint32)).all(-1))
     assert bits_equal(got, want), f"{len(bad)} pixels differ, first {bad[:5].tolist()}"
 
+
+
+# The light buffer (shadow cells, rt_kernels.hip shadow_opaque_lb) forced on
+# for every case above, whatever the list size (the driver's default only
+# builds it past 1,024 triangles), and at cell resolutions from coarse to
+# fine (RT_AMD_LB_SCALE: R from 16 up to the 1,024 cap), so cell borders,
+# face edges and the dcap list all meet the stress geometry.
+@pytest.fixture
+def lightbuf(monkeypatch):
+    def on(scale=None):
+        monkeypatch.setenv("RT_AMD_LIGHTBUF", "1")
+        if scale is not None:
+            monkeypatch.setenv("RT_AMD_LB_SCALE", str(scale))
+    return on
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,seed,w,h,depth", [c for c in CASES if c[4] == 0])
+def test_gpu_lightbuf_matches_reference(cull_golden, lightbuf, tmp_path, name, seed, w, h, depth):
+    import rt_amd
+
+    lightbuf()
+    ctx = rt_amd.Context(0)
+    s = rt_amd.Scene(_path(tmp_path, seed, depth), w, h, depth)
+    ctx.upload(s)
+    got = ctx.render_float(s.frame)
+    assert bits_equal(got, cull_golden[name])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scale", [0.25, 1.0, 4.0, 64.0])
+@pytest.mark.parametrize("seed", [100, 101, 104, 106, 107, 110, 111])
+def test_gpu_lightbuf_random_views(oracle, lightbuf, tmp_path, seed, scale):
+    import rt_amd
+
+    lightbuf(scale)
+    n_small = 1200 if seed >= 106 else 60
+    path = cull_scenes.write(str(tmp_path / f"lb{seed}.dat"), seed, 0.0, n_small)
+    w, h = 96, 72
+    ctx = rt_amd.Context(0)
+    s = rt_amd.Scene(path, w, h, 0)
+    ctx.upload(s)
+    got = ctx.render_float(s.frame)
+    want = oracle.render(path, w, h, 0)
+    bad = np.argwhere(~(got.view(np.uint32) == want.view(np.uint32)).all(-1))
+    assert bits_equal(got, want), f"{len(bad)} pixels differ, first {bad[:5].tolist()}"
