@@ -7,8 +7,9 @@ slabs meet in ONE gather over xGMI:
 
 * ``RootGather`` — the frame is assembled on rank 0 (the display / writer):
   rank 0 renders its slab straight into the frame buffer and receives every
-  other slab with grouped point-to-point RCCL sends/receives, so each peer
-  uses its own direct xGMI link to the root (RCCL has no ncclGather).  Frames
+  other slab in one ``dist.gather`` per frame (RCCL has no ncclGather;
+  torch's NCCL backend issues it as one group of point-to-point sends and
+  receives, so each peer uses its own direct xGMI link to the root).  Frames
   are double-buffered, so the gather of frame k runs on RCCL's stream while
   frame k+1 renders on the compute stream.
 * ``gather_frame`` — the all-gather form (every rank gets the frame).
@@ -75,6 +76,8 @@ class RootGather:
             self.frames = []
             self.slabs = [torch.zeros(shape_slab, dtype=dtype, device=device) for _ in range(depth)]
         self.pending: List[Optional[list]] = [None] * depth
+        # rank 0: the frame buffer's row slabs, in rank order (contiguous views)
+        self.views = [[f[r * self.rows:(r + 1) * self.rows] for r in range(self.world)] for f in self.frames]
 
     def target(self, k: int):
         """Buffer to render frame k's slab into (waits until it is free)."""
@@ -82,21 +85,15 @@ class RootGather:
         return self.slabs[k % self.depth]
 
     def submit(self, k: int):
+        """Post frame k's gather: ONE collective call per frame (RCCL runs it
+        as a group of point-to-point receives on rank 0 and one send per
+        peer, each over its own direct xGMI link), so the host cost per frame
+        does not grow with the number of ranks."""
         if self.world == 1:
             return
         d, b = self.dist, k % self.depth
-        ops = []
-        if self.rank == 0:
-            for r in range(1, self.world):
-                view = self.frames[b][r * self.rows:(r + 1) * self.rows]
-                ops.append(d.P2POp(d.irecv, view, r))
-        else:
-            ops.append(d.P2POp(d.isend, self.slabs[b], 0))
-        if d.get_backend() == "gloo":
-            works = [op.op(op.tensor, op.peer) for op in ops]
-        else:
-            works = d.batch_isend_irecv(ops)
-        self.pending[b] = works
+        views = self.views[b] if self.rank == 0 else None
+        self.pending[b] = [d.gather(self.slabs[b], gather_list=views, dst=0, async_op=True)]
 
     def wait(self, k: int):
         b = k % self.depth
