@@ -188,8 +188,23 @@ def main():
     path = scene_path(name)
     scene = rt_amd.Scene(path, W, H, depth)
     ctx = rt_amd.Context(local)
-    ctx.upload(scene)
+    torch.cuda.synchronize()
+    t_up = time.perf_counter()
+    ctx.upload(scene)  # device copy + cone/cluster prepasses + light-buffer build (synchronous)
+    upload_ms = (time.perf_counter() - t_up) * 1e3
+    lbinfo = None
+    L = rt_amd.lib()
+    if hasattr(L, "rt_debug_lb_info"):
+        L.rt_debug_lb_info.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        info = (ctypes.c_double * 64)()
+        if L.rt_debug_lb_info(ctx._h, info, 64) == 0 and info[0]:
+            nl = scene.flat.n_lights
+            lbinfo = {"entries": int(info[1]), "build_ms": round(info[2], 2),
+                      "cells_per_face_edge": [int(info[3 + 3 * j]) for j in range(min(nl, 20))],
+                      "uncullable_pairs": [int(info[4 + 3 * j]) for j in range(min(nl, 20))]}
     types = scene.arrays()[0]
+    # compulsory scene bytes: 64-byte surface + 48-byte material records, 32-byte lights
+    scene_bytes = int(types.shape[0]) * 112 + int(scene.flat.n_lights) * 32
 
     from rt_amd.dist import RootGather, slab_rows
 
@@ -269,11 +284,22 @@ def main():
         ms = elapsed * 1e3 / args.steps
         value = W * H * args.steps / elapsed / 1e6
         achieved = flops / (kernel_ms * 1e-3) / 1e12
-        traffic = None
-        tfile = os.path.join(REPO, "profiles", "traffic.json")
+        # Hardware counters of the same kernel on the same config, from the
+        # rocprofv3 --pmc passes committed under profiles/ (tools/pmc_summary.py):
+        # HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE) and VALU
+        # wave-instructions per launch; VALU busy = those x 2 cycles (wave64
+        # on a SIMD32) over 1,024 SIMDs x this run's kernel time at 2.4 GHz.
+        traffic, valu_busy, pmc_src = None, None, None
+        tfile = os.path.join(REPO, "profiles", "pmc.json")
         if os.path.exists(tfile):
             with open(tfile) as f:
-                traffic = json.load(f).get(f"{args.config}_n{world}")
+                rec = json.load(f).get(f"{args.config}_n{world}")
+            if rec:
+                traffic = rec.get("hbm_bytes_per_launch")
+                if rec.get("SQ_INSTS_VALU"):
+                    valu_busy = round(rec["SQ_INSTS_VALU"] * 2 / (1024 * kernel_ms * 1e-3 * 2.4e9), 3)
+                pmc_src = rec.get("source")
+        alg_bytes = 4 * W * (frame.row_end - frame.row_begin) + scene_bytes
         out = {
             "metric": "Mray/s and ms/frame at 1920x1080 depth=3, 1/2/4/8 MI355X vs host CPU",
             "value": round(value, 3),
@@ -293,7 +319,15 @@ def main():
             "total_rays_per_s_M": round((tot_primary + tot_bounce + tot_shadow) * args.steps / elapsed / 1e6, 3),
             "rays_per_frame": {"primary": int(tot_primary), "bounce": int(tot_bounce), "shadow": int(tot_shadow)},
             "kernel_ms": round(kernel_ms, 4),
+            "upload_ms": round(upload_ms, 2),
+            "light_buffer": lbinfo,
+            "hbm": {"algorithmic_bytes": int(alg_bytes), "measured_bytes": traffic,
+                    "measured_gbps": round(traffic / (kernel_ms * 1e-3) / 1e9, 1) if traffic else None,
+                    "frac_of_8TBps": round(traffic / (kernel_ms * 1e-3) / 8e12, 4) if traffic else None,
+                    "valu_busy": valu_busy, "source": pmc_src},
             "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
+                         "bound_note": "FP32 VALU-bound (no dense contraction, so no MFMA); peak = the MI355X "
+                                       "dense FP32 rate (157.3 TF, equal for vector and f32 MFMA)",
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
                          "frac_vs_nofma_issue_peak": round(achieved / PEAK_NOFMA_TOPS, 4),
                          "flops_per_launch": int(flops), "kernel": f"rt_trace_kernel<{st.stack_depth},{st.light_batch}>",

@@ -2593,7 +2593,8 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
         }
     }
     HIP_TRY(c, hipDeviceSynchronize());
-    if (ntr > 0 && nl > 0 && n_tri_o > 0 && opaque && lb_mode() != 0) {
+    const int lbm = lb_mode();  // built only where launch() will use it
+    if (ntr > 0 && nl > 0 && n_tri_o > 0 && opaque && (lbm == 1 || (lbm == 2 && ntr > (size_t)kClusterMinTriangles))) {
         const int rc = lb_build(c, (int)ntr, n_tri_o, nl, lb_dcov);
         if (rc) return rc;
     }

@@ -1,0 +1,32 @@
+"""Collect per-config PMC summaries (tools/pmc_summary.py output) into
+profiles/pmc.json, the file bench.py reads its measured HBM bytes and VALU
+instruction counts from.
+
+    python tools/pmc_collect.py profiles/r01/session2 c2 c3 c5 c4s9
+"""
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main(src, *configs):
+    out_path = os.path.join(REPO, "profiles", "pmc.json")
+    out = json.load(open(out_path)) if os.path.exists(out_path) else {}
+    for c in configs:
+        f = os.path.join(src, f"pmc_{c}_summary.json")
+        d = json.load(open(f))
+        out[f"{c}_n1"] = {"hbm_bytes_per_launch": d.get("hbm_bytes_per_launch"),
+                          "SQ_INSTS_VALU": d.get("SQ_INSTS_VALU"), "SQ_INSTS_SALU": d.get("SQ_INSTS_SALU"),
+                          "SQ_WAVES": d.get("SQ_WAVES"), "source": os.path.relpath(f, REPO)}
+    out["_note"] = ("Per timed rt_trace_kernel launch, from rocprofv3 --pmc passes (one counter group per run): "
+                    "hbm_bytes_per_launch = FETCH_SIZE*1024*2 + WRITE_SIZE*1024 (gfx950 x2 FETCH correction, "
+                    "MI355X_MICROARCH.md; an upper bound for this kernel's scalar reads), SQ_INSTS_VALU = VALU "
+                    "wave-instructions.")
+    json.dump(out, open(out_path, "w"), indent=1, sort_keys=True)
+    print(json.dumps(out, indent=1, sort_keys=True))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])
