@@ -46,7 +46,8 @@ for s in $STEPS; do
 
     prof) P=gpurun_out/prof_${CONFIG:-c2}
           run rocprof_${CONFIG:-c2} 400 rocprofv3 --kernel-trace --stats --output-format csv -d $P -o run -- python bench.py --steps ${PROF_STEPS:-200} --no-cpu-baseline --config ${CONFIG:-c2}
-          python tools/prof_summary.py $P/run_kernel_trace.csv > $P/summary.json ;;
+          python tools/prof_summary.py $P/run_kernel_trace.csv > $P/summary.json
+          grep '^{"metric"' gpurun_out/rocprof_${CONFIG:-c2}.log > $P/bench_under_rocprof.json ;;
   esac
 done
 exit 0
