@@ -168,6 +168,8 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--partition", default="auto", choices=["auto", "slabs", "bands"],
+                    help="N>1: row slabs, cyclic 16-row bands, or bands when slabs are >10%% imbalanced")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -206,13 +208,40 @@ def main():
     # compulsory scene bytes: 64-byte surface + 48-byte material records, 32-byte lights
     scene_bytes = int(types.shape[0]) * 112 + int(scene.flat.n_lights) * 32
 
-    from rt_amd.dist import RootGather, slab_rows
+    from rt_amd.dist import RootGather, band_layout, slab_rows
 
     r0, r1, rows = slab_rows(H, world, rank)   # equal slabs (padded when H % world != 0)
     frame = scene.frame.copy()
     frame.row_begin, frame.row_end = r0, r1
     stream = torch.cuda.current_stream().cuda_stream
-    gather = RootGather(dist, H, W, "cuda") if world > 1 else None
+    # Partition: contiguous row slabs, or cyclic 16-row bands
+    # when the slabs' render times differ by more than 10% (measured here on
+    # every rank before the run; the decision is the same on all ranks).
+    partition, imbalance = "slabs", None
+    if world > 1 and args.partition != "slabs":
+        tmp = torch.zeros((max(rows, 1), W, 4), dtype=torch.uint8, device="cuda")
+        for _ in range(2):
+            ctx.render_async(frame, tmp.data_ptr(), 0, stream)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(5):
+            ctx.render_async(frame, tmp.data_ptr(), 0, stream)
+        e1.record()
+        torch.cuda.synchronize()
+        t = e0.elapsed_time(e1) / 5
+        tmax = torch.tensor([t], dtype=torch.float64, device="cuda")
+        tsum = tmax.clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        dist.all_reduce(tsum)
+        imbalance = float(tmax.item()) / (float(tsum.item()) / world) - 1.0
+        if args.partition == "bands" or imbalance > 0.10:
+            partition = "bands"
+        del tmp
+    band = 16 if partition == "bands" else 0
+    if band:
+        frame.band_rows, frame.band_count, frame.band_index = band, world, rank
+        _, rows = band_layout(H, world, band)
+    gather = RootGather(dist, H, W, "cuda", band_rows=band) if world > 1 else None
     single = torch.zeros((rows, W, 4), dtype=torch.uint8, device="cuda")
 
     # one counted render (atomics) for the algorithmic work of this rank's slab
@@ -299,7 +328,7 @@ def main():
                 if rec.get("SQ_INSTS_VALU"):
                     valu_busy = round(rec["SQ_INSTS_VALU"] * 2 / (1024 * kernel_ms * 1e-3 * 2.4e9), 3)
                 pmc_src = rec.get("source")
-        alg_bytes = 4 * W * (frame.row_end - frame.row_begin) + scene_bytes
+        alg_bytes = 4 * W * rt_amd.frame_rows(frame) + scene_bytes
         out = {
             "metric": "Mray/s and ms/frame at 1920x1080 depth=3, 1/2/4/8 MI355X vs host CPU",
             "value": round(value, 3),
@@ -315,7 +344,9 @@ def main():
             "data": f"reference scene file {name}" if name != "heightfield" else "synthetic 50k-triangle heightfield (rt_amd.synth)",
             "config": {"workload": f"{name} {W}x{H} max_bounces={depth}", "width": W, "height": H,
                        "max_bounces": depth, "surfaces": int(types.shape[0]),
-                       "parallelism": f"row-slab x{world}" + (" + RCCL p2p gather to rank 0 (double-buffered)" if world > 1 else "")},
+                       "parallelism": (f"row-band16 x{world}" if band else f"row-slab x{world}") +
+                                      (" + RCCL gather to rank 0 (double-buffered)" if world > 1 else ""),
+                       "slab_imbalance": round(imbalance, 3) if imbalance is not None else None},
             "total_rays_per_s_M": round((tot_primary + tot_bounce + tot_shadow) * args.steps / elapsed / 1e6, 3),
             "rays_per_frame": {"primary": int(tot_primary), "bounce": int(tot_bounce), "shadow": int(tot_shadow)},
             "kernel_ms": round(kernel_ms, 4),

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 2
+#define RT_ABI_VERSION 3
 
 enum {
     RT_OK = 0,
@@ -85,6 +85,16 @@ typedef struct rt_frame {
     float min_energy;     /* m_EnergieMinRayon (0.01)                       */
     float scene_ior;      /* m_IndiceRefractionScene (1.0)                  */
     int32_t flags;        /* RT_FLAG_*                                      */
+    /* ABI 3, multi-GPU load balance: band_rows > 0 (a
+     * multiple of 16) renders cyclic row bands instead of the slab — global
+     * bands b = band_index, band_index + band_count, ... of band_rows rows
+     * each (band b = rows [b*band_rows, (b+1)*band_rows)), packed in that
+     * order into the output; rows >= height are skipped and row_begin /
+     * row_end are ignored.  The output then holds rt_band_rows(height,
+     * band_rows, band_count, band_index) rows.  band_rows = 0: the slab.   */
+    int32_t band_rows;
+    int32_t band_count;
+    int32_t band_index;
 } rt_frame;
 
 #define RT_FLAG_STATS 1   /* count rays / tests into rt_stats (small cost)  */
@@ -141,6 +151,8 @@ const char* rt_last_error(rt_ctx*);
 void rt_destroy(rt_ctx*);
 
 int rt_abi_version(void);
+/* Output rows of one rank's band set (see rt_frame.band_rows); -1 if invalid. */
+int32_t rt_band_rows(int32_t height, int32_t band_rows, int32_t band_count, int32_t band_index);
 
 #ifdef __cplusplus
 }

@@ -131,6 +131,10 @@ struct SceneDev {
     const float4* __restrict__ lb_ent;
     const float4* __restrict__ lb_dcap;
     const float4* __restrict__ lb_meta;  // per light: [off base, dcap base, n dcap, dcov] (ints as float bits)
+    // Small lists (no clusters): ONE cluster record over all triangles for
+    // the camera (uni[0..1]) and over the opaque ones for each light
+    // (uni[2 + 2l ..]); nullptr: none.
+    const float4* __restrict__ uni;
 };
 
 struct FrameDev {
@@ -142,6 +146,7 @@ struct FrameDev {
     int max_bounces;
     float min_energy, scene_ior;
     int flags;
+    int band_rows, band_count, band_index;  // band_rows > 0: cyclic row bands (rt.h)
 };
 
 struct StatsDev {
@@ -630,7 +635,14 @@ __device__ __forceinline__ int closest_hit_camera_wave(const SceneDev& S, const 
             }
         }
     } else {
-        for (int k0 = 0; k0 < S.n_tri; k0 += 64) camera_wave_batch(S, wc, k0, O, D, bt, bi, cnt);
+        // the union record of all triangles first (small lists): one wave test
+        bool any_tri = true;
+        if (S.uni) {
+            const float far = wave_max(bi >= 0 ? bt : INFINITY);
+            any_tri = cone_overlap(wc, S.uni[0], S.uni[1].w, 0.0f, 4e-6f) & !(far < S.uni[1].x);
+        }
+        if (any_tri)
+            for (int k0 = 0; k0 < S.n_tri; k0 += 64) camera_wave_batch(S, wc, k0, O, D, bt, bi, cnt);
     }
     for (int k = 0; k < S.n_quad; ++k) {
         const float4* r = S.quad + 3 * k;
@@ -844,11 +856,13 @@ __global__ void rt_cone_prepass(const float4* __restrict__ tri, const float4* __
 // a surviving member always has a surviving cluster.  A member that is
 // always tested (cosT <= 0), or T_c >= 80 degrees, makes the cluster always
 // tested.  For lights: dmin = min, 2/dmin = max, dcap = min over the members.
-__global__ void rt_cluster_prepass(const float4* __restrict__ cone, int n, int nclu, float4* __restrict__ out)
+// csize: members per cluster (64; or n for the union record of small lists).
+__global__ void rt_cluster_prepass(const float4* __restrict__ cone, int n, int nclu, float4* __restrict__ out,
+                                   int csize = 64)
 {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= nclu) return;
-    const int k0 = 64 * c, k1 = min(n, k0 + 64);
+    const int k0 = csize * c, k1 = min(n, k0 + csize);
     double ax = 0, ay = 0, az = 0, dmin = INFINITY, inv = 0.0, dcap = INFINITY;
     bool always = false;
     for (int k = k0; k < k1; ++k) {
@@ -1338,6 +1352,25 @@ __device__ __forceinline__ void shadow_opaque_batch(const SceneDev& S, int l0, i
     }
 }
 
+// May some gated lane's shadow ray need any triangle of the union record
+// u?  Each lane is taken as a wave of one live lane (the cone wave_cone
+// builds for it: w = d, cosW = d.d - 1e-6), so the test is the proven
+// cluster test of shadow_opaque_wave with dmax = the lane's dist.
+__device__ __forceinline__ bool union_reach(const float4* u, const Vec3 L, float dist, bool gate)
+{
+    const Vec3 d = -L;
+    WaveCone c;
+    c.w = d;
+    c.cosW = dot(d, d) - 1e-6f;
+    c.sinW = __builtin_amdgcn_sqrtf(fmaxf(0.0f, 1.0f - c.cosW * c.cosW)) + 1e-6f;
+    c.chord = __builtin_amdgcn_sqrtf(2.0f * (1.0f - c.cosW)) + 1e-6f;
+    const float dm = dist == dist ? dist : INFINITY;
+    const float4 q0 = u[0], q1 = u[1];
+    const bool reach = !(c.cosW >= 0.5f) | ((q1.x < dm) & cone_overlap(c, q0, q1.w, dm * 1e-6f * q1.y, 4e-6f)) |
+                       (dm > q1.z);
+    return __any(gate & reach);
+}
+
 // One batch of 64 opaque triangles [k0, k0 + 64) for the lights in the bit
 // set `lights`: one lane per triangle against each light's wave cone, then
 // exact any-hit tests on the survivors; the light-independent part of the
@@ -1410,7 +1443,7 @@ __device__ __forceinline__ void shadow_wave_batch(const SceneDev& S, const float
 // per-lane form).  Same any-hit results: a triangle no lane of the wave can
 // reach is skipped, the rest are tested exactly per lane.
 template <int kLightBatch, bool CLU>
-__device__ __forceinline__ void shadow_opaque_wave(const SceneDev& S, int l0, int nl, const Vec3 P,
+__device__ __forceinline__ void shadow_opaque_wave(const SceneDev& S, int l0, int nl, unsigned tmask, const Vec3 P,
                                                    const Vec3 (&L)[kLightBatch], const float (&dist)[kLightBatch],
                                                    bool (&occ)[kLightBatch], const WaveCone (&wc)[kLightBatch],
                                                    const float (&dmax)[kLightBatch], Counters& cnt)
@@ -1460,16 +1493,20 @@ __device__ __forceinline__ void shadow_opaque_wave(const SceneDev& S, int l0, in
             }
         }
     } else {
-        for (int k0 = 0; k0 < S.n_tri_opaque; k0 += 64) {
+        for (int k0 = 0; k0 < S.n_tri_opaque && tmask; k0 += 64) {
             bool live = false;
 #pragma unroll
-            for (int j = 0; j < kLightBatch; ++j) live |= (j < nl) & !occ[j];
+            for (int j = 0; j < kLightBatch; ++j) live |= (j < nl) & ((tmask >> j) & 1u) & !occ[j];
             if (!__any(live)) break;
-            shadow_wave_batch<kLightBatch>(S, cone, cstride, k0, (1u << nl) - 1u, P, L, dist, occ, wc, dmax, cnt);
+            shadow_wave_batch<kLightBatch>(S, cone, cstride, k0, tmask, P, L, dist, occ, wc, dmax, cnt);
         }
     }
     RT_MARK(cnt, 3);
+#ifndef RT_ABLATE_SHADOW_PLANE  // timing-only build: no plane shadow tests
     for (int k = 0; k < S.n_plane_opaque; ++k) {
+#else
+    for (int k = 0; k < 0; ++k) {
+#endif
         const float4 a = S.plane[2 * k];
 #pragma unroll
         for (int j = 0; j < kLightBatch; ++j) {
@@ -1511,6 +1548,7 @@ __device__ __forceinline__ void shadow_opaque_lb(const SceneDev& S, int l, const
         ++cnt.pla;
         occ |= shadow_plane_hit(S.plane[2 * k], P, L, dist);
     }
+    {
     const float4 m0 = S.lb_meta[2 * l], m1 = S.lb_meta[2 * l + 1];
     const unsigned obase = __float_as_uint(m0.x), dbase = __float_as_uint(m0.y), ndcap = __float_as_uint(m0.z);
     const int R = __float_as_int(m0.w);
@@ -1596,6 +1634,7 @@ __device__ __forceinline__ void shadow_opaque_lb(const SceneDev& S, int l, const
             o2 |= ok & (t > kEps) & (t < dist);
         }
         occ = use ? occ : o2;
+    }
     }
     RT_MARK(cnt, 7);
     for (int k = 0; k < S.n_quad_opaque; ++k) {
@@ -1715,12 +1754,21 @@ __device__ __forceinline__ Color shade_local(const SceneDev& S, const Mat& m, co
         bool use_wave = (WAVE & 3) > 0 && wave_full();
         WaveCone wc[kLightBatch];
         float dmax[kLightBatch];
+        unsigned tmask = (1u << nl) - 1u;  // lights whose triangles the wave must walk
+#ifdef RT_ABLATE_SHADOW_TRI  // timing-only build: no triangle shadow tests
+        tmask = 0;
+#endif
         if (use_wave) {
 #pragma unroll
             for (int j = 0; j < kLightBatch; ++j) {
                 wc[j].ok = false;
                 dmax[j] = 0.0f;
-                if (j < nl) {
+                if (j < nl && ((tmask >> j) & 1u)) {
+                    // no lane's ray can need any triangle: skip the wave cone too
+                    if ((WAVE & 3) == 1 && S.uni && !union_reach(S.uni + 2 * (1 + lb + j), L[j], dist[j], gate[j])) {
+                        tmask &= ~(1u << j);
+                        continue;
+                    }
                     wc[j] = wave_cone(-L[j], gate[j]);  // directions from the light
                     dmax[j] = wave_max(gate[j] ? (dist[j] == dist[j] ? dist[j] : INFINITY) : 0.0f);
                     use_wave &= wc[j].ok | !__any(gate[j]);
@@ -1729,7 +1777,7 @@ __device__ __forceinline__ Color shade_local(const SceneDev& S, const Mat& m, co
         }
 #ifndef RT_ABLATE_SHADOW  // timing-only build: no shadow rays
         RT_MARK(cnt, 3);
-        if (use_wave) shadow_opaque_wave<kLightBatch, (WAVE & 3) == 2>(S, lb, nl, P, L, dist, occ, wc, dmax, cnt);
+        if (use_wave) shadow_opaque_wave<kLightBatch, (WAVE & 3) == 2>(S, lb, nl, tmask, P, L, dist, occ, wc, dmax, cnt);
         else shadow_opaque_batch<kLightBatch>(S, lb, nl, P, L, dist, occ, cnt);
 #endif
         RT_MARK(cnt, 4);
@@ -1914,9 +1962,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MAXD == 0 ?
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int px = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
-    const int ly = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
-    const int py = F.row_begin + ly;
-    const bool valid = px < F.width && py < F.row_end;
+    const int ly0 = blockIdx.y * 16 + (wave >> 1) * 8;  // the wave's first output row
+    const int ly = ly0 + (lane >> 3);
+    // frame row of output row r: the slab, or band (r / band_rows) of this
+    // rank's cyclic set (a wave's 8 rows never straddle a band: 16 | band_rows)
+    int py0 = F.row_begin + ly0, rend = F.row_end;
+    if (F.band_rows > 0) {
+        py0 = ((ly0 / F.band_rows) * F.band_count + F.band_index) * F.band_rows + ly0 % F.band_rows;
+        rend = F.height;
+    }
+    if (py0 >= rend) return;  // the whole wave lies past the frame (wave-uniform)
+    const int py = py0 + (lane >> 3);
+    const bool valid = px < F.width && py < rend;
 
     Counters cnt;
 #ifdef RT_PROF
@@ -1927,7 +1984,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MAXD == 0 ?
     // pixel, result dropped) so edge waves stay whole for wave-level culling.
     if (MAXD == 0 || valid) {
         const int pxc = px < F.width ? px : F.width - 1;
-        const int pyc = py < F.row_end ? py : F.row_end - 1;
+        const int pyc = py < rend ? py : rend - 1;
         // Scene.cpp:1543-1552: (float)(2*PixX) * InvW - 1, then * HalfW
         const Vec3 d0 = make3((2 * pxc * F.inv_w - 1) * F.half_w, (2 * pyc * F.inv_h - 1) * F.half_h, -1.0f);
         Mat4 M;
@@ -2060,6 +2117,7 @@ struct rt_ctx {
     float4* d_clu_cam = nullptr;
     float4* d_clu_light = nullptr;
     int n_clu = 0;
+    float4* d_uni = nullptr;  // union records (small lists): camera, then one per light
     // light buffer (shadow cells), rt_lb_build
     unsigned* d_lb_off = nullptr;
     float4* d_lb_ent = nullptr;
@@ -2146,6 +2204,7 @@ RT_EXPORT void rt_destroy(rt_ctx* c)
     hipFree(c->d_lb_ent);
     hipFree(c->d_lb_dcap);
     hipFree(c->d_lb_meta);
+    hipFree(c->d_uni);
     hipFree(c->d_stats);
     hipFree(c->d_scratch);
     if (c->ev0) hipEventDestroy(c->ev0);
@@ -2492,6 +2551,8 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
     c->d_lb_ent = c->d_lb_dcap = c->d_lb_meta = nullptr;
     c->lb_ready = false;
     c->lb_entries = 0;
+    hipFree(c->d_uni);
+    c->d_uni = nullptr;
     c->cam_valid = false;
     c->d_geom = c->d_mat = c->d_lights = c->d_tri = c->d_plane = c->d_quad = nullptr;
     c->d_translucent = nullptr;
@@ -2592,6 +2653,23 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
             HIP_TRY(c, hipGetLastError());
         }
     }
+    if (ntr > 0 && ntr <= (size_t)kClusterMinTriangles) {
+        // union records: [camera (filled when the camera is set)] [light 0] ...
+        HIP_TRY(c, hipMalloc((void**)&c->d_uni, (size_t)(nl + 1) * 2 * sizeof(float4)));
+        for (int j = 0; j < nl && n_tri_o > 0; ++j) {
+            hipLaunchKernelGGL(rt_cluster_prepass, dim3(1), dim3(64), 0, 0, c->d_cone_light + kConeRec * ntr * j,
+                               n_tri_o, 1, c->d_uni + 2 * (1 + (size_t)j), n_tri_o);
+            HIP_TRY(c, hipGetLastError());
+        }
+        if (n_tri_o == 0) {  // no opaque triangle: nothing for shadow rays to walk ("never" record)
+            std::vector<float4> nev((size_t)nl * 2);
+            for (int j = 0; j < nl; ++j) {
+                nev[2 * j] = make_float4(0.f, 0.f, 0.f, 2.0f);
+                nev[2 * j + 1] = make_float4(INFINITY, 0.f, INFINITY, 0.f);
+            }
+            if (nl) HIP_TRY(c, hipMemcpy(c->d_uni + 2, nev.data(), nev.size() * sizeof(float4), hipMemcpyHostToDevice));
+        }
+    }
     HIP_TRY(c, hipDeviceSynchronize());
     const int lbm = lb_mode();  // built only where launch() will use it
     if (ntr > 0 && nl > 0 && n_tri_o > 0 && opaque && (lbm == 1 || (lbm == 2 && ntr > (size_t)kClusterMinTriangles))) {
@@ -2684,6 +2762,13 @@ static kernel_fn pick_kernel(int depth, int n_tri, int n_lights, bool lbuf, int&
     return nullptr;
 }
 
+// Output rows of a launch: the slab, or this rank's band set.
+static int frame_rows(const rt_frame* f)
+{
+    if (f->band_rows != 0) return std::max(0, (int)rt_band_rows(f->height, f->band_rows, f->band_count, f->band_index));
+    return f->row_end - f->row_begin;
+}
+
 static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_dev, hipStream_t st, bool timed)
 {
     if (!c || !f) return RT_E_ARG;
@@ -2692,7 +2777,8 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
         return RT_E_STATE;
     }
     if (f->width <= 0 || f->height <= 0 || f->row_begin < 0 || f->row_end > f->height ||
-        f->row_begin > f->row_end || f->max_bounces < 0) {
+        f->row_begin > f->row_end || f->max_bounces < 0 ||
+        (f->band_rows != 0 && rt_band_rows(f->height, f->band_rows, f->band_count, f->band_index) < 0)) {
         c->err = "bad rt_frame geometry";
         return RT_E_ARG;
     }
@@ -2711,7 +2797,8 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
                use_tricam, c->n_tri <= kEdgeMaxTriangles, c->d_cone_cam, c->d_cone_light, c->d_clu_cam,
                c->d_clu_light, c->n_clu, c->n_surf, c->n_lights, c->n_tri, c->n_plane, c->n_quad,
                c->n_tri_opaque, c->n_plane_opaque, c->n_quad_opaque, c->n_translucent, c->shadow_split,
-               lbuf ? 1 : 0, c->d_lb_off, c->d_lb_ent, c->d_lb_dcap, c->d_lb_meta};
+               lbuf ? 1 : 0, c->d_lb_off, c->d_lb_ent, c->d_lb_dcap, c->d_lb_meta,
+               (c->d_uni && !getenv("RT_AMD_NO_UNION")) ? c->d_uni : nullptr};
     FrameDev F;
     std::memcpy(F.cam, f->cam_pos, sizeof F.cam);
     std::memcpy(F.orient, f->orient, sizeof F.orient);
@@ -2728,7 +2815,10 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
     F.min_energy = f->min_energy;
     F.scene_ior = f->scene_ior;
     F.flags = f->flags;
-    const int rows = f->row_end - f->row_begin;
+    F.band_rows = f->band_rows;
+    F.band_count = f->band_count;
+    F.band_index = f->band_index;
+    const int rows = frame_rows(f);
     c->last = rt_stats{};
     c->last.stack_depth = cap;
     c->last.light_batch = lb;
@@ -2745,6 +2835,11 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
         hipLaunchKernelGGL(rt_cone_prepass, dim3((c->n_tri + 255) / 256), dim3(256), 0, st, c->d_tri, c->d_trisph,
                            c->d_trinrm, c->d_tricoef, c->n_tri, cp[0], cp[1], cp[2], 1, 0.0f, c->d_cone_cam);
         HIP_TRY(c, hipGetLastError());
+        if (c->d_uni) {
+            hipLaunchKernelGGL(rt_cluster_prepass, dim3(1), dim3(64), 0, st, c->d_cone_cam, c->n_tri, 1, c->d_uni,
+                               c->n_tri);
+            HIP_TRY(c, hipGetLastError());
+        }
         if (c->n_clu > 0) {
             float4* tmp = c->d_clu_cam + 2 * (size_t)c->n_clu;  // second half: unsorted
             hipLaunchKernelGGL(rt_cluster_prepass, dim3((unsigned)((c->n_clu + 63) / 64)), dim3(64), 0, st,
@@ -2823,7 +2918,7 @@ static int render_sync(rt_ctx* c, const rt_frame* f, void* out, bool as_float)
 {
     if (!c || !f || !out) return RT_E_ARG;
     HIP_TRY(c, hipSetDevice(c->device));
-    const size_t px = (size_t)f->width * (size_t)std::max(0, f->row_end - f->row_begin);
+    const size_t px = (size_t)f->width * (size_t)std::max(0, frame_rows(f));
     const size_t bytes = px * (as_float ? 12 : 4);
     const bool dev = is_device_ptr(out);
     void* target = out;

@@ -380,6 +380,16 @@ struct rt_scene {
 
 RT_EXPORT int rt_abi_version(void) { return RT_ABI_VERSION; }
 
+RT_EXPORT int32_t rt_band_rows(int32_t height, int32_t band_rows, int32_t band_count, int32_t band_index)
+{
+    if (height < 0 || band_rows <= 0 || band_rows % 16 != 0 || band_count <= 0 || band_index < 0 ||
+        band_index >= band_count)
+        return -1;
+    const int64_t nb = ((int64_t)height + band_rows - 1) / band_rows;  // bands in the frame
+    const int64_t mine = nb > band_index ? (nb - band_index + band_count - 1) / band_count : 0;
+    return (int32_t)(mine * band_rows);
+}
+
 RT_EXPORT int rt_scene_create(rt_scene** out)
 {
     if (!out) return RT_E_ARG;

@@ -23,7 +23,7 @@ from typing import Optional
 import numpy as np
 
 __all__ = [
-    "RtError", "SceneFlat", "Frame", "Stats", "Scene", "Context", "CScene", "lib",
+    "RtError", "SceneFlat", "Frame", "Stats", "Scene", "Context", "CScene", "lib", "band_rows", "frame_rows",
     "LIB_PATH", "TRIANGLE", "PLANE", "QUADRIC", "FLAG_STATS",
 ]
 
@@ -56,7 +56,8 @@ class Frame(ctypes.Structure):
                 ("width", ctypes.c_int32), ("height", ctypes.c_int32),
                 ("row_begin", ctypes.c_int32), ("row_end", ctypes.c_int32),
                 ("max_bounces", ctypes.c_int32), ("min_energy", ctypes.c_float),
-                ("scene_ior", ctypes.c_float), ("flags", ctypes.c_int32)]
+                ("scene_ior", ctypes.c_float), ("flags", ctypes.c_int32),
+                ("band_rows", ctypes.c_int32), ("band_count", ctypes.c_int32), ("band_index", ctypes.c_int32)]
 
     def copy(self) -> "Frame":
         f = Frame()
@@ -78,6 +79,7 @@ _lib: Optional[ctypes.CDLL] = None
 _VP = ctypes.c_void_p
 SIGNATURES = {
     "rt_abi_version": (ctypes.c_int, []),
+    "rt_band_rows": (ctypes.c_int32, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
     "rt_scene_create": (ctypes.c_int, [ctypes.POINTER(_VP)]),
     "rt_scene_set_resolution": (ctypes.c_int, [_VP, ctypes.c_int32, ctypes.c_int32]),
     "rt_scene_set_max_bounces": (ctypes.c_int, [_VP, ctypes.c_int32]),
@@ -98,6 +100,21 @@ SIGNATURES = {
     "rt_last_error": (ctypes.c_char_p, [_VP]),
     "rt_destroy": (None, [_VP]),
 }
+
+
+def band_rows(height: int, band_rows: int, band_count: int, band_index: int) -> int:
+    """Output rows of one rank's cyclic band set (rt.h rt_band_rows), host-side."""
+    if height < 0 or band_rows <= 0 or band_rows % 16 or band_count <= 0 or not 0 <= band_index < band_count:
+        raise ValueError("bad band layout")
+    nb = -(-height // band_rows)
+    return (-(-(nb - band_index) // band_count) if nb > band_index else 0) * band_rows
+
+
+def frame_rows(frame: "Frame") -> int:
+    """Rows a render of `frame` writes: the slab, or the packed band set."""
+    if frame.band_rows:  # an invalid layout gives 0 rows here; the render call rejects it
+        return max(0, lib().rt_band_rows(frame.height, frame.band_rows, frame.band_count, frame.band_index))
+    return frame.row_end - frame.row_begin
 
 
 def lib() -> ctypes.CDLL:
@@ -194,14 +211,15 @@ class Context:
         _check("rt_upload_scene", lib().rt_upload_scene(self._h, ctypes.byref(scene.flat)), self._err)
 
     def render(self, frame: Frame) -> np.ndarray:
-        """RGBA8 (rows, W, 4), row 0 = frame.row_begin (bottom-up)."""
-        rows = frame.row_end - frame.row_begin
+        """RGBA8 (rows, W, 4), row 0 = frame.row_begin (bottom-up), or this
+        rank's packed band set when frame.band_rows > 0."""
+        rows = frame_rows(frame)
         out = np.zeros((rows, frame.width, 4), np.uint8)
         _check("rt_render", lib().rt_render(self._h, ctypes.byref(frame), out.ctypes.data), self._err)
         return out
 
     def render_float(self, frame: Frame) -> np.ndarray:
-        rows = frame.row_end - frame.row_begin
+        rows = frame_rows(frame)
         out = np.zeros((rows, frame.width, 3), np.float32)
         _check("rt_render_float", lib().rt_render_float(self._h, ctypes.byref(frame), out.ctypes.data), self._err)
         return out

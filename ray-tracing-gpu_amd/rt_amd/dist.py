@@ -32,6 +32,16 @@ def slab_rows(height: int, world: int, rank: int) -> Tuple[int, int, int]:
     return r0, r1, rows
 
 
+def band_layout(height: int, world: int, band_rows: int = 16) -> Tuple[int, int]:
+    """Cyclic row bands (rt_frame.band_rows): (bands per rank Q, rows per
+    rank Q * band_rows).  Every rank gets an equal buffer; rank r's band k is
+    the frame's band k * world + r (rows past the frame are left unwritten)."""
+    if world <= 0 or band_rows <= 0 or band_rows % 16:
+        raise ValueError("bad band layout")
+    q = -(-(-(-height // band_rows)) // world)
+    return q, q * band_rows
+
+
 def gather_frame(slab, full, dist, group=None):
     """All-gather equal-height slabs into `full` ([world*rows, W, 4]) on every
     rank.  RCCL: one all-gather; gloo (CPU tests): the list form."""
@@ -57,27 +67,40 @@ class RootGather:
     frame once ``g.wait(k)`` (or ``g.finish()``) has run.
     """
 
-    def __init__(self, dist, height: int, width: int, device, depth: int = 2, dtype=None, channels: int = 4):
+    def __init__(self, dist, height: int, width: int, device, depth: int = 2, dtype=None, channels: int = 4,
+                 band_rows: int = 0):
         import torch
 
         self.dist = dist
         self.world = dist.get_world_size()
         self.rank = dist.get_rank()
-        self.H, self.W = height, width
-        _, _, self.rows = slab_rows(height, self.world, self.rank)
+        self.H, self.W, self.C = height, width, channels
+        # band_rows > 0: each rank renders cyclic row bands (rt_frame.band_rows)
+        # for load balance; rank 0 gathers the band sets into a staging buffer
+        # and un-permutes them into the frame with one strided copy.
+        self.band_rows = band_rows
+        if band_rows:
+            self.q, self.rows = band_layout(height, self.world, band_rows)
+        else:
+            _, _, self.rows = slab_rows(height, self.world, self.rank)
         self.depth = depth
         dtype = dtype or torch.uint8
         shape_full = (self.world * self.rows, width, channels)
         shape_slab = (self.rows, width, channels)
+        self.staging = []
         if self.rank == 0:
             self.frames = [torch.zeros(shape_full, dtype=dtype, device=device) for _ in range(depth)]
-            self.slabs = [f[: self.rows] for f in self.frames]
+            if band_rows:
+                self.staging = [torch.zeros(shape_full, dtype=dtype, device=device) for _ in range(depth)]
+            src = self.staging if band_rows else self.frames
+            self.slabs = [f[: self.rows] for f in src]
+            # the gather's targets: row blocks in rank order (contiguous views)
+            self.views = [[f[r * self.rows:(r + 1) * self.rows] for r in range(self.world)] for f in src]
         else:
             self.frames = []
             self.slabs = [torch.zeros(shape_slab, dtype=dtype, device=device) for _ in range(depth)]
+            self.views = []
         self.pending: List[Optional[list]] = [None] * depth
-        # rank 0: the frame buffer's row slabs, in rank order (contiguous views)
-        self.views = [[f[r * self.rows:(r + 1) * self.rows] for r in range(self.world)] for f in self.frames]
 
     def target(self, k: int):
         """Buffer to render frame k's slab into (waits until it is free)."""
@@ -101,6 +124,11 @@ class RootGather:
             for w in self.pending[b]:
                 w.wait()
             self.pending[b] = None
+            if self.band_rows and self.rank == 0:
+                # staging[rank][local band][row] -> frame[global band = local * world + rank][row]
+                br, W, C = self.band_rows, self.W, self.C
+                self.frames[b].view(self.q, self.world, br, W, C).copy_(
+                    self.staging[b].view(self.world, self.q, br, W, C).transpose(0, 1))
 
     def finish(self):
         for b in range(self.depth):

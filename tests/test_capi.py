@@ -36,7 +36,7 @@ def test_header_symbols_exported():
 
 
 def test_abi_version():
-    assert rt_amd.lib().rt_abi_version() == 2
+    assert rt_amd.lib().rt_abi_version() == 3
 
 
 def test_struct_layouts_match_header():
@@ -45,9 +45,9 @@ def test_struct_layouts_match_header():
 #include <stddef.h>
 #include "rt.h"
 int main(void){
-  printf("%zu %zu %zu %zu %zu %zu %zu\n", sizeof(rt_scene_flat), sizeof(rt_frame), sizeof(rt_stats),
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(rt_scene_flat), sizeof(rt_frame), sizeof(rt_stats),
          offsetof(rt_frame, width), offsetof(rt_frame, flags), offsetof(rt_stats, kernel_ms),
-         offsetof(rt_stats, triangle_tests));
+         offsetof(rt_stats, triangle_tests), offsetof(rt_frame, band_index));
   return 0; }
 """
     import tempfile
@@ -60,7 +60,7 @@ int main(void){
         vals = list(map(int, subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split()))
     assert vals == [ctypes.sizeof(rt_amd.SceneFlat), ctypes.sizeof(rt_amd.Frame), ctypes.sizeof(rt_amd.Stats),
                     rt_amd.Frame.width.offset, rt_amd.Frame.flags.offset, rt_amd.Stats.kernel_ms.offset,
-                    rt_amd.Stats.triangle_tests.offset]
+                    rt_amd.Stats.triangle_tests.offset, rt_amd.Frame.band_index.offset]
 
 
 def test_null_arguments_are_errors():
@@ -94,3 +94,18 @@ def test_cli_built():
     assert os.access(exe, os.X_OK)
     r = subprocess.run([exe], capture_output=True, text=True)
     assert r.returncode == 1 and "Aucune fichier" in r.stderr
+
+
+def test_band_rows_matches_binding():
+    L = rt_amd.lib()
+    for h in (1, 15, 16, 17, 1080, 4320):
+        for br in (16, 32, 48):
+            for n in (1, 2, 3, 8):
+                tot = 0
+                for i in range(n):
+                    got = L.rt_band_rows(h, br, n, i)
+                    assert got == rt_amd.band_rows(h, br, n, i)
+                    tot += got
+                assert tot == -(-h // br) * br  # every band exactly once
+    assert L.rt_band_rows(100, 8, 2, 0) == -1    # not a multiple of 16
+    assert L.rt_band_rows(100, 16, 2, 2) == -1   # index out of range

@@ -45,20 +45,29 @@ def _worker(rank, world, port, path, w, h, depth, out_q):
     dist.destroy_process_group()
 
 
-def _worker_root(rank, world, port, path, w, h, depth, out_q):
-    """RootGather: 3 frames through the double-buffered p2p gather."""
+def _worker_root(rank, world, port, path, w, h, depth, out_q, band_rows=0):
+    """RootGather: 3 frames through the double-buffered gather (row slabs,
+    or cyclic bands of `band_rows` rows un-permuted on rank 0)."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from conftest import Oracle
     from rt_amd.dist import RootGather
 
-    g = RootGather(dist, h, w, "cpu", depth=2)
+    g = RootGather(dist, h, w, "cpu", depth=2, band_rows=band_rows)
     r0, r1, rows = slab_rows(h, world, rank)
     frames = []
     for k in range(3):
         buf = g.target(k)
         buf.zero_()
-        if r1 > r0:
+        if band_rows:
+            # frame k = the scene at depth k; this rank's bands, packed in order
+            for q in range(g.q):
+                a = (q * world + rank) * band_rows
+                if a < h:
+                    e = min(h, a + band_rows)
+                    img = Oracle().render(path, w, h, k, (a, e, 0, w), threads=1)
+                    buf[q * band_rows: q * band_rows + (e - a)] = torch.from_numpy(rgba8(img))
+        elif r1 > r0:
             # frame k = the scene at depth k (different images per frame)
             img = Oracle().render(path, w, h, k, (r0, r1, 0, w), threads=1)
             buf[: r1 - r0] = torch.from_numpy(rgba8(img))
@@ -74,14 +83,15 @@ def _worker_root(rank, world, port, path, w, h, depth, out_q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,h", [(2, 30), (3, 31)])
-def test_root_gather_pipelined(oracle, world, h):
+@pytest.mark.parametrize("world,h,band_rows", [(2, 30, 0), (3, 31, 0), (2, 70, 16), (3, 71, 16), (3, 50, 32)])
+def test_root_gather_pipelined(oracle, world, h, band_rows):
     w = 36
     path = os.path.join(SCENES, "scene7.dat")
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker_root, args=(r, world, port, path, w, h, 0, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker_root, args=(r, world, port, path, w, h, 0, q, band_rows))
+             for r in range(world)]
     for p in procs:
         p.start()
     got = q.get(timeout=120)
@@ -120,3 +130,18 @@ def test_slab_rows_cover_frame():
             assert spans[0][0] == 0 and spans[-1][1] == h
             for a, b in zip(spans, spans[1:]):
                 assert a[1] == b[0]
+
+
+def test_band_layout_covers_frame():
+    from rt_amd import band_rows
+    from rt_amd.dist import band_layout
+
+    for h in (1, 17, 1080, 4320, 2161):
+        for world in (1, 2, 3, 8):
+            for br in (16, 32):
+                q, rows = band_layout(h, world, br)
+                assert rows == q * br
+                # every rank's packed band set fits its equal buffer, and the
+                # band sets tile the frame's bands exactly once
+                assert all(band_rows(h, br, world, r) <= rows for r in range(world))
+                assert sum(band_rows(h, br, world, r) for r in range(world)) == -(-h // br) * br

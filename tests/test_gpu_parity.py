@@ -138,6 +138,39 @@ def test_row_slabs_reassemble(ctx, nslabs):
     assert np.array_equal(np.concatenate(parts, 0), full)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("sc,depth,w,h", [(2, 3, 200, 150), (7, 3, 120, 90), (9, 5, 96, 70)])
+@pytest.mark.parametrize("nranks,band_rows", [(2, 16), (3, 16), (8, 16), (3, 32)])
+def test_row_bands_reassemble(ctx, sc, depth, w, h, nranks, band_rows):
+    """Cyclic row bands (rt_frame.band_rows, ABI 3): every rank's packed band
+    set, un-permuted, == the full frame (float RGB, bit for bit)."""
+    s = rt_amd.Scene(scene(sc), w, h, depth)
+    ctx.upload(s)
+    full = ctx.render_float(s.frame)
+    got = np.full_like(full, np.nan)
+    for r in range(nranks):
+        f = s.frame.copy()
+        f.band_rows, f.band_count, f.band_index = band_rows, nranks, r
+        part = ctx.render_float(f)
+        assert part.shape[0] == rt_amd.band_rows(h, band_rows, nranks, r)
+        for q in range(part.shape[0] // band_rows):
+            a = (q * nranks + r) * band_rows
+            e = min(h, a + band_rows)
+            got[a:e] = part[q * band_rows: q * band_rows + (e - a)]
+    assert bits_equal(got, full)
+
+
+@pytest.mark.gpu
+def test_bad_band_layout_rejected(ctx):
+    s = rt_amd.Scene(scene(2), 64, 64, 0)
+    ctx.upload(s)
+    for br, n, i in ((8, 2, 0), (16, 0, 0), (16, 2, 2), (16, 2, -1)):
+        f = s.frame.copy()
+        f.band_rows, f.band_count, f.band_index = br, n, i
+        with pytest.raises(rt_amd.RtError):
+            ctx.render(f)
+
+
 def test_async_device_outputs(ctx):
     torch = pytest.importorskip("torch")
     s = rt_amd.Scene(scene(6), 128, 96, 3)

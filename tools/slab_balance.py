@@ -62,9 +62,16 @@ def main():
                 fr = s.frame.copy()
                 fr.row_begin, fr.row_end = r0, r1
                 ts.append(time_frame(ctx, fr, out, stream, frames))
+            bs = []
+            for rank in range(n):  # cyclic 16-row bands (rt_frame.band_rows)
+                fr = s.frame.copy()
+                fr.band_rows, fr.band_count, fr.band_index = 16, n, rank
+                bs.append(time_frame(ctx, fr, out, stream, frames))
             r[f"n{n}"] = {"slab_ms": [round(t, 4) for t in ts], "max_ms": round(max(ts), 4),
                           "imbalance": round(max(ts) / (sum(ts) / n) - 1.0, 3),
-                          "ideal_speedup": round(full / max(ts), 2)}
+                          "ideal_speedup": round(full / max(ts), 2),
+                          "band_ms": [round(t, 4) for t in bs], "band_imbalance": round(max(bs) / (sum(bs) / n) - 1.0, 3),
+                          "band_ideal_speedup": round(full / max(bs), 2)}
         res[cfg] = r
         print(json.dumps({cfg: r}), flush=True)
     print(json.dumps(res))
