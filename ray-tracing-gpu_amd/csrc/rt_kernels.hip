@@ -938,6 +938,7 @@ __global__ void rt_cluster_sort(const float4* __restrict__ in, int nclu, float4*
 // per-light list sorted by dcap, tested by the lanes with dist > dcap — the
 // per-lane predicate light_reach, split in two.
 constexpr int kLbGroup = 16;  // cells per supercell edge (two-level build)
+constexpr int kLbEnt = 3;     // float4 per light-buffer entry (48 B)
 
 __device__ __forceinline__ int lb_cell(const Vec3 d, int R)
 {
@@ -1067,17 +1068,17 @@ __global__ __launch_bounds__(256) void rt_lb_super(const float4* __restrict__ co
     if (!lists && threadIdx.x == 0) counts[s] = total;
 }
 
-// 64-byte light-buffer entry of triangle k (tri[] record + light record):
-//   [p0, key] [e1, e2.x] [e2.y e2.z, 2/dmin, 0] [c0 = dir to centre, cosT]
-// key = dmin (cell lists) or dcap (dcap list).
-__device__ __forceinline__ void lb_write(float4* o, const float4* __restrict__ tri, int k, const float4 c0,
-                                         const float4 c1, float key)
+// 48-byte light-buffer entry of triangle k (its tri[] record):
+//   [p0, key] [e1, e2.x] [e2.y e2.z, 0, 0]
+// key = dmin (cell lists) or dcap (dcap list).  (A per-lane cone test in
+// front of the exact test was measured to spare no wave any exact test: a
+// cell's list is already what its lanes' cones can reach.)
+__device__ __forceinline__ void lb_write(float4* o, const float4* __restrict__ tri, int k, float key)
 {
     const float4 a = tri[3 * k], b = tri[3 * k + 1], c = tri[3 * k + 2];
     o[0] = make_float4(a.x, a.y, a.z, key);
     o[1] = make_float4(a.w, b.x, b.y, b.z);
-    o[2] = make_float4(b.w, c.x, c1.y, 0.0f);
-    o[3] = c0;
+    o[2] = make_float4(b.w, c.x, 0.0f, 0.0f);
 }
 
 // Build pass 2: one thread per cell of a supercell, over the supercell's
@@ -1112,7 +1113,7 @@ __global__ __launch_bounds__(256) void rt_lb_cells(const float4* __restrict__ co
         for (int x = 0; x < m; ++x) {
             const float4 c0 = rec[kConeRec * x], c1 = rec[kConeRec * x + 1];
             if (!lb_keep(wc, c0, c1, rec + kConeRec * x + 2, dcov)) continue;
-            if (ent) lb_write(ent + 4 * (size_t)out++, tri, kid[x], c0, c1, c1.x);
+            if (ent) lb_write(ent + kLbEnt * (size_t)out++, tri, kid[x], c1.x);
             else ++cnt;
         }
     }
@@ -1127,7 +1128,7 @@ __global__ void rt_lb_dcap(const float4* __restrict__ cone, const float4* __rest
     if (q >= m) return;
     const int k = perm[q];
     const float4 c0 = cone[2 * k], c1 = cone[2 * k + 1];
-    lb_write(out + 4 * (size_t)q, tri, k, c0, c1, c1.z == c1.z ? c1.z : -INFINITY);
+    lb_write(out + kLbEnt * (size_t)q, tri, k, c1.z == c1.z ? c1.z : -INFINITY);
 }
 
 // Shadow-ray cull predicate (L normalised towards the light, dist to it):
@@ -1564,31 +1565,43 @@ __device__ __forceinline__ void shadow_opaque_lb(const SceneDev& S, int l, const
     }
     const float slack = dist * 1e-6f;
     RT_MARK(cnt, 3);
+    // The next entry's loads are issued before the current entry's exact
+    // test (software pipelining of the per-lane gathers).
+    float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0, r2 = r0;
+    bool have = e < end;
+    if (have) {
+        const float4* r = S.lb_ent + kLbEnt * (size_t)e;
+        r0 = r[0];
+        r1 = r[1];
+        r2 = r[2];
+    }
     for (;;) {
-        const bool act = (e < end) & !occ;
+        const bool act = have & !occ;
         if (!__any(act)) break;
         RT_EV(cnt, 3);
         bool go = false;
-        float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0, r2 = r0;
+        const float4 c0 = r0, c1 = r1, c2 = r2;
         if (act) {
-            const float4* r = S.lb_ent + 4 * (size_t)e;
-            r0 = r[0];
-            r1 = r[1];
-            r2 = r[2];
-            const float4 r3 = r[3];
-            if (!(r0.w < dist)) {
-                e = end;  // this and every later entry lie beyond P (dmin)
+            if (!(c0.w < dist)) {
+                have = false;  // this and every later entry lie beyond P (dmin)
             } else {
+                go = true;
                 ++e;
-                go = -dot(L, make3(r3.x, r3.y, r3.z)) >= r3.w - slack * r2.z;
+                have = e < end;
+                if (have) {
+                    const float4* r = S.lb_ent + kLbEnt * (size_t)e;
+                    r0 = r[0];
+                    r1 = r[1];
+                    r2 = r[2];
+                }
             }
         }
         if (__any(go)) {
             ++cnt.tri;
             RT_EV(cnt, 4);
             if (go) {
-                const Vec3 e1 = make3(r1.x, r1.y, r1.z), e2 = make3(r1.w, r2.x, r2.y);
-                const TriU u = tri_u(make3(r0.x, r0.y, r0.z), e1, e2, P, L);
+                const Vec3 e1 = make3(c1.x, c1.y, c1.z), e2 = make3(c1.w, c2.x, c2.y);
+                const TriU u = tri_u(make3(c0.x, c0.y, c0.z), e1, e2, P, L);
                 float t;
                 const bool ok = tri_vt(u, e1, e2, L, t);
                 occ |= ok & (t > kEps) & (t < dist);
@@ -1599,7 +1612,7 @@ __device__ __forceinline__ void shadow_opaque_lb(const SceneDev& S, int l, const
     // pairs not culled up to dcov: sorted by dcap, so once no live lane lies
     // beyond an entry's cap none lies beyond a later one
     for (unsigned q = 0; q < ndcap; ++q) {
-        const float4* r = S.lb_dcap + 4 * (size_t)(dbase + q);
+        const float4* r = S.lb_dcap + kLbEnt * (size_t)(dbase + q);
         const float4 r0 = r[0];
         const bool need = use & !occ & (dist > r0.w);
         if (!__any(need)) break;
@@ -2366,8 +2379,8 @@ static int lb_build(rt_ctx* c, int ntr, int n_opaque, int nl, const std::vector<
             goto done;
         }
         LB_TRY(hipMalloc(&c->d_lb_off, off_words * sizeof(unsigned)));
-        LB_TRY(hipMalloc(&c->d_lb_ent, std::max<size_t>(total, 1) * 4 * sizeof(float4)));
-        LB_TRY(hipMalloc(&c->d_lb_dcap, std::max<size_t>(dcap_total, 1) * 4 * sizeof(float4)));
+        LB_TRY(hipMalloc(&c->d_lb_ent, std::max<size_t>(total, 1) * kLbEnt * sizeof(float4)));
+        LB_TRY(hipMalloc(&c->d_lb_dcap, std::max<size_t>(dcap_total, 1) * kLbEnt * sizeof(float4)));
         LB_TRY(hipMalloc(&c->d_lb_meta, std::max(nl, 1) * 2 * sizeof(float4)));
         std::vector<float4> meta((size_t)std::max(nl, 1) * 2);
         size_t obase = 0, ebase = 0, dbase = 0;
@@ -2389,7 +2402,7 @@ static int lb_build(rt_ctx* c, int ntr, int n_opaque, int nl, const std::vector<
             if (!b.dperm.empty()) {
                 LB_TRY(hipMemcpy(d_perm, b.dperm.data(), b.dperm.size() * sizeof(int), hipMemcpyHostToDevice));
                 hipLaunchKernelGGL(rt_lb_dcap, dim3((unsigned)((b.dperm.size() + 255) / 256)), dim3(256), 0, 0, cone,
-                                   c->d_tri, d_perm, (int)b.dperm.size(), c->d_lb_dcap + 4 * dbase);
+                                   c->d_tri, d_perm, (int)b.dperm.size(), c->d_lb_dcap + kLbEnt * dbase);
                 LB_TRY(hipGetLastError());
                 LB_TRY(hipDeviceSynchronize());  // d_perm is reused by the next light
             }
