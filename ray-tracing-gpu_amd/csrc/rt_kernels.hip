@@ -1568,7 +1568,11 @@ __device__ __forceinline__ void shadow_opaque_lb(const SceneDev& S, int l, const
     // The next entry's loads are issued before the current entry's exact
     // test (software pipelining of the per-lane gathers).
     float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0, r2 = r0;
+#ifdef RT_ABLATE_LBCELL  // timing-only build: no cell walk
+    bool have = false;
+#else
     bool have = e < end;
+#endif
     if (have) {
         const float4* r = S.lb_ent + kLbEnt * (size_t)e;
         r0 = r[0];
@@ -1602,16 +1606,22 @@ __device__ __forceinline__ void shadow_opaque_lb(const SceneDev& S, int l, const
             if (go) {
                 const Vec3 e1 = make3(c1.x, c1.y, c1.z), e2 = make3(c1.w, c2.x, c2.y);
                 const TriU u = tri_u(make3(c0.x, c0.y, c0.z), e1, e2, P, L);
-                float t;
-                const bool ok = tri_vt(u, e1, e2, L, t);
-                occ |= ok & (t > kEps) & (t < dist);
+                if (__any(u.ok)) {  // v and t only where some lane's u is in [0, 1]
+                    float t;
+                    const bool ok = tri_vt(u, e1, e2, L, t);
+                    occ |= ok & (t > kEps) & (t < dist);
+                }
             }
         }
     }
     RT_MARK(cnt, 4);
     // pairs not culled up to dcov: sorted by dcap, so once no live lane lies
     // beyond an entry's cap none lies beyond a later one
+#ifdef RT_ABLATE_LBLIST  // timing-only build: no per-light list
+    for (unsigned q = 0; q < 0; ++q) {
+#else
     for (unsigned q = 0; q < ndcap; ++q) {
+#endif
         const float4* r = S.lb_dcap + kLbEnt * (size_t)(dbase + q);
         const float4 r0 = r[0];
         const bool need = use & !occ & (dist > r0.w);
@@ -1622,9 +1632,11 @@ __device__ __forceinline__ void shadow_opaque_lb(const SceneDev& S, int l, const
         if (need) {
             const Vec3 e1 = make3(r1.x, r1.y, r1.z), e2 = make3(r1.w, r2.x, r2.y);
             const TriU u = tri_u(make3(r0.x, r0.y, r0.z), e1, e2, P, L);
-            float t;
-            const bool ok = tri_vt(u, e1, e2, L, t);
-            occ |= ok & (t > kEps) & (t < dist);
+            if (__any(u.ok)) {
+                float t;
+                const bool ok = tri_vt(u, e1, e2, L, t);
+                occ |= ok & (t > kEps) & (t < dist);
+            }
         }
     }
     // lanes the buffer does not cover: every opaque triangle, culled per lane
