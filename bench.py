@@ -249,6 +249,12 @@ def main():
     sf.flags = rt_amd.FLAG_STATS
     ctx.render(sf)
     st = ctx.stats()
+    cbinfo = None  # the camera buffer, built by that synchronous render (per camera)
+    if hasattr(L, "rt_debug_cb_info"):
+        L.rt_debug_cb_info.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        ci = (ctypes.c_double * 4)()
+        if L.rt_debug_cb_info(ctx._h, ci, 4) == 0 and ci[0]:
+            cbinfo = {"entries": int(ci[1]), "build_ms": round(ci[2], 2), "tiles": int(ci[3])}
     brute = algorithmic_flops(types, st.primary_rays, st.bounce_rays, st.shadow_rays)
     flops = executed_flops(st)
     brute_tests = (st.primary_rays + st.bounce_rays + st.shadow_rays) * int(types.shape[0])
@@ -352,6 +358,7 @@ def main():
             "kernel_ms": round(kernel_ms, 4),
             "upload_ms": round(upload_ms, 2),
             "light_buffer": lbinfo,
+            "camera_buffer": cbinfo,
             "hbm": {"algorithmic_bytes": int(alg_bytes), "measured_bytes": traffic,
                     "measured_gbps": round(traffic / (kernel_ms * 1e-3) / 1e9, 1) if traffic else None,
                     "frac_of_8TBps": round(traffic / (kernel_ms * 1e-3) / 8e12, 4) if traffic else None,

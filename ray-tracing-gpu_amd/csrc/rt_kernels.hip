@@ -135,6 +135,15 @@ struct SceneDev {
     // the camera (uni[0..1]) and over the opaque ones for each light
     // (uni[2 + 2l ..]); nullptr: none.
     const float4* __restrict__ uni;
+    // Camera buffer (depth-0 kernels, WAVE bit 8): per 8x8 tile of the full
+    // frame (tile = row/8 * cb_tiles_x + col/8), the triangles the tile's
+    // wave cone can reach (the camera wave test), with a key = min dmin of
+    // the entry and every later one; cb_flag[tile] != 0: no list (per-wave
+    // path).  Built once per camera (rt_cb_build).  cb_tiles_x = 0: none.
+    const unsigned* __restrict__ cb_off;
+    const int2* __restrict__ cb_ent;
+    const unsigned* __restrict__ cb_flag;
+    int cb_tiles_x;
 };
 
 struct FrameDev {
@@ -657,16 +666,72 @@ __device__ __forceinline__ int closest_hit_camera_wave(const SceneDev& S, const 
     return bi;
 }
 
+// Scene.cpp:1543-1552: the primary ray direction of pixel (pxc, pyc):
+// (float)(2*PixX) * InvW - 1, then * HalfW; times the orientation; then
+// Vecteur3.h Normaliser with the exact fast sqrt / reciprocal sequences
+// (rt_fastmath.h; the IEEE results whichever path the wave takes, so the bits
+// do not depend on the wave's other lanes).
+__device__ __forceinline__ Vec3 camera_dir(const FrameDev& F, int pxc, int pyc)
+{
+    const Vec3 d0 = make3((2 * pxc * F.inv_w - 1) * F.half_w, (2 * pyc * F.inv_h - 1) * F.half_h, -1.0f);
+    Mat4 M;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) M.m[i >> 2][i & 3] = F.orient[i];
+    const Vec3 dm = d0 * M;
+    const float len = sqrt_w(dm.x * dm.x + dm.y * dm.y + dm.z * dm.z);
+    return len > kEps ? dm * recip_w(len) : make3(0.f, 0.f, 0.f);
+}
+
+// Closest hit for camera rays from the tile's camera-buffer list (the wave
+// is the tile: full, rows aligned).  Planes and quadrics first (their hits
+// tighten the exit); then the list in cluster order, leaving once every
+// lane holds a hit nearer than the entry's key (no later entry can report a
+// nearer or equal hit: t >= dmin > best, as in the cluster early exit).
+__device__ __forceinline__ int closest_hit_camera_list(const SceneDev& S, int tile, const Vec3 O, const Vec3 D,
+                                                       float& best_t, Counters& cnt)
+{
+    float bt = -1.0f;
+    int bi = -1;
+    for (int k = 0; k < S.n_plane; ++k) {
+        const float4 a = S.plane[2 * k], b = S.plane[2 * k + 1];
+        float t;
+        ++cnt.pla;
+        const bool ok = hit_plane(make_float4(0.f, a.x, a.y, a.z), make_float4(a.w, 0.f, 0.f, 0.f), O, D, t);
+        take_min(ok, t, __float_as_int(b.x), bt, bi);
+    }
+    for (int k = 0; k < S.n_quad; ++k) {
+        const float4* r = S.quad + 3 * k;
+        const float4 a = r[0], b = r[1], c = r[2];
+        float t;
+        ++cnt.qua;
+        const bool ok = hit_quadric(make_float4(0.f, a.x, a.y, a.z), make_float4(a.w, b.x, b.y, b.z),
+                                    make_float4(b.w, c.x, c.y, 0.f), O, D, t);
+        take_min(ok, t, __float_as_int(c.z), bt, bi);
+    }
+    const unsigned e1 = S.cb_off[tile + 1];
+    for (unsigned e = S.cb_off[tile]; e < e1; ++e) {
+        const int2 en = S.cb_ent[e];
+        if (!__any((bi < 0) | !(bt < __int_as_float(en.y)))) break;
+        RT_EV(cnt, 2);
+        const float4* r = S.tricam + 4 * en.x;
+        camera_tri(r[0], r[1], r[2], r[3], D, bt, bi, cnt);
+    }
+    best_t = bt;
+    return bi;
+}
+
 // Primary rays: wave-culled when the whole wave is here, else per lane.
 // WAVE: 0 per lane only, 1 wave-level culling, 2 wave-level two-level
 // (clustered) culling.
+// tile >= 0: the wave is that camera-buffer tile (WAVE bit 8).
 template <int WAVE>
 __device__ __forceinline__ int closest_hit_primary(const SceneDev& S, const Vec3 O, const Vec3 D, float& t,
-                                                   Counters& cnt)
+                                                   Counters& cnt, int tile = -1)
 {
-    if (WAVE > 0 && wave_full()) {
+    if ((WAVE & 8) && tile >= 0 && wave_full()) return closest_hit_camera_list(S, tile, O, D, t, cnt);
+    if ((WAVE & 3) > 0 && wave_full()) {
         const WaveCone wc = wave_cone(D, true);
-        if (wc.ok) return closest_hit_camera_wave<WAVE == 2>(S, wc, O, D, t, cnt);
+        if (wc.ok) return closest_hit_camera_wave<(WAVE & 3) == 2>(S, wc, O, D, t, cnt);
     }
     return S.use_tricam ? closest_hit_camera(S, O, D, t, cnt) : closest_hit<true>(S, O, D, t, cnt);
 }
@@ -1129,6 +1194,87 @@ __global__ void rt_lb_dcap(const float4* __restrict__ cone, const float4* __rest
     const int k = perm[q];
     const float4 c0 = cone[2 * k], c1 = cone[2 * k + 1];
     lb_write(out + kLbEnt * (size_t)q, tri, k, c1.z == c1.z ? c1.z : -INFINITY);
+}
+
+// ---------------------------------------------------------- camera buffer
+// One wave per 8x8 tile of the full frame, laid out like rt_trace_kernel
+// (256-thread blocks of 2 x 2 tiles): the tile's 64 camera rays (camera_dir
+// on the same clamped pixels as the trace kernel, so the same bits), their
+// wave cone, and the camera wave test of every cluster / member
+// (cone_overlap, and the edge planes) — the culling closest_hit_camera_wave
+// runs per frame, done once per camera.  COUNT: cnt[tile] = survivors;
+// else the survivors {triangle, dmin} in cluster order from off[tile].
+template <bool FILL>
+__global__ __launch_bounds__(256) void rt_cb_build(const SceneDev S, const FrameDev F, const unsigned* __restrict__ off,
+                                                   unsigned* __restrict__ cnt, unsigned* __restrict__ flag,
+                                                   int2* __restrict__ ent)
+{
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int tx = blockIdx.x * 2 + (wave & 1), ty = blockIdx.y * 2 + (wave >> 1);
+    if (tx * 8 >= F.width || ty * 8 >= F.height) return;
+    const int tile = ty * S.cb_tiles_x + tx;
+    const int px = tx * 8 + (lane & 7), py = ty * 8 + (lane >> 3);
+    const Vec3 D = camera_dir(F, px < F.width ? px : F.width - 1, py < F.height ? py : F.height - 1);
+    const WaveCone wc = wave_cone(D, true);
+    if (!wc.ok) {  // no list: the trace kernel's per-wave path
+        if (!FILL && lane == 0) {
+            flag[tile] = 1u;
+            cnt[tile] = 0u;
+        }
+        return;
+    }
+    unsigned n = 0, base = FILL ? off[tile] : 0u;
+    const unsigned long long below = (1ull << lane) - 1ull;
+    auto batch = [&](int k0) {
+        const int k = k0 + lane;
+        bool reach = false;
+        float dmin = 0.0f;
+        if (k < S.n_tri) {
+            const float4 c0 = S.cone_cam[2 * k], c1 = S.cone_cam[2 * k + 1];
+            dmin = c1.x;
+            reach = cone_overlap(wc, c0, c1.w, 0.0f) && edges_open(wc, S.cone_cam + 2 * (size_t)S.n_tri + 3 * k, 0.0f);
+        }
+        const unsigned long long m = __ballot(reach);
+        if (FILL && reach) ent[base + n + (unsigned)__popcll(m & below)] = make_int2(k, __float_as_int(dmin));
+        n += (unsigned)__popcll(m);
+    };
+    if (S.n_clu > 0) {
+        for (int c0i = 0; c0i < S.n_clu; c0i += 64) {
+            const int cl = c0i + lane;
+            float4 q0 = make_float4(0.f, 0.f, 0.f, 1.f), q1 = make_float4(INFINITY, 0.f, 0.f, 0.f);
+            if (cl < S.n_clu) {
+                q0 = S.clu_cam[2 * cl];
+                q1 = S.clu_cam[2 * cl + 1];
+            }
+            const int id = __float_as_int(q1.y);
+            unsigned long long cm = __ballot(cone_overlap(wc, q0, q1.w, 0.0f, 4e-6f));
+            while (cm) {
+                const int b = (int)__builtin_ctzll(cm);
+                cm &= cm - 1;
+                batch(64 * __builtin_amdgcn_readlane(id, b));
+            }
+        }
+    } else {
+        for (int k0 = 0; k0 < S.n_tri; k0 += 64) batch(k0);
+    }
+    if (!FILL && lane == 0) {
+        cnt[tile] = n;
+        flag[tile] = 0u;
+    }
+}
+
+// Keys: entry e's key = min dmin over entries [e, end) of its tile (one
+// thread per tile), so a wave may stop at the first key beyond its hits.
+__global__ void rt_cb_keys(const unsigned* __restrict__ off, int ntiles, int2* __restrict__ ent)
+{
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ntiles) return;
+    float m = INFINITY;
+    for (unsigned e = off[t + 1]; e > off[t]; --e) {
+        const float d = __int_as_float(ent[e - 1].y);
+        m = d == d ? fminf(m, d) : -INFINITY;
+        ent[e - 1].y = __float_as_int(m);
+    }
 }
 
 // Shadow-ray cull predicate (L normalised towards the light, dist to it):
@@ -1842,7 +1988,7 @@ struct Refr {
 };
 
 template <int MAXD, int LB, int WAVE>
-__device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, Counters& cnt, bool live)
+__device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, Counters& cnt, bool live, int tile)
 {
     const Color bg{F.bg[0], F.bg[1], F.bg[2]};
     if constexpr (MAXD == 0) {
@@ -1851,7 +1997,7 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
 #endif
         float t;
         RT_MARK(cnt, 0);
-        const int idx = closest_hit_primary<(WAVE & 3)>(S, O, D, t, cnt);
+        const int idx = closest_hit_primary<(WAVE & 11)>(S, O, D, t, cnt, tile);
         RT_MARK(cnt, 1);
         // Lanes that miss (or lie outside the frame) stay in step through the
         // shading so the wave stays whole for wave-level shadow culling.
@@ -1886,7 +2032,8 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
         for (;;) {
             if (trace) {
                 float t;
-                const int idx = camera_ray ? closest_hit_primary<(WAVE & 3)>(S, O, D, t, cnt) : closest_hit<false>(S, O, D, t, cnt);
+                const int idx = camera_ray ? closest_hit_primary<(WAVE & 11)>(S, O, D, t, cnt, tile)
+                                           : closest_hit<false>(S, O, D, t, cnt);
                 camera_ray = false;
                 ret = bg;
                 if (idx >= 0) {
@@ -2010,19 +2157,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MAXD == 0 ?
     if (MAXD == 0 || valid) {
         const int pxc = px < F.width ? px : F.width - 1;
         const int pyc = py < rend ? py : rend - 1;
-        // Scene.cpp:1543-1552: (float)(2*PixX) * InvW - 1, then * HalfW
-        const Vec3 d0 = make3((2 * pxc * F.inv_w - 1) * F.half_w, (2 * pyc * F.inv_h - 1) * F.half_h, -1.0f);
-        Mat4 M;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) M.m[i >> 2][i & 3] = F.orient[i];
-        // Vecteur3.h Normaliser (rt_math.h normalize) with the exact fast
-        // sqrt / reciprocal sequences (rt_fastmath.h) when the wave is in range
-        const Vec3 dm = d0 * M;
-        const float len = sqrt_w(dm.x * dm.x + dm.y * dm.y + dm.z * dm.z);
-        const Vec3 D = len > kEps ? dm * recip_w(len) : make3(0.f, 0.f, 0.f);
+        const Vec3 D = camera_dir(F, pxc, pyc);
         const Vec3 O = make3(F.cam[0], F.cam[1], F.cam[2]);
         cnt.primary = valid ? 1u : 0u;
-        c = radiance<MAXD, LB, WAVE>(S, F, O, D, cnt, valid);
+        // camera-buffer tile: this wave's 8 rows must be one tile row of the
+        // full frame (the buffer's lists hold for its lanes' clamped pixels)
+        int tile = -1;
+        if ((WAVE & 8) && S.cb_tiles_x > 0 && (py0 & 7) == 0) {
+            tile = (py0 >> 3) * S.cb_tiles_x + (int)(blockIdx.x * 2 + (wave & 1));
+            if (S.cb_flag[tile]) tile = -1;
+        }
+        c = radiance<MAXD, LB, WAVE>(S, F, O, D, cnt, valid, tile);
         if (valid) {
             const size_t o = (size_t)ly * F.width + px;
             if (rgbf) {
@@ -2143,6 +2288,16 @@ struct rt_ctx {
     float4* d_clu_light = nullptr;
     int n_clu = 0;
     float4* d_uni = nullptr;  // union records (small lists): camera, then one per light
+    // camera buffer (rt_cb_build): per-tile lists for the camera of cb_key
+    unsigned* d_cb_off = nullptr;
+    unsigned* d_cb_flag = nullptr;
+    int2* d_cb_ent = nullptr;
+    size_t cb_cap = 0;          // entries allocated
+    int cb_tiles_x = 0, cb_ntiles = 0;
+    float cb_key[25] = {};      // cam_pos, orient, half_w, half_h, inv_w, inv_h, width, height (as float bits)
+    bool cb_valid = false;
+    double cb_build_ms = 0.0;
+    size_t cb_entries = 0;
     // light buffer (shadow cells), rt_lb_build
     unsigned* d_lb_off = nullptr;
     float4* d_lb_ent = nullptr;
@@ -2230,6 +2385,9 @@ RT_EXPORT void rt_destroy(rt_ctx* c)
     hipFree(c->d_lb_dcap);
     hipFree(c->d_lb_meta);
     hipFree(c->d_uni);
+    hipFree(c->d_cb_off);
+    hipFree(c->d_cb_flag);
+    hipFree(c->d_cb_ent);
     hipFree(c->d_stats);
     hipFree(c->d_scratch);
     if (c->ev0) hipEventDestroy(c->ev0);
@@ -2578,6 +2736,7 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
     c->lb_entries = 0;
     hipFree(c->d_uni);
     c->d_uni = nullptr;
+    c->cb_valid = false;  // buffers are kept (reallocated on demand)
     c->cam_valid = false;
     c->d_geom = c->d_mat = c->d_lights = c->d_tri = c->d_plane = c->d_quad = nullptr;
     c->d_translucent = nullptr;
@@ -2753,23 +2912,26 @@ typedef void (*kernel_fn)(const SceneDev, const FrameDev, unsigned*, float*, Sta
 #define RT_WAVE_LB 2
 #endif
 template <bool COUNT>
-static kernel_fn pick_kernel(int depth, int n_tri, int n_lights, bool lbuf, int& cap, int& lb)
+static kernel_fn pick_kernel(int depth, int n_tri, int n_lights, bool lbuf, bool cbuf, int& cap, int& lb)
 {
     lb = 1;
     if (depth == 0 && n_tri > 0 && lbuf) {  // light-buffer shadows, one light per pass
         cap = 0;
-        if (n_tri > kClusterMinTriangles) return (kernel_fn)&rt_trace_kernel<0, 1, 6, COUNT>;
-        return (kernel_fn)&rt_trace_kernel<0, 1, 5, COUNT>;
+        if (n_tri > kClusterMinTriangles)
+            return cbuf ? (kernel_fn)&rt_trace_kernel<0, 1, 14, COUNT> : (kernel_fn)&rt_trace_kernel<0, 1, 6, COUNT>;
+        return cbuf ? (kernel_fn)&rt_trace_kernel<0, 1, 13, COUNT> : (kernel_fn)&rt_trace_kernel<0, 1, 5, COUNT>;
     }
     if (depth == 0 && n_tri > kClusterMinTriangles) {
         cap = 0;
         lb = RT_WAVE_LB;
-        return (kernel_fn)&rt_trace_kernel<0, RT_WAVE_LB, 2, COUNT>;
+        return cbuf ? (kernel_fn)&rt_trace_kernel<0, RT_WAVE_LB, 10, COUNT>
+                    : (kernel_fn)&rt_trace_kernel<0, RT_WAVE_LB, 2, COUNT>;
     }
     if (depth == 0 && n_tri > 0) {
         cap = 0;
         lb = RT_WAVE_LB;
-        return (kernel_fn)&rt_trace_kernel<0, RT_WAVE_LB, 1, COUNT>;
+        return cbuf ? (kernel_fn)&rt_trace_kernel<0, RT_WAVE_LB, 9, COUNT>
+                    : (kernel_fn)&rt_trace_kernel<0, RT_WAVE_LB, 1, COUNT>;
     }
     if (depth == 0 && n_lights > 1) {
         cap = 0;
@@ -2794,37 +2956,28 @@ static int frame_rows(const rt_frame* f)
     return f->row_end - f->row_begin;
 }
 
-static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_dev, hipStream_t st, bool timed)
+// RT_AMD_CAMBUF (A/B switch): 0 = no camera buffer; unset/1 = for depth-0
+// scenes with triangles.
+static bool cb_mode()
 {
-    if (!c || !f) return RT_E_ARG;
-    if (!c->uploaded) {
-        c->err = "render before rt_upload_scene";
-        return RT_E_STATE;
-    }
-    if (f->width <= 0 || f->height <= 0 || f->row_begin < 0 || f->row_end > f->height ||
-        f->row_begin > f->row_end || f->max_bounces < 0 ||
-        (f->band_rows != 0 && rt_band_rows(f->height, f->band_rows, f->band_count, f->band_index) < 0)) {
-        c->err = "bad rt_frame geometry";
-        return RT_E_ARG;
-    }
-    const int depth = reachable_depth(c, f);
-    int cap = 0, lb = 1;
-    const int mode = lb_mode();
-    const bool lbuf = c->lb_ready && (mode == 1 || (mode == 2 && c->n_tri > kClusterMinTriangles));
-    kernel_fn k = (f->flags & RT_FLAG_STATS) ? pick_kernel<true>(depth, c->n_tri, c->n_lights, lbuf, cap, lb)
-                                              : pick_kernel<false>(depth, c->n_tri, c->n_lights, lbuf, cap, lb);
-    if (!k) {
-        c->err = "reachable bounce depth " + std::to_string(depth) + " exceeds the compiled stack (32)";
-        return RT_E_UNSUPPORTED;
-    }
-    const int use_tricam = c->n_tri > 0 && c->n_tri <= kTricamMaxTriangles;
-    SceneDev S{c->d_geom, c->d_mat, c->d_lights, c->d_tri, c->d_plane, c->d_quad, c->d_translucent, c->d_tricam,
-               use_tricam, c->n_tri <= kEdgeMaxTriangles, c->d_cone_cam, c->d_cone_light, c->d_clu_cam,
-               c->d_clu_light, c->n_clu, c->n_surf, c->n_lights, c->n_tri, c->n_plane, c->n_quad,
-               c->n_tri_opaque, c->n_plane_opaque, c->n_quad_opaque, c->n_translucent, c->shadow_split,
-               lbuf ? 1 : 0, c->d_lb_off, c->d_lb_ent, c->d_lb_dcap, c->d_lb_meta,
-               (c->d_uni && !getenv("RT_AMD_NO_UNION")) ? c->d_uni : nullptr};
-    FrameDev F;
+    const char* v = getenv("RT_AMD_CAMBUF");
+    return !(v && *v == '0');
+}
+
+static void cb_key_of(const rt_frame* f, float* key)
+{
+    std::memcpy(key, f->cam_pos, 3 * sizeof(float));
+    std::memcpy(key + 3, f->orient, 16 * sizeof(float));
+    key[19] = f->half_w;
+    key[20] = f->half_h;
+    key[21] = f->inv_w;
+    key[22] = f->inv_h;
+    std::memcpy(key + 23, &f->width, sizeof(int));
+    std::memcpy(key + 24, &f->height, sizeof(int));
+}
+
+static void frame_dev(const rt_frame* f, FrameDev& F)
+{
     std::memcpy(F.cam, f->cam_pos, sizeof F.cam);
     std::memcpy(F.orient, f->orient, sizeof F.orient);
     F.half_w = f->half_w;
@@ -2843,40 +2996,164 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
     F.band_rows = f->band_rows;
     F.band_count = f->band_count;
     F.band_index = f->band_index;
+}
+
+// Per-camera prepasses (when the camera position moved): camera-ray
+// triangle values, camera cone records, union / cluster records.
+static int camera_prepass(rt_ctx* c, const rt_frame* f, hipStream_t st, bool all_tricam)
+{
+    if (c->n_tri <= 0 || (c->cam_valid && std::memcmp(c->cam_key, f->cam_pos, sizeof c->cam_key) == 0)) return RT_OK;
+    const float* cp = f->cam_pos;
+    if (all_tricam || c->n_tri <= kTricamMaxTriangles) {
+        hipLaunchKernelGGL(rt_camera_prepass, dim3((c->n_tri + 255) / 256), dim3(256), 0, st, c->d_tri, c->n_tri,
+                           cp[0], cp[1], cp[2], c->d_tricam);
+        HIP_TRY(c, hipGetLastError());
+    }
+    hipLaunchKernelGGL(rt_cone_prepass, dim3((c->n_tri + 255) / 256), dim3(256), 0, st, c->d_tri, c->d_trisph,
+                       c->d_trinrm, c->d_tricoef, c->n_tri, cp[0], cp[1], cp[2], 1, 0.0f, c->d_cone_cam);
+    HIP_TRY(c, hipGetLastError());
+    if (c->d_uni) {
+        hipLaunchKernelGGL(rt_cluster_prepass, dim3(1), dim3(64), 0, st, c->d_cone_cam, c->n_tri, 1, c->d_uni,
+                           c->n_tri);
+        HIP_TRY(c, hipGetLastError());
+    }
+    if (c->n_clu > 0) {
+        float4* tmp = c->d_clu_cam + 2 * (size_t)c->n_clu;  // second half: unsorted
+        hipLaunchKernelGGL(rt_cluster_prepass, dim3((unsigned)((c->n_clu + 63) / 64)), dim3(64), 0, st,
+                           c->d_cone_cam, c->n_tri, c->n_clu, tmp);
+        HIP_TRY(c, hipGetLastError());
+        hipLaunchKernelGGL(rt_cluster_sort, dim3((unsigned)((c->n_clu + 255) / 256)), dim3(256), 0, st, tmp,
+                           c->n_clu, c->d_clu_cam);
+        HIP_TRY(c, hipGetLastError());
+    }
+    std::memcpy(c->cam_key, f->cam_pos, sizeof c->cam_key);
+    c->cam_valid = true;
+    c->cb_valid = false;
+    return RT_OK;
+}
+
+static SceneDev scene_dev(rt_ctx* c, bool lbuf, bool cbuf)
+{
+    const int use_tricam = c->n_tri > 0 && c->n_tri <= kTricamMaxTriangles;
+    return SceneDev{c->d_geom, c->d_mat, c->d_lights, c->d_tri, c->d_plane, c->d_quad, c->d_translucent, c->d_tricam,
+                    use_tricam, c->n_tri <= kEdgeMaxTriangles, c->d_cone_cam, c->d_cone_light, c->d_clu_cam,
+                    c->d_clu_light, c->n_clu, c->n_surf, c->n_lights, c->n_tri, c->n_plane, c->n_quad,
+                    c->n_tri_opaque, c->n_plane_opaque, c->n_quad_opaque, c->n_translucent, c->shadow_split,
+                    lbuf ? 1 : 0, c->d_lb_off, c->d_lb_ent, c->d_lb_dcap, c->d_lb_meta,
+                    (c->d_uni && !getenv("RT_AMD_NO_UNION")) ? c->d_uni : nullptr,
+                    c->d_cb_off, c->d_cb_ent, c->d_cb_flag, cbuf ? c->cb_tiles_x : 0};
+}
+
+// Camera buffer for the frame's camera (synchronous: the list sizes come
+// back to the host for the offsets).  Needs the camera prepass done.
+static int cb_build(rt_ctx* c, const rt_frame* f, hipStream_t st)
+{
+    const auto t0 = std::chrono::steady_clock::now();
+    const int tx = (f->width + 7) / 8, ty = (f->height + 7) / 8, nt = tx * ty;
+    if (nt > c->cb_ntiles || !c->d_cb_off) {
+        hipFree(c->d_cb_off);
+        hipFree(c->d_cb_flag);
+        c->d_cb_off = nullptr;
+        c->d_cb_flag = nullptr;
+        HIP_TRY(c, hipMalloc(&c->d_cb_off, (size_t)(nt + 1) * sizeof(unsigned)));
+        HIP_TRY(c, hipMalloc(&c->d_cb_flag, (size_t)std::max(nt, 1) * sizeof(unsigned)));
+        c->cb_ntiles = nt;
+    }
+    c->cb_tiles_x = tx;
+    SceneDev S = scene_dev(c, false, true);
+    FrameDev F;
+    frame_dev(f, F);
+    dim3 grid((tx + 1) / 2, (ty + 1) / 2);
+    unsigned* cnt = c->d_cb_off + 1;  // counts land one slot up, scanned in place on the host
+    hipLaunchKernelGGL(rt_cb_build<false>, grid, dim3(256), 0, st, S, F, (const unsigned*)nullptr, cnt, c->d_cb_flag,
+                       (int2*)nullptr);
+    HIP_TRY(c, hipGetLastError());
+    std::vector<unsigned> off((size_t)nt + 1, 0u);
+    HIP_TRY(c, hipMemcpyAsync(off.data() + 1, cnt, (size_t)nt * sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    HIP_TRY(c, hipStreamSynchronize(st));
+    size_t run = 0;
+    for (int t = 0; t < nt; ++t) {
+        run += off[t + 1];
+        if (run > 0xFFFFFFF0ull) {
+            c->err = "camera buffer too large";
+            return RT_E_UNSUPPORTED;
+        }
+        off[t + 1] = (unsigned)run;
+    }
+    if (run > c->cb_cap || !c->d_cb_ent) {
+        hipFree(c->d_cb_ent);
+        c->d_cb_ent = nullptr;
+        HIP_TRY(c, hipMalloc(&c->d_cb_ent, std::max<size_t>(run, 1) * sizeof(int2)));
+        c->cb_cap = std::max<size_t>(run, 1);
+    }
+    HIP_TRY(c, hipMemcpyAsync(c->d_cb_off, off.data(), off.size() * sizeof(unsigned), hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(rt_cb_build<true>, grid, dim3(256), 0, st, S, F, (const unsigned*)c->d_cb_off, (unsigned*)nullptr,
+                       c->d_cb_flag, c->d_cb_ent);
+    HIP_TRY(c, hipGetLastError());
+    hipLaunchKernelGGL(rt_cb_keys, dim3((nt + 255) / 256), dim3(256), 0, st, (const unsigned*)c->d_cb_off, nt,
+                       c->d_cb_ent);
+    HIP_TRY(c, hipGetLastError());
+    HIP_TRY(c, hipStreamSynchronize(st));  // off[] (host) must outlive the copy
+    cb_key_of(f, c->cb_key);
+    c->cb_valid = true;
+    c->cb_entries = run;
+    c->cb_build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return RT_OK;
+}
+
+static bool cb_matches(const rt_ctx* c, const rt_frame* f)
+{
+    if (!c->cb_valid) return false;
+    float key[25];
+    cb_key_of(f, key);
+    return std::memcmp(key, c->cb_key, sizeof key) == 0;
+}
+
+// allow_build: synchronous renders may (re)build the camera buffer; the
+// async path (no host sync, capturable) uses it only when it is current.
+static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_dev, hipStream_t st, bool timed,
+                  bool allow_build = false)
+{
+    if (!c || !f) return RT_E_ARG;
+    if (!c->uploaded) {
+        c->err = "render before rt_upload_scene";
+        return RT_E_STATE;
+    }
+    if (f->width <= 0 || f->height <= 0 || f->row_begin < 0 || f->row_end > f->height ||
+        f->row_begin > f->row_end || f->max_bounces < 0 ||
+        (f->band_rows != 0 && rt_band_rows(f->height, f->band_rows, f->band_count, f->band_index) < 0)) {
+        c->err = "bad rt_frame geometry";
+        return RT_E_ARG;
+    }
+    const int depth = reachable_depth(c, f);
+    int cap = 0, lb = 1;
+    const int mode = lb_mode();
+    const bool lbuf = c->lb_ready && (mode == 1 || (mode == 2 && c->n_tri > kClusterMinTriangles));
+    const bool cb_want = depth == 0 && c->n_tri > 0 && cb_mode();
     const int rows = frame_rows(f);
+    if (rows > 0) {
+        const int rc = camera_prepass(c, f, st, cb_want);
+        if (rc) return rc;
+        if (cb_want && allow_build && !cb_matches(c, f)) {
+            const int rc2 = cb_build(c, f, st);
+            if (rc2) return rc2;
+        }
+    }
+    const bool cbuf = cb_want && cb_matches(c, f);
+    kernel_fn k = (f->flags & RT_FLAG_STATS) ? pick_kernel<true>(depth, c->n_tri, c->n_lights, lbuf, cbuf, cap, lb)
+                                              : pick_kernel<false>(depth, c->n_tri, c->n_lights, lbuf, cbuf, cap, lb);
+    if (!k) {
+        c->err = "reachable bounce depth " + std::to_string(depth) + " exceeds the compiled stack (32)";
+        return RT_E_UNSUPPORTED;
+    }
+    SceneDev S = scene_dev(c, lbuf, cbuf);
+    FrameDev F;
+    frame_dev(f, F);
     c->last = rt_stats{};
     c->last.stack_depth = cap;
     c->last.light_batch = lb;
     if (rows == 0) return RT_OK;
     if (f->flags & RT_FLAG_STATS) HIP_TRY(c, hipMemsetAsync(c->d_stats, 0, kStatSlots * sizeof(StatsDev), st));
-    // Camera-ray triangle values: recomputed only when the camera moves.
-    if (c->n_tri > 0 && (!c->cam_valid || std::memcmp(c->cam_key, f->cam_pos, sizeof c->cam_key) != 0)) {
-        const float* cp = f->cam_pos;
-        if (use_tricam) {
-            hipLaunchKernelGGL(rt_camera_prepass, dim3((c->n_tri + 255) / 256), dim3(256), 0, st, c->d_tri, c->n_tri,
-                               cp[0], cp[1], cp[2], c->d_tricam);
-            HIP_TRY(c, hipGetLastError());
-        }
-        hipLaunchKernelGGL(rt_cone_prepass, dim3((c->n_tri + 255) / 256), dim3(256), 0, st, c->d_tri, c->d_trisph,
-                           c->d_trinrm, c->d_tricoef, c->n_tri, cp[0], cp[1], cp[2], 1, 0.0f, c->d_cone_cam);
-        HIP_TRY(c, hipGetLastError());
-        if (c->d_uni) {
-            hipLaunchKernelGGL(rt_cluster_prepass, dim3(1), dim3(64), 0, st, c->d_cone_cam, c->n_tri, 1, c->d_uni,
-                               c->n_tri);
-            HIP_TRY(c, hipGetLastError());
-        }
-        if (c->n_clu > 0) {
-            float4* tmp = c->d_clu_cam + 2 * (size_t)c->n_clu;  // second half: unsorted
-            hipLaunchKernelGGL(rt_cluster_prepass, dim3((unsigned)((c->n_clu + 63) / 64)), dim3(64), 0, st,
-                               c->d_cone_cam, c->n_tri, c->n_clu, tmp);
-            HIP_TRY(c, hipGetLastError());
-            hipLaunchKernelGGL(rt_cluster_sort, dim3((unsigned)((c->n_clu + 255) / 256)), dim3(256), 0, st, tmp,
-                               c->n_clu, c->d_clu_cam);
-            HIP_TRY(c, hipGetLastError());
-        }
-        std::memcpy(c->cam_key, f->cam_pos, sizeof c->cam_key);
-        c->cam_valid = true;
-    }
     dim3 grid((f->width + 15) / 16, (rows + 15) / 16);
     if (timed) HIP_TRY(c, hipEventRecord(c->ev0, st));
     StatsDev* stats = c->d_stats;
@@ -2952,7 +3229,8 @@ static int render_sync(rt_ctx* c, const rt_frame* f, void* out, bool as_float)
         if (rc) return rc;
         target = c->d_scratch;
     }
-    int rc = launch(c, f, as_float ? nullptr : (unsigned*)target, as_float ? (float*)target : nullptr, c->stream, true);
+    int rc = launch(c, f, as_float ? nullptr : (unsigned*)target, as_float ? (float*)target : nullptr, c->stream, true,
+                    true);
     if (rc) return rc;
     if (!dev && bytes) HIP_TRY(c, hipMemcpyAsync(out, target, bytes, hipMemcpyDeviceToHost, c->stream));
     return finish_sync(c, f, c->stream, true);
@@ -3026,6 +3304,18 @@ RT_EXPORT int rt_debug_lb_info(rt_ctx* c, double* out, int n)
         out[4 + 3 * j] = nd;
         out[5 + 3 * j] = meta[2 * j + 1].x;
     }
+    return RT_OK;
+}
+
+// Diagnostic (not in include/rt.h): camera-buffer summary: out[0] = current
+// (0/1), out[1] = entries, out[2] = last build ms, out[3] = tiles.
+RT_EXPORT int rt_debug_cb_info(rt_ctx* c, double* out, int n)
+{
+    if (!c || !out || n < 4) return RT_E_ARG;
+    out[0] = c->cb_valid ? 1.0 : 0.0;
+    out[1] = (double)c->cb_entries;
+    out[2] = c->cb_build_ms;
+    out[3] = (double)c->cb_ntiles;
     return RT_OK;
 }
 

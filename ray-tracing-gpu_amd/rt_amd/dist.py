@@ -23,10 +23,13 @@ from typing import List, Optional, Tuple
 
 
 def slab_rows(height: int, world: int, rank: int) -> Tuple[int, int, int]:
-    """(row_begin, row_end, padded_rows) of `rank`'s slab; row 0 = bottom."""
+    """(row_begin, row_end, padded_rows) of `rank`'s slab; row 0 = bottom.
+    Slab heights are multiples of 8 rows (the last slab takes the rest)."""
     if world <= 0 or not 0 <= rank < world:
         raise ValueError("bad world/rank")
-    rows = -(-height // world)
+    # heights in whole 8-row tiles, so every wave covers one tile row of the
+    # frame (the camera buffer's unit)
+    rows = -(-(-(-height // world)) // 8) * 8
     r0 = min(height, rank * rows)
     r1 = min(height, (rank + 1) * rows)
     return r0, r1, rows
