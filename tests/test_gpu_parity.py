@@ -171,6 +171,37 @@ def test_bad_band_layout_rejected(ctx):
             ctx.render(f)
 
 
+def test_camera_buffer_follows_the_camera(monkeypatch):
+    """The camera buffer (per-tile lists, built per camera by synchronous
+    renders) must never serve a stale camera: after the camera moves, the
+    async path renders without it until a synchronous render rebuilds it —
+    every image bit-identical to a context that never had one."""
+    torch = pytest.importorskip("torch")
+    s = rt_amd.Scene(scene(2), 160, 120, 0)
+    frames = []
+    for dx in (0.0, 7.5, -12.25):
+        f = s.frame.copy()
+        f.cam_pos[0] += dx
+        frames.append(f)
+    monkeypatch.setenv("RT_AMD_CAMBUF", "0")
+    ref = rt_amd.Context(0)
+    ref.upload(s)
+    want = [ref.render_float(f) for f in frames]
+    monkeypatch.delenv("RT_AMD_CAMBUF")
+    c = rt_amd.Context(0)
+    c.upload(s)
+    out = torch.zeros((120, 160, 3), dtype=torch.float32, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    for k, (f, w) in enumerate(zip(frames, want)):
+        c.render_async(f, 0, out.data_ptr(), stream)  # stale (or no) buffer: not used
+        torch.cuda.synchronize()
+        assert bits_equal(out.cpu().numpy(), w), k
+        assert bits_equal(c.render_float(f), w), k  # rebuilt for this camera
+        c.render_async(f, 0, out.data_ptr(), stream)  # current: used
+        torch.cuda.synchronize()
+        assert bits_equal(out.cpu().numpy(), w), k
+
+
 def test_async_device_outputs(ctx):
     torch = pytest.importorskip("torch")
     s = rt_amd.Scene(scene(6), 128, 96, 3)
