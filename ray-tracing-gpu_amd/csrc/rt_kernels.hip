@@ -2905,11 +2905,12 @@ typedef void (*kernel_fn)(const SceneDev, const FrameDev, unsigned*, float*, Sta
 
 // Kernel variants (tools/ab_variants.py, MI355X).  Without bounces and with
 // triangles: wave-level culling (two-level above kClusterMinTriangles),
-// RT_WAVE_LB lights per shadow pass (2: best of 1-3 on C2 and C3).  Without
+// RT_WAVE_LB lights per shadow pass (1: with the camera buffer and the union
+// pre-test, C2 -5.3% and C4 -6.9% against 2; 3 is 50% slower).  Without
 // triangles nothing is culled: light batches of 3.  Bounce kernels:
 // per-lane culling, one light per pass (LB 3 regressed scene7 by 4%).
 #ifndef RT_WAVE_LB
-#define RT_WAVE_LB 2
+#define RT_WAVE_LB 1
 #endif
 template <bool COUNT>
 static kernel_fn pick_kernel(int depth, int n_tri, int n_lights, bool lbuf, bool cbuf, int& cap, int& lb)
