@@ -1531,15 +1531,23 @@ __device__ __forceinline__ void shadow_wave_batch(const SceneDev& S, const float
 {
     const int k = k0 + (int)(threadIdx.x & 63);
     // every record load of the batch first (one wait), then the tests
-    float4 c0[kLightBatch], c1[kLightBatch];
+    float4 c0[kLightBatch], c1[kLightBatch], ed[kLightBatch][3];
+    const bool edges = RT_EDGES && S.use_edges;
 #pragma unroll
     for (int j = 0; j < kLightBatch; ++j) {
         c0[j] = make_float4(0.f, 0.f, 0.f, 1.f);
         c1[j] = make_float4(INFINITY, 0.f, INFINITY, 0.f);  // no reach
+        for (int q = 0; q < 3; ++q) ed[j][q] = make_float4(0.f, 0.f, 0.f, -4.0f);  // open
         if (((lights >> j) & 1u) && k < S.n_tri_opaque) {
             const float4* rec = cone + cstride * j + 2 * k;
             c0[j] = rec[0];
             c1[j] = rec[1];
+            if (edges) {  // with the sphere records: one memory round trip
+                const float4* er = cone + cstride * j + 2 * (size_t)S.n_tri + 3 * k;
+                ed[j][0] = er[0];
+                ed[j][1] = er[1];
+                ed[j][2] = er[2];
+            }
         }
     }
     RT_EV(cnt, 4);
@@ -1550,9 +1558,7 @@ __device__ __forceinline__ void shadow_wave_batch(const SceneDev& S, const float
         if (((lights >> j) & 1u) && wc[j].ok) {
             const float ang = dmax[j] * 1e-6f * c1[j].y;
             bool reach = (c1[j].x < dmax[j]) & cone_overlap(wc[j], c0[j], c1[j].w, ang);
-            // edge records only for sphere survivors
-            if (RT_EDGES && S.use_edges && reach)
-                reach = edges_open(wc[j], cone + cstride * j + 2 * (size_t)S.n_tri + 3 * k, ang);
+            if (edges) reach &= edges_open(wc[j], ed[j], ang);
             reach |= dmax[j] > c1[j].z;
             mj[j] = __ballot(reach);
             m |= mj[j];
