@@ -57,6 +57,10 @@ def main():
         ctx = ctypes.c_void_p()
         assert L.rt_create(0, ctypes.byref(ctx)) == 0
         assert L.rt_upload_scene(ctx, ctypes.byref(flat)) == 0
+        # one synchronous render first: it builds what is built per camera
+        # (the camera buffer) exactly as bench.py's counted render does
+        host = (ctypes.c_uint8 * (W * H * 4))()
+        assert L.rt_render(ctx, ctypes.byref(fr), host) == 0
         L.rt_render_async(ctx, ctypes.byref(fr), out.data_ptr(), None, None)
         torch.cuda.synchronize()
         img = out.clone()
