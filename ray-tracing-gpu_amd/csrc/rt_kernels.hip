@@ -796,6 +796,45 @@ __global__ void rt_camera_prepass(const float4* __restrict__ tri, int n, float c
 // up to m, at distance >= s_min = dv - r - m from A: the direction d from A
 // has d . n_e >= -m / s_min =: lim for all three edges.  A wave whose cone
 // has max d . n_e < lim for some edge reaches no point of the triangle.
+// Distance from point a to the triangle (v0, v1, v2), in double (closest
+// point by the triangle's Voronoi regions).
+__device__ double point_triangle_dist(const double* a, const double (*v)[3])
+{
+    double ab[3], ac[3], ap[3], cl[3];
+    for (int i = 0; i < 3; ++i) {
+        ab[i] = v[1][i] - v[0][i];
+        ac[i] = v[2][i] - v[0][i];
+        ap[i] = a[i] - v[0][i];
+    }
+    auto dot3 = [](const double* x, const double* y) { return x[0] * y[0] + x[1] * y[1] + x[2] * y[2]; };
+    auto at = [&](double s, double t) {
+        for (int i = 0; i < 3; ++i) cl[i] = v[0][i] + s * ab[i] + t * ac[i];
+    };
+    const double d1 = dot3(ab, ap), d2 = dot3(ac, ap);
+    double bp[3], cp[3];
+    for (int i = 0; i < 3; ++i) {
+        bp[i] = a[i] - v[1][i];
+        cp[i] = a[i] - v[2][i];
+    }
+    const double d3 = dot3(ab, bp), d4 = dot3(ac, bp), d5 = dot3(ab, cp), d6 = dot3(ac, cp);
+    const double va = d3 * d6 - d5 * d4, vb = d5 * d2 - d1 * d6, vc = d1 * d4 - d3 * d2;
+    if (d1 <= 0 && d2 <= 0) at(0, 0);
+    else if (d3 >= 0 && d4 <= d3) at(1, 0);
+    else if (vc <= 0 && d1 >= 0 && d3 <= 0) at(d1 / (d1 - d3), 0);
+    else if (d6 >= 0 && d5 <= d6) at(0, 1);
+    else if (vb <= 0 && d2 >= 0 && d6 <= 0) at(0, d2 / (d2 - d6));
+    else if (va <= 0 && (d4 - d3) >= 0 && (d5 - d6) >= 0) {
+        const double w = (d4 - d3) / ((d4 - d3) + (d5 - d6));
+        for (int i = 0; i < 3; ++i) cl[i] = v[1][i] + w * (v[2][i] - v[1][i]);
+    } else {
+        const double den = 1.0 / (va + vb + vc);
+        at(vb * den, vc * den);
+    }
+    double q = 0;
+    for (int i = 0; i < 3; ++i) q += (a[i] - cl[i]) * (a[i] - cl[i]);
+    return sqrt(q);
+}
+
 __global__ void rt_cone_prepass(const float4* __restrict__ tri, const float4* __restrict__ sph,
                                 const float4* __restrict__ nrm, const float4* __restrict__ coef, int n, float ax,
                                 float ay, float az, int camera, float dtarget, float4* __restrict__ out)
@@ -820,6 +859,20 @@ __global__ void rt_cone_prepass(const float4* __restrict__ tri, const float4* __
     float4 c0 = make_float4(0.f, 0.f, 0.f, -2.0f);
     float4 c1 = make_float4(-INFINITY, 0.f, -INFINITY, 2.0f);
     bool never = false;
+    // dmin: a reported hit's plane crossing X lies within m of the triangle
+    // and its t within m/3 of X's, so no hit is reported nearer the apex than
+    // (nearest point of the triangle) - 4m/3.  The triangle's own nearest
+    // point (>= the sphere's, dv - r0), less the cone's 2e-5 dv rounding slack.
+    double dnear = dv - r0;
+    {
+        const float4 t1 = tri[3 * k + 1], t2 = tri[3 * k + 2];
+        const double Vt[3][3] = {{p0.x, p0.y, p0.z},
+                                 {(double)p0.x + p0.w, (double)p0.y + t1.x, (double)p0.z + t1.y},
+                                 {(double)p0.x + t1.z, (double)p0.y + t1.w, (double)p0.z + t2.x}};
+        const double Ap[3] = {ax, ay, az};
+        const double dt = point_triangle_dist(Ap, Vt);
+        if (dt == dt) dnear = fmax(dnear, dt * (1.0 - 1e-9));
+    }
     // m <= 10 r: wider cones cost more than the pairs they would cull
     // (a wide member cone widens its cluster's cone and floods light-buffer
     // cells; measured with m <= dv/2 for lights: C3 +7%, C5 +4%)
@@ -836,12 +889,12 @@ __global__ void rt_cone_prepass(const float4* __restrict__ tri, const float4* __
             if (h_eff >= (gS * (dv + r0) + gL) * phi) {
                 // dmin: no reported hit of this triangle has t < dmin (the
                 // near-regime t error is <= m/3) — the closest-hit early exit
-                const double dmin = (dv - rc - m / 3.0) * (1.0 - 1e-5);
+                const double dmin = (dnear - 4.0 * m / 3.0 - 2e-5 * dv) * (1.0 - 1e-5);
                 c0 = cone;
                 c1 = make_float4((float)dmin, 0.f, 0.f, sinT);
             }
         } else {
-            const double dmin = (dv - rc - m / 3.0) * (1.0 - 1e-5);
+            const double dmin = (dnear - 4.0 * m / 3.0 - 2e-5 * dv) * (1.0 - 1e-5);
             const double dcap1 = ((h_eff / phi - gL) / gS - dv - r0) / 1.0001;
             const double rhoN = fmin(m / (3.0 * L), rho_cap);  // rho where well conditioned
             const double dcap2 =
