@@ -136,15 +136,21 @@ typedef struct rt_ctx rt_ctx;
 int rt_create(int32_t hip_device, rt_ctx** out);
 int rt_upload_scene(rt_ctx*, const rt_scene_flat*);
 /* Synchronous.  rgba8_out: host or device pointer to
- * (row_end-row_begin)*width*4 bytes, RGBA8 = GL float->unorm8 of the RGB
- * (clamp to [0,1], round to nearest, alpha 255). */
+ * (row_end-row_begin)*width*4 bytes (or rt_band_rows(...) rows for bands),
+ * RGBA8 = GL float->unorm8 of the RGB (clamp to [0,1], round to nearest,
+ * alpha 255).  The synchronous renders also (re)build what is kept per
+ * camera — the camera buffer of per-tile triangle lists — when the camera
+ * (position, orientation, resolution) changed since the last build. */
 int rt_render(rt_ctx*, const rt_frame*, uint8_t* rgba8_out);
 /* Parity/debug: float RGB exactly as m_InfoPixel (unclamped), 3 floats/px. */
 int rt_render_float(rt_ctx*, const rt_frame*, float* rgb_out);
 /* Asynchronous, device pointers only, enqueued on `hip_stream` (a hipStream_t;
  * NULL = the HIP null stream, as in every HIP API).  Either output may be
  * NULL.  No host sync, no allocation: safe to capture in a hipGraph or to
- * enqueue ahead of an RCCL collective on the same stream. */
+ * enqueue ahead of an RCCL collective on the same stream.  It uses the
+ * camera buffer only when it is current for the frame's camera (never
+ * builds it): one synchronous render after a camera change makes the
+ * following async renders take the fast path.  Same image either way. */
 int rt_render_async(rt_ctx*, const rt_frame*, uint8_t* rgba8_dev, float* rgb_dev, void* hip_stream);
 int rt_last_stats(rt_ctx*, rt_stats* out);
 const char* rt_last_error(rt_ctx*);
