@@ -2534,12 +2534,15 @@ static void cluster_order(std::vector<float>& tri, int n_opaque)
 }
 
 // RT_AMD_LIGHTBUF (diagnostic/A-B switch): 0 = never build or use the light
-// buffer, 1 = use it for every depth-0 scene with triangles; unset = for
-// lists above kClusterMinTriangles.  RT_AMD_LB_SCALE scales the cell count.
+// buffer (wave-level shadow culling), 2 = only for lists above
+// kClusterMinTriangles; unset/1 = every depth-0 scene with opaque
+// triangles (same-box A/B since the exact dmin and the camera buffer: C1
+// -8%, C2 -6%, C4 -6% against the wave path).  RT_AMD_LB_SCALE scales the
+// cell count.
 static int lb_mode()
 {
     const char* v = getenv("RT_AMD_LIGHTBUF");
-    if (!v || !*v) return 2;
+    if (!v || !*v) return 1;
     return atoi(v);
 }
 
