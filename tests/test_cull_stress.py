@@ -84,11 +84,10 @@ def test_gpu_matches_oracle_random_views(oracle, tmp_path, seed):
 
 
 
-# The light buffer (shadow cells, rt_kernels.hip shadow_opaque_lb) forced on
-# for every case above, whatever the list size (the driver's default only
-# builds it past 1,024 triangles), and at cell resolutions from coarse to
-# fine (RT_AMD_LB_SCALE: R from 16 up to the 1,024 cap), so cell borders,
-# face edges and the dcap list all meet the stress geometry.
+# The light buffer (shadow cells, rt_kernels.hip shadow_opaque_lb) at cell
+# resolutions from coarse to fine (RT_AMD_LB_SCALE: R from 16 up to the
+# 1,024 cap), so cell borders, face edges and the per-light list all meet
+# the stress geometry.
 @pytest.fixture
 def lightbuf(monkeypatch):
     def on(scale=None):
@@ -128,3 +127,18 @@ def test_gpu_lightbuf_random_views(oracle, lightbuf, tmp_path, seed, scale):
     want = oracle.render(path, w, h, 0)
     bad = np.argwhere(~(got.view(np.uint32) == want.view(np.uint32)).all(-1))
     assert bits_equal(got, want), f"{len(bad)} pixels differ, first {bad[:5].tolist()}"
+
+
+# The wave-level shadow culling (the path with the light buffer switched
+# off: RT_AMD_LIGHTBUF=0), which the default no longer takes for these
+# scenes, against the same reference goldens.
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,seed,w,h,depth", [c for c in CASES if c[4] == 0])
+def test_gpu_wave_culling_matches_reference(cull_golden, monkeypatch, tmp_path, name, seed, w, h, depth):
+    import rt_amd
+
+    monkeypatch.setenv("RT_AMD_LIGHTBUF", "0")
+    ctx = rt_amd.Context(0)
+    s = rt_amd.Scene(_path(tmp_path, seed, depth), w, h, depth)
+    ctx.upload(s)
+    assert bits_equal(ctx.render_float(s.frame), cull_golden[name])
