@@ -562,8 +562,13 @@ static int lb_build(rt_ctx* c, int ntr, int n_opaque, int nl, const std::vector<
 {
     const auto t0 = std::chrono::steady_clock::now();
     const char* sc = getenv("RT_AMD_LB_SCALE");
-    // cells of ~1/4 the median cone radius: best of 0.5-6 on C3 and C5
-    const double scale = sc && *sc ? atof(sc) : 4.0;
+    // cells of ~1/4 the median cone radius: best of 1-8 on C3 and C5; and
+    // no coarser than 128 cells per face edge (small scenes: C2 -3.3%, C4
+    // -2.5% against their 16-48, flat from 192 to 512).  An explicit
+    // RT_AMD_LB_SCALE (A/B, the stress tests' coarse cells) sets R alone.
+    const bool scale_set = sc && *sc;
+    const double scale = scale_set ? atof(sc) : 4.0;
+    const int r_min = scale_set ? kLbGroup : 128;
     struct Build {
         int R = 16;
         std::vector<int> dperm;
@@ -603,7 +608,7 @@ static int lb_build(rt_ctx* c, int ntr, int n_opaque, int nl, const std::vector<
                 std::nth_element(T.begin(), T.begin() + T.size() / 2, T.end());
                 const double med = std::max(T[T.size() / 2], 1e-4);
                 b.R = (int)std::lround(scale / (kLbGroup * med)) * kLbGroup;
-                b.R = std::min(1024, std::max(kLbGroup, b.R));
+                b.R = std::min(1024, std::max(r_min, b.R));
             }
             std::sort(perm.begin(), perm.end(), [&](int x, int y) {
                 return h[2 * x + 1].x < h[2 * y + 1].x || (h[2 * x + 1].x == h[2 * y + 1].x && x < y);

@@ -3,6 +3,10 @@
 RTLD_LOCAL so their identical symbol names do not collide.
 
     python tools/ab_variants.py --config c2 lib/var/librt_amd_base.so lib/var/librt_amd_nosl.so ...
+
+A variant may carry environment settings for its upload and first
+(synchronous) render, e.g. lib/librt_amd.so@RT_AMD_LB_SCALE=2 (several:
+@A=1,B=2); they are restored afterwards.
 """
 import argparse
 import ctypes
@@ -43,7 +47,11 @@ def main():
     out = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
     ref = None
     vs = []
-    for lp in a.libs:
+    for spec in a.libs:
+        lp, _, envs = spec.partition("@")
+        env = dict(kv.split("=", 1) for kv in envs.split(",") if kv)
+        saved = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
         L = load(lp)
         sc = ctypes.c_void_p()
         assert L.rt_scene_create(ctypes.byref(sc)) == 0
@@ -64,9 +72,14 @@ def main():
         L.rt_render_async(ctx, ctypes.byref(fr), out.data_ptr(), None, None)
         torch.cuda.synchronize()
         img = out.clone()
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
         same = True if ref is None else bool(torch.equal(img, ref))
         ref = img if ref is None else ref
-        vs.append(dict(lib=os.path.basename(lp), L=L, ctx=ctx, fr=fr, sc=sc, times=[], same_as_first=same))
+        vs.append(dict(lib=os.path.basename(lp) + ("@" + envs if envs else ""), L=L, ctx=ctx, fr=fr, sc=sc, times=[], same_as_first=same))
     for _ in range(a.rounds):
         for v in vs:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

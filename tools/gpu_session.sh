@@ -25,6 +25,7 @@ for s in $STEPS; do
     bench) run bench 400 python bench.py ;;
     bench_all)
       for c in c1 c2 c3 c4 c4s7 c4s9 c5; do run bench_$c 400 python bench.py --config $c --steps 10 --cpu-seconds 5; done ;;
+    bench_one) run bench_${CONFIG:-c2} 400 python bench.py --config ${CONFIG:-c2} --steps 20 --no-cpu-baseline ;;
     listpmc) run list_counters 120 rocprofv3 -L ;;
     pmc)
       B="python bench.py --steps 5 --warmup 1 --no-cpu-baseline --config ${CONFIG:-c2}"
@@ -35,6 +36,7 @@ for s in $STEPS; do
       python tools/pmc_summary.py gpurun_out/pmc_${CONFIG:-c2} > gpurun_out/pmc_${CONFIG:-c2}/summary.json
       ;;
     ab) run ab_${CONFIG:-c2} 600 python tools/ab_variants.py --config ${CONFIG:-c2} ray-tracing-gpu_amd/lib/var/*.so ;;
+    abenv) run abenv_${CONFIG:-c2} 600 python tools/ab_variants.py --config ${CONFIG:-c2} $AB_ARGS ;;
     pmcvar)
       for L in ray-tracing-gpu_amd/lib/var/*.so; do
         n=$(basename $L .so)
