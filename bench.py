@@ -160,6 +160,39 @@ def cpu_allcores(path, w, h, depth, seconds):
                       f"{el:.1f} s, OpenMP over rows"}
 
 
+def host_boundary(ctx, frame, W):
+    """The drop-in's host-buffer form (not `value`): synchronous rt_render into
+    host memory, as the reference's CScene::LancerRayons hands its frame to
+    glTexImage2D from host memory (Scene.cpp:1562) — the kernel, the RGBA8
+    device-to-host copy over PCIe and the host sync, per frame, into a
+    pageable (numpy) and a pinned (torch) buffer."""
+    import numpy as np
+    import torch
+
+    import rt_amd
+
+    L = rt_amd.lib()
+    rows = rt_amd.frame_rows(frame)
+    frames = 20 if W * rows <= 4_000_000 else 5
+    page = np.empty((rows, W, 4), np.uint8)
+    pinned = torch.empty((rows, W, 4), dtype=torch.uint8).pin_memory()
+    torch.cuda.synchronize()
+    res = {}
+    for kind, ptr in (("pageable", page.ctypes.data), ("pinned", pinned.data_ptr())):
+        if L.rt_render(ctx._h, ctypes.byref(frame), ptr) != 0:
+            return {"error": (L.rt_last_error(ctx._h) or b"").decode()}
+        t0 = time.perf_counter()
+        for _ in range(frames):
+            L.rt_render(ctx._h, ctypes.byref(frame), ptr)
+        ms = (time.perf_counter() - t0) * 1e3 / frames
+        res[kind] = {"ms_per_frame": round(ms, 4), "mray_s": round(W * rows / ms / 1e3, 1)}
+    res["bytes_per_frame"] = int(W * rows * 4)
+    res["frames"] = frames
+    res["note"] = ("rt_render (synchronous) into host memory: kernel + RGBA8 device-to-host copy over PCIe + "
+                   "host sync; the PCIe-inclusive rate, never `value`")
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -373,6 +406,8 @@ def main():
                          "tests_executed": int(run_tests), "tests_brute_force": int(brute_tests),
                          "brute_force_equiv_tflops": round(brute / (kernel_ms * 1e-3) / 1e12, 3)},
         }
+        if world == 1:
+            out["host_boundary"] = host_boundary(ctx, frame, W)
         if world == 1 and not args.no_cpu_baseline:
             cb = cpu_baseline(path, W, H, depth, args.cpu_seconds)
             cb["gpu_over_cpu"] = round(value / cb["value"], 1) if cb["value"] else None
