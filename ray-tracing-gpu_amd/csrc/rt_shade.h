@@ -458,6 +458,10 @@ __device__ __forceinline__ void shadow_opaque_lb(const SceneDev& S, int l, const
     const int cf = bu ? __builtin_amdgcn_readlane(cell, (int)__builtin_ctzll(bu)) : 0;
     const bool one_cell = bu != 0 && __all(!use | (cell == cf));
     unsigned e = 0, end = 0;
+    if (bu) {
+        if (one_cell) RT_EV(cnt, 0);
+        else RT_EV(cnt, 1);
+    }
     if (one_cell) {
         const unsigned* o = S.lb_off + obase + cf;
         const unsigned q0 = o[0], q1 = o[1];

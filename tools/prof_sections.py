@@ -25,7 +25,7 @@ sys.path.insert(0, REPO)
 EVENTS = ["cam_cluster_batches", "cam_member_batches", "cam_exact", "shadow_cluster_ballots",
           "shadow_member_batches", "shadow_exact", "shadow_clusters_by_dcap_only", "shadow_clusters_by_cone"]
 # with the light buffer (shadow_opaque_lb), events 3-7 are its own
-EVENTS_LB = EVENTS[:3] + ["lb_walk_iters", "lb_walk_exact", "lb_dcap_iters", "lb_fallback_waves", "lb_fallback_exact"]
+EVENTS_LB = ["lb_one_cell_walks", "lb_multi_cell_walks", EVENTS[2]] + ["lb_walk_iters", "lb_walk_exact", "lb_dcap_iters", "lb_fallback_waves", "lb_fallback_exact"]
 NAMES = ["setup", "primary", "shade_setup", "shadow_cull", "shadow_exact_tri", "lambert_phong", "store", "shadow_planes"]
 
 
@@ -62,7 +62,7 @@ def main():
     L.rt_debug_prof(buf)
     L.rt_debug_prof_events(ev)
     waves = ((W + 7) // 8) * ((H + 7) // 8) * a.frames
-    ev_names = EVENTS_LB if lbinfo and (a.config in ("c3", "c5") or os.environ.get("RT_AMD_LIGHTBUF") == "1") else EVENTS
+    ev_names = EVENTS_LB if lbinfo and os.environ.get("RT_AMD_LIGHTBUF") != "0" else EVENTS
     tot = sum(buf[:8]) or 1
     print(json.dumps({"config": a.config, "frames": a.frames,
                       "share": {n: round(buf[i] / tot, 4) for i, n in enumerate(NAMES)},
