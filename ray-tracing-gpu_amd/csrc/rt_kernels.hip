@@ -189,17 +189,24 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
 }
 
 // Occupancy floor (waves per SIMD) for the depth-0 kernels: 7 (<= 72
-// VGPRs).  It costs 4 VGPR spills (scratch: ~7 MB of HBM writes per C2
-// frame, far below any bandwidth limit) and wins C2 by 4% over the
-// unconstrained 81 VGPRs / 5 waves; 6 and 8 waves are slower
-// (tools/ab_variants.py, MI355X).
+// VGPRs, no spills) — C2 -4% against the unconstrained 5 waves, 6 waves
+// +1-3% and 8 waves +40% (spills) at C2/C4 — except the big-list kernels
+// with clusters, camera and light buffer (WAVE 14: C3, C5), which run best
+// at 8: -3% / -4% against 7 (tools/ab_variants.py, MI355X).
 #ifndef RT_WAVES_PER_EU
 #define RT_WAVES_PER_EU 7
 #endif
+#ifndef RT_WAVES_PER_EU_BIG
+#define RT_WAVES_PER_EU_BIG 8
+#endif
+constexpr int waves_per_eu(int maxd, int wave)
+{
+    return maxd != 0 ? 1 : (wave == 14 ? RT_WAVES_PER_EU_BIG : RT_WAVES_PER_EU);
+}
 // COUNT: also tally the exact tests executed (the RT_FLAG_STATS launch); in
 // the timed kernels the tallies are dead and compile away.
 template <int MAXD, int LB, int WAVE, bool COUNT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MAXD == 0 ? RT_WAVES_PER_EU : 1))) void rt_trace_kernel(const SceneDev S, const FrameDev F, unsigned* __restrict__ rgba,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(waves_per_eu(MAXD, WAVE)))) void rt_trace_kernel(const SceneDev S, const FrameDev F, unsigned* __restrict__ rgba,
                                                        float* __restrict__ rgbf, StatsDev* __restrict__ stats)
 {
     const int lane = threadIdx.x & 63;
