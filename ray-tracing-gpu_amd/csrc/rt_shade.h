@@ -429,6 +429,10 @@ __device__ __forceinline__ void shadow_opaque_wave(const SceneDev& S, int l0, in
 // lies beyond its point) with the per-lane cone test in front of the exact
 // test, then the dcap list while its dist exceeds the entries' caps; lanes
 // the buffer does not cover take the per-lane loop over every triangle.
+// PIPE: the per-lane walk issues the next entry's gathers before the
+// current entry's test (long lists: C3, C5); without it the walk holds 12
+// fewer VGPRs (short lists).
+template <bool PIPE>
 __device__ __forceinline__ void shadow_opaque_lb(const SceneDev& S, int l, const Vec3 P, const Vec3 L, float dist,
                                                  bool& occ, Counters& cnt)
 {
@@ -500,7 +504,7 @@ __device__ __forceinline__ void shadow_opaque_lb(const SceneDev& S, int l, const
 #else
     bool have = e < end;
 #endif
-    if (have) {
+    if (PIPE && have) {
         const float4* r = S.lb_ent + kLbEnt * (size_t)e;
         r0 = r[0];
         r1 = r[1];
@@ -511,6 +515,12 @@ __device__ __forceinline__ void shadow_opaque_lb(const SceneDev& S, int l, const
         if (!__any(act)) break;
         RT_EV(cnt, 3);
         bool go = false;
+        if (!PIPE && act) {
+            const float4* r = S.lb_ent + kLbEnt * (size_t)e;
+            r0 = r[0];
+            r1 = r[1];
+            r2 = r[2];
+        }
         const float4 c0 = r0, c1 = r1, c2 = r2;
         if (act) {
             if (!(c0.w < dist)) {
@@ -519,7 +529,7 @@ __device__ __forceinline__ void shadow_opaque_lb(const SceneDev& S, int l, const
                 go = true;
                 ++e;
                 have = e < end;
-                if (have) {
+                if (PIPE && have) {
                     const float4* r = S.lb_ent + kLbEnt * (size_t)e;
                     r0 = r[0];
                     r1 = r[1];
@@ -632,6 +642,9 @@ __device__ __forceinline__ void add_light(Color& res, const Mat& m, const float4
     }
 }
 
+#ifndef RT_LB_PIPE
+#define RT_LB_PIPE(WAVE) (((WAVE) & 2) != 0)
+#endif
 template <int kLightBatch, int WAVE>
 __device__ __forceinline__ Color shade_local(const SceneDev& S, const Mat& m, const Vec3 P, const Vec3 N,
                                              const Vec3 D, Counters& cnt, bool active = true)
@@ -662,7 +675,7 @@ __device__ __forceinline__ Color shade_local(const SceneDev& S, const Mat& m, co
             bool occ = !gate;
             RT_MARK(cnt, 2);
 #ifndef RT_ABLATE_SHADOW
-            shadow_opaque_lb(S, li, P, L, dist, occ, cnt);
+            shadow_opaque_lb<RT_LB_PIPE(WAVE)>(S, li, P, L, dist, occ, cnt);
 #endif
             RT_MARK(cnt, 7);
             if (gate) {
