@@ -201,6 +201,8 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-boundary", action="store_true",
+                    help="skip the PCIe-inclusive rt_render leg (profiling runs: only the timed launches)")
     ap.add_argument("--partition", default="auto", choices=["auto", "slabs", "bands"],
                     help="N>1: row slabs, cyclic 16-row bands, or bands when slabs are >10%% imbalanced")
     args = ap.parse_args()
@@ -406,7 +408,7 @@ def main():
                          "tests_executed": int(run_tests), "tests_brute_force": int(brute_tests),
                          "brute_force_equiv_tflops": round(brute / (kernel_ms * 1e-3) / 1e12, 3)},
         }
-        if world == 1:
+        if world == 1 and not args.no_host_boundary:
             out["host_boundary"] = host_boundary(ctx, frame, W)
         if world == 1 and not args.no_cpu_baseline:
             cb = cpu_baseline(path, W, H, depth, args.cpu_seconds)

@@ -28,7 +28,7 @@ for s in $STEPS; do
     bench_one) run bench_${CONFIG:-c2} 400 python bench.py --config ${CONFIG:-c2} --steps 20 --no-cpu-baseline ;;
     listpmc) run list_counters 120 rocprofv3 -L ;;
     pmc)
-      B="python bench.py --steps 5 --warmup 1 --no-cpu-baseline --config ${CONFIG:-c2}"
+      B="python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-host-boundary --config ${CONFIG:-c2}"
       run pmc_fetch_${CONFIG:-c2} 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_${CONFIG:-c2} -o fetch -- $B
       run pmc_write_${CONFIG:-c2} 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_${CONFIG:-c2} -o write -- $B
       run pmc_sq_${CONFIG:-c2} 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmc_${CONFIG:-c2} -o sq -- $B
@@ -47,7 +47,7 @@ for s in $STEPS; do
     fastmath) run fastmath_check 600 tools/fastmath_check ;;
 
     prof) P=gpurun_out/prof_${CONFIG:-c2}
-          run rocprof_${CONFIG:-c2} 400 rocprofv3 --kernel-trace --stats --output-format csv -d $P -o run -- python bench.py --steps ${PROF_STEPS:-200} --no-cpu-baseline --config ${CONFIG:-c2}
+          run rocprof_${CONFIG:-c2} 400 rocprofv3 --kernel-trace --stats --output-format csv -d $P -o run -- python bench.py --steps ${PROF_STEPS:-200} --no-cpu-baseline --no-host-boundary --config ${CONFIG:-c2}
           python tools/prof_summary.py $P/run_kernel_trace.csv > $P/summary.json
           grep '^{"metric"' gpurun_out/rocprof_${CONFIG:-c2}.log > $P/bench_under_rocprof.json ;;
   esac
