@@ -565,6 +565,19 @@ static int lb_mode()
 // the median angular radius of the light's triangle cones (cell half-width
 // ~ that radius), nearest-first cell lists built on the device in two
 // levels (supercells of 16 x 16 cells, then cells), offsets by host scans.
+// Shadow-ray culling covers rays up to dcov = F x the light's farthest
+// triangle (the prepass sizes each pair's margin for it; lanes beyond take
+// the per-lane loop over every triangle).  Big lists: F = 4 (16 and 64 widen
+// the cones: C3 2.3x / 8.8x slower); small lists (<= 1,024 triangles, no
+// clusters): F = RT_DCOV_FACTOR_SMALL — far ground-plane points then stay
+// in the buffer (A/B against 4: 16 / 32 / 64 / 256 = C2 -8 / -10 / -11 /
+// +1%, C4 -8 / -8 / -6 / +5%; C1 and the bounce scenes flat).
+#ifndef RT_DCOV_FACTOR
+#define RT_DCOV_FACTOR 4.0
+#endif
+#ifndef RT_DCOV_FACTOR_SMALL
+#define RT_DCOV_FACTOR_SMALL 32.0
+#endif
 static int lb_build(rt_ctx* c, int ntr, int n_opaque, int nl, const std::vector<double>& dcov)
 {
     const auto t0 = std::chrono::steady_clock::now();
@@ -917,9 +930,10 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
     HIP_TRY(c, hipMalloc((void**)&c->d_cone_cam, std::max<size_t>(ntr, 1) * kConeRec * sizeof(float4)));
     HIP_TRY(c, hipMalloc((void**)&c->d_cone_light, std::max<size_t>(ntr * nl, 1) * kConeRec * sizeof(float4)));
     std::vector<double> lb_dcov((size_t)std::max(nl, 0), 0.0);
+    const double dfac = ntr > (size_t)kClusterMinTriangles ? RT_DCOV_FACTOR : RT_DCOV_FACTOR_SMALL;
     for (int j = 0; j < nl && ntr > 0; ++j) {
         const float* l = s->lights + 7 * (size_t)j;
-        // shadow rays are culled up to 4x the light's farthest triangle
+        // shadow rays are culled up to dfac x the light's farthest triangle
         double far = 0;
         for (size_t k = 0; k < ntr; ++k) {
             double d2 = 0;
@@ -927,10 +941,10 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
             far = std::max(far, std::sqrt(d2) + sph[4 * k + 3]);
         }
         hipLaunchKernelGGL(rt_cone_prepass, dim3((unsigned)((ntr + 255) / 256)), dim3(256), 0, 0, c->d_tri, c->d_trisph,
-                           c->d_trinrm, c->d_tricoef, (int)ntr, l[0], l[1], l[2], 0, (float)(4.0 * far),
+                           c->d_trinrm, c->d_tricoef, (int)ntr, l[0], l[1], l[2], 0, (float)(dfac * far),
                            c->d_cone_light + kConeRec * ntr * j);
         HIP_TRY(c, hipGetLastError());
-        lb_dcov[j] = (double)(float)(4.0 * far);
+        lb_dcov[j] = (double)(float)(dfac * far);
     }
     if (ntr > (size_t)kClusterMinTriangles) {
         c->n_clu = (int)((ntr + 63) / 64);
