@@ -402,6 +402,7 @@ struct rt_ctx {
     float4* d_lb_dcap = nullptr;
     float4* d_lb_meta = nullptr;
     bool lb_ready = false;
+    bool lb_far = false;  // slots n_lights.. are the lights' far buffers
     size_t lb_entries = 0;
     double lb_build_ms = 0.0;
     float cam_key[3] = {0.f, 0.f, 0.f};
@@ -567,19 +568,31 @@ static int lb_mode()
 // levels (supercells of 16 x 16 cells, then cells), offsets by host scans.
 // Shadow-ray culling covers rays up to dcov = F x the light's farthest
 // triangle (the prepass sizes each pair's margin for it; lanes beyond take
-// the per-lane loop over every triangle).  Big lists: F = 4 (16 and 64 widen
-// the cones: C3 2.3x / 8.8x slower); small lists (<= 1,024 triangles, no
-// clusters): F = RT_DCOV_FACTOR_SMALL — far ground-plane points then stay
+// the per-lane loop over every triangle).  Big lists: F = 3 for the light
+// buffer and F = 64 for its far buffer, which takes the lanes beyond
+// (A/B against F = 4 without a far buffer: C3 -11%, C5 -15%; F = 2 or 1.5
+// send so many lanes to the far buffer that C3 is 2.1x / 2.7x slower — and
+// without the far buffer F = 2 was 120x slower: the per-lane loop over
+// 50k triangles); a single F = 16 or 64 widens every cone (C3 2.3x / 8.8x
+// slower).  Small lists (<= 1,024 triangles, no clusters, no far buffer):
+// F = RT_DCOV_FACTOR_SMALL — far ground-plane points then stay
 // in the buffer (A/B against 4: 16 / 32 / 64 / 256 = C2 -8 / -10 / -11 /
 // +1%, C4 -8 / -8 / -6 / +5%; C1 and the bounce scenes flat).
 #ifndef RT_DCOV_FACTOR
-#define RT_DCOV_FACTOR 4.0
+#define RT_DCOV_FACTOR 3.0
 #endif
 #ifndef RT_DCOV_FACTOR_SMALL
 #define RT_DCOV_FACTOR_SMALL 32.0
 #endif
-static int lb_build(rt_ctx* c, int ntr, int n_opaque, int nl, const std::vector<double>& dcov)
+#ifndef RT_DCOV_FACTOR_FAR
+#define RT_DCOV_FACTOR_FAR 64.0
+#endif
+// Slots: one buffer per entry of `cones` (a light's cone records, built for
+// the distance dcov[j]): the lights, then (big lists) their far buffers.
+static int lb_build(rt_ctx* c, int ntr, int n_opaque, const std::vector<const float4*>& cones,
+                    const std::vector<double>& dcov)
 {
+    const int nl = (int)cones.size();
     const auto t0 = std::chrono::steady_clock::now();
     const char* sc = getenv("RT_AMD_LB_SCALE");
     // cells of ~1/4 the median cone radius: best of 1-8 on C3 and C5; and
@@ -614,7 +627,7 @@ static int lb_build(rt_ctx* c, int ntr, int n_opaque, int nl, const std::vector<
         LB_TRY(hipMalloc(&d_perm, std::max<size_t>(ntr, 1) * sizeof(int)));
         for (int j = 0; j < nl; ++j) {
             Build& b = B[j];
-            const float4* cone = c->d_cone_light + kConeRec * (size_t)ntr * j;
+            const float4* cone = cones[j];
             LB_TRY(hipMemcpy(h.data(), cone, h.size() * sizeof(float4), hipMemcpyDeviceToHost));
             std::vector<double> T;
             std::vector<int> perm;
@@ -675,7 +688,7 @@ static int lb_build(rt_ctx* c, int ntr, int n_opaque, int nl, const std::vector<
         size_t obase = 0, ebase = 0, dbase = 0;
         for (int j = 0; j < nl; ++j) {
             Build& b = B[j];
-            const float4* cone = c->d_cone_light + kConeRec * (size_t)ntr * j;
+            const float4* cone = cones[j];
             const unsigned G = b.R / kLbGroup, nsup = 6u * G * G, ncell = 6u * b.R * b.R;
             std::vector<unsigned> off(ncell + 1);
             size_t run = ebase;
@@ -852,6 +865,7 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
     c->d_lb_off = nullptr;
     c->d_lb_ent = c->d_lb_dcap = c->d_lb_meta = nullptr;
     c->lb_ready = false;
+    c->lb_far = false;
     c->lb_entries = 0;
     hipFree(c->d_uni);
     c->d_uni = nullptr;
@@ -930,7 +944,13 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
     HIP_TRY(c, hipMalloc((void**)&c->d_cone_cam, std::max<size_t>(ntr, 1) * kConeRec * sizeof(float4)));
     HIP_TRY(c, hipMalloc((void**)&c->d_cone_light, std::max<size_t>(ntr * nl, 1) * kConeRec * sizeof(float4)));
     std::vector<double> lb_dcov((size_t)std::max(nl, 0), 0.0);
-    const double dfac = ntr > (size_t)kClusterMinTriangles ? RT_DCOV_FACTOR : RT_DCOV_FACTOR_SMALL;
+    // RT_AMD_DCOV_NEAR / RT_AMD_DCOV_FAR override the big-list factors (tests:
+    // force lanes into the far buffer and beyond it)
+    const char* env_near = getenv("RT_AMD_DCOV_NEAR");
+    const char* env_far = getenv("RT_AMD_DCOV_FAR");
+    const double fac_near = env_near && *env_near ? atof(env_near) : RT_DCOV_FACTOR;
+    const double fac_far = env_far && *env_far ? atof(env_far) : RT_DCOV_FACTOR_FAR;
+    const double dfac = ntr > (size_t)kClusterMinTriangles ? fac_near : RT_DCOV_FACTOR_SMALL;
     for (int j = 0; j < nl && ntr > 0; ++j) {
         const float* l = s->lights + 7 * (size_t)j;
         // shadow rays are culled up to dfac x the light's farthest triangle
@@ -977,8 +997,31 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
     HIP_TRY(c, hipDeviceSynchronize());
     const int lbm = lb_mode();  // built only where launch() will use it
     if (ntr > 0 && nl > 0 && n_tri_o > 0 && opaque && (lbm == 1 || (lbm == 2 && ntr > (size_t)kClusterMinTriangles))) {
-        const int rc = lb_build(c, (int)ntr, n_tri_o, nl, lb_dcov);
+        std::vector<const float4*> cones;
+        for (int j = 0; j < nl; ++j) cones.push_back(c->d_cone_light + kConeRec * ntr * j);
+        std::vector<double> dcov = lb_dcov;
+        // Big lists: a far buffer per light, its cone records built for
+        // RT_DCOV_FACTOR_FAR x the farthest triangle, for the lanes beyond the
+        // near buffer's dcov (else the per-lane loop over every triangle).
+        float4* d_cone_far = nullptr;
+        if (ntr > (size_t)kClusterMinTriangles) {
+            HIP_TRY(c, hipMalloc((void**)&d_cone_far, ntr * nl * kConeRec * sizeof(float4)));
+            for (int j = 0; j < nl; ++j) {
+                const float* l = s->lights + 7 * (size_t)j;
+                const double dfar = lb_dcov[j] / dfac * fac_far;
+                hipLaunchKernelGGL(rt_cone_prepass, dim3((unsigned)((ntr + 255) / 256)), dim3(256), 0, 0, c->d_tri,
+                                   c->d_trisph, c->d_trinrm, c->d_tricoef, (int)ntr, l[0], l[1], l[2], 0, (float)dfar,
+                                   d_cone_far + kConeRec * ntr * j);
+                HIP_TRY(c, hipGetLastError());
+                cones.push_back(d_cone_far + kConeRec * ntr * j);
+                dcov.push_back((double)(float)dfar);
+            }
+            HIP_TRY(c, hipDeviceSynchronize());
+        }
+        const int rc = lb_build(c, (int)ntr, n_tri_o, cones, dcov);
+        hipFree(d_cone_far);
         if (rc) return rc;
+        c->lb_far = c->lb_ready && d_cone_far != nullptr;
     }
     HIP_TRY(c, hipMalloc(&c->d_geom, geom.size() * sizeof(float)));
     HIP_TRY(c, hipMalloc(&c->d_mat, mat.size() * sizeof(float)));
@@ -1160,7 +1203,7 @@ static SceneDev scene_dev(rt_ctx* c, bool lbuf, bool cbuf)
                     use_tricam, c->n_tri <= kEdgeMaxTriangles, c->d_cone_cam, c->d_cone_light, c->d_clu_cam,
                     c->d_clu_light, c->n_clu, c->n_surf, c->n_lights, c->n_tri, c->n_plane, c->n_quad,
                     c->n_tri_opaque, c->n_plane_opaque, c->n_quad_opaque, c->n_translucent, c->shadow_split,
-                    lbuf ? 1 : 0, c->d_lb_off, c->d_lb_ent, c->d_lb_dcap, c->d_lb_meta,
+                    lbuf ? (c->lb_far ? 2 : 1) : 0, c->d_lb_off, c->d_lb_ent, c->d_lb_dcap, c->d_lb_meta,
                     (c->d_uni && !getenv("RT_AMD_NO_UNION")) ? c->d_uni : nullptr,
                     c->d_cb_off, c->d_cb_ent, c->d_cb_flag, cbuf ? c->cb_tiles_x : 0};
 }

@@ -422,35 +422,25 @@ __device__ __forceinline__ void shadow_opaque_wave(const SceneDev& S, int l0, in
     }
 }
 
-// One light's shadow rays against the OPAQUE surfaces with the light buffer
-// (shadow_split scenes).  occ: in = lanes without a shadow ray, out = also
-// the occluded ones (any-hit, so the order of the tests is free).  Each lane
-// walks its own cell's list (nearest first, leaving at the first entry that
-// lies beyond its point) with the per-lane cone test in front of the exact
-// test, then the dcap list while its dist exceeds the entries' caps; lanes
-// the buffer does not cover take the per-lane loop over every triangle.
+// One buffer slot's walk for the lanes in `cand` (slot = a light, or
+// n_lights + the light for its far buffer): the lanes whose dist the slot
+// covers (dist <= its dcov) look their cell up, walk its list, then the
+// slot's dcap list while their dist exceeds the entries' caps.  Returns
+// those lanes (the covered ones).
 // PIPE: the per-lane walk issues the next entry's gathers before the
 // current entry's test (long lists: C3, C5); without it the walk holds 12
 // fewer VGPRs (short lists).
 template <bool PIPE>
-__device__ __forceinline__ void shadow_opaque_lb(const SceneDev& S, int l, const Vec3 P, const Vec3 L, float dist,
-                                                 bool& occ, Counters& cnt)
+__device__ __forceinline__ bool lb_slot(const SceneDev& S, int slot, const Vec3 P, const Vec3 L, float dist, bool cand,
+                                        bool& occ, Counters& cnt)
 {
-    for (int k = 0; k < S.n_plane_opaque; ++k) {
-        if (!__any(!occ)) return;
-        ++cnt.pla;
-        occ |= shadow_plane_hit(S.plane[2 * k], P, L, dist);
-    }
-    {
-    const float4 m0 = S.lb_meta[2 * l], m1 = S.lb_meta[2 * l + 1];
+    const float4 m0 = S.lb_meta[2 * slot], m1 = S.lb_meta[2 * slot + 1];
     const unsigned obase = __float_as_uint(m0.x), dbase = __float_as_uint(m0.y), ndcap = __float_as_uint(m0.z);
     const int R = __float_as_int(m0.w);
     const float dcov = m1.x;
     const Vec3 d = -L;
-    const float mx = fmaxf(fabsf(d.x), fmaxf(fabsf(d.y), fabsf(d.z)));
-    const bool use = !occ & (dist <= dcov) & (mx >= 0.5f) & (R > 0);
+    const bool use = cand & !occ & (dist <= dcov) & (R > 0);
     const int cell = use ? lb_cell(d, R) : 0;
-    const float slack = dist * 1e-6f;
     RT_MARK(cnt, 3);
     // Every lane that uses the buffer in ONE cell (a tile's points seen from
     // the light usually are, at coarse resolutions): the wave walks that list
@@ -576,6 +566,32 @@ __device__ __forceinline__ void shadow_opaque_lb(const SceneDev& S, int l, const
             }
         }
     }
+    return use;
+}
+
+// One light's shadow rays against the OPAQUE surfaces with the light buffer
+// (shadow_split scenes).  occ: in = lanes without a shadow ray, out = also
+// the occluded ones (any-hit, so the order of the tests is free).  Lanes
+// within the light's buffer distance walk it (lb_slot); with a far buffer
+// (big lists, S.lb_R == 2) the lanes beyond walk that one; lanes no buffer
+// covers take the per-lane loop over every triangle.
+template <bool PIPE>
+__device__ __forceinline__ void shadow_opaque_lb(const SceneDev& S, int l, const Vec3 P, const Vec3 L, float dist,
+                                                 bool& occ, Counters& cnt)
+{
+    for (int k = 0; k < S.n_plane_opaque; ++k) {
+        if (!__any(!occ)) return;
+        ++cnt.pla;
+        occ |= shadow_plane_hit(S.plane[2 * k], P, L, dist);
+    }
+    {
+    const float mx = fmaxf(fabsf(L.x), fmaxf(fabsf(L.y), fabsf(L.z)));
+    const bool cand = !occ & (mx >= 0.5f);  // a direction the lookup takes
+    bool use = lb_slot<PIPE>(S, l, P, L, dist, cand, occ, cnt);
+    if constexpr (PIPE) {  // big lists: lanes beyond the near buffer
+        if (S.lb_R == 2 && __any(cand & !use & !occ)) use |= lb_slot<PIPE>(S, S.n_lights + l, P, L, dist, cand & !use, occ, cnt);
+    }
+    const float slack = dist * 1e-6f;
     // lanes the buffer does not cover: every opaque triangle, culled per lane
     if (__any(!occ & !use)) {
         RT_EV(cnt, 6);

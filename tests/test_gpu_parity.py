@@ -91,6 +91,23 @@ def test_heightfield_windows(ctx, golden_images, heightfield_path):
         check(full[r0:r1, c0:c1], golden_images[k], 0)
 
 
+@pytest.mark.parametrize("near,far", [(1.5, 64.0), (1.5, 1.6)])
+def test_heightfield_far_buffer(monkeypatch, golden_images, heightfield_path, near, far):
+    """Big lists: lanes beyond the light buffer's distance walk the light's
+    far buffer, lanes beyond that the per-lane loop over every triangle.
+    Both distances shrunk (RT_AMD_DCOV_NEAR/FAR x the farthest triangle) so
+    that many lanes take each path: still the reference's bits."""
+    monkeypatch.setenv("RT_AMD_DCOV_NEAR", str(near))
+    monkeypatch.setenv("RT_AMD_DCOV_FAR", str(far))
+    c = rt_amd.Context(0)
+    full = render(c, heightfield_path, 1920, 1080, 1)
+    keys = [k for k in golden_images.files if k.startswith("hf_1080p_d1_win_")]
+    assert keys
+    for k in keys:
+        r0, r1, c0, c1 = map(int, k.rsplit("_win_", 1)[1].split("_"))
+        check(full[r0:r1, c0:c1], golden_images[k], 0)
+
+
 def test_scene2_1080p_digest_and_counts(ctx, digests):
     full = render(ctx, scene(2), 1920, 1080, 0, flags=rt_amd.FLAG_STATS)
     st = ctx.stats()
