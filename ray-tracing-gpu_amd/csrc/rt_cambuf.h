@@ -81,10 +81,38 @@ __global__ __launch_bounds__(256) void rt_cb_build(const SceneDev S, const Frame
 
 // Keys: entry e's key = min dmin over entries [e, end) of its tile (one
 // thread per tile), so a wave may stop at the first key beyond its hits.
+// Lists of up to RT_CB_SORT entries are first sorted nearest-first (the
+// closest hit is order-free: lexicographic (t, index)), so the keys rise
+// with the walk and the exit comes at the first entry beyond every lane's
+// hit; longer lists keep cluster order.
+#ifndef RT_CB_SORT
+#define RT_CB_SORT 256
+#endif
+__device__ __forceinline__ float cb_dmin(int2 en)
+{
+    const float d = __int_as_float(en.y);
+    return d == d ? d : -INFINITY;
+}
 __global__ void rt_cb_keys(const unsigned* __restrict__ off, int ntiles, int2* __restrict__ ent)
 {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= ntiles) return;
+    const unsigned b = off[t], n = off[t + 1] - off[t];
+    if (n <= RT_CB_SORT) {  // insertion sort by (dmin, triangle)
+        for (unsigned i = 1; i < n; ++i) {
+            const int2 x = ent[b + i];
+            const float dx = cb_dmin(x);
+            unsigned j = i;
+            while (j > 0) {
+                const int2 y = ent[b + j - 1];
+                const float dy = cb_dmin(y);
+                if (dy < dx || (dy == dx && y.x < x.x)) break;
+                ent[b + j] = y;
+                --j;
+            }
+            ent[b + j] = x;
+        }
+    }
     float m = INFINITY;
     for (unsigned e = off[t + 1]; e > off[t]; --e) {
         const float d = __int_as_float(ent[e - 1].y);

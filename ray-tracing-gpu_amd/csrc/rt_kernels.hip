@@ -589,6 +589,9 @@ static int lb_mode()
 #endif
 // Slots: one buffer per entry of `cones` (a light's cone records, built for
 // the distance dcov[j]): the lights, then (big lists) their far buffers.
+#ifndef RT_LB_RMIN
+#define RT_LB_RMIN 128
+#endif
 static int lb_build(rt_ctx* c, int ntr, int n_opaque, const std::vector<const float4*>& cones,
                     const std::vector<double>& dcov)
 {
@@ -601,7 +604,7 @@ static int lb_build(rt_ctx* c, int ntr, int n_opaque, const std::vector<const fl
     // RT_AMD_LB_SCALE (A/B, the stress tests' coarse cells) sets R alone.
     const bool scale_set = sc && *sc;
     const double scale = scale_set ? atof(sc) : 4.0;
-    const int r_min = scale_set ? kLbGroup : 128;
+    const int r_min = scale_set ? kLbGroup : RT_LB_RMIN;
     struct Build {
         int R = 16;
         std::vector<int> dperm;
