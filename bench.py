@@ -398,9 +398,10 @@ def main():
                     "measured_gbps": round(traffic / (kernel_ms * 1e-3) / 1e9, 1) if traffic else None,
                     "frac_of_8TBps": round(traffic / (kernel_ms * 1e-3) / 8e12, 4) if traffic else None,
                     "valu_busy": valu_busy, "source": pmc_src},
-            "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
-                         "bound_note": "FP32 VALU-bound (no dense contraction, so no MFMA); peak = the MI355X "
-                                       "dense FP32 rate (157.3 TF, equal for vector and f32 MFMA)",
+            "roofline": {"bound": "mfma", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
+                         "bound_note": "compute-bound, priced against the dense FP32 peak (the schema's 'mfma' "
+                                       "roofline: 157.3 TF, equal for FP32 vector and MFMA); the kernel itself "
+                                       "runs on the FP32 VALU — no dense contraction, so no MFMA instructions",
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
                          "frac_vs_nofma_issue_peak": round(achieved / PEAK_NOFMA_TOPS, 4),
                          "flops_per_launch": int(flops), "kernel": f"rt_trace_kernel<{st.stack_depth},{st.light_batch}>",
