@@ -121,5 +121,23 @@ __global__ void rt_cb_keys(const unsigned* __restrict__ off, int ntiles, int2* _
     }
 }
 
+// The walk's records: entry e = the tricam record of its triangle, key in
+// [3].z (tricam's [3] = [e2 . Q, file index, 0, 0]).  One thread per entry.
+__global__ void rt_cb_expand(const int2* __restrict__ ent, unsigned n, const float4* __restrict__ tricam,
+                             float4* __restrict__ rec)
+{
+    const unsigned e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n) return;
+    const int2 en = ent[e];
+    const float4* t = tricam + 4 * (size_t)en.x;
+    float4* o = rec + 4 * (size_t)e;
+    o[0] = t[0];
+    o[1] = t[1];
+    o[2] = t[2];
+    float4 d = t[3];
+    d.z = __int_as_float(en.y);
+    o[3] = d;
+}
+
 }  // namespace rt
 #endif  // RT_AMD_RT_CAMBUF_H

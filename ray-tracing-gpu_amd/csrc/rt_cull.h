@@ -241,6 +241,8 @@ __device__ __forceinline__ Vec3 camera_dir(const FrameDev& F, int pxc, int pyc)
 // tighten the exit); then the list in cluster order, leaving once every
 // lane holds a hit nearer than the entry's key (no later entry can report a
 // nearer or equal hit: t >= dmin > best, as in the cluster early exit).
+// INLINE (big lists): walk the inline records when the buffer has them.
+template <bool INLINE>
 __device__ __forceinline__ int closest_hit_camera_list(const SceneDev& S, int tile, const Vec3 O, const Vec3 D,
                                                        float& best_t, Counters& cnt)
 {
@@ -263,12 +265,22 @@ __device__ __forceinline__ int closest_hit_camera_list(const SceneDev& S, int ti
         take_min(ok, t, __float_as_int(c.z), bt, bi);
     }
     const unsigned e1 = S.cb_off[tile + 1];
-    for (unsigned e = S.cb_off[tile]; e < e1; ++e) {
-        const int2 en = S.cb_ent[e];
-        if (!__any((bi < 0) | !(bt < __int_as_float(en.y)))) break;
-        RT_EV(cnt, 2);
-        const float4* r = S.tricam + 4 * en.x;
-        camera_tri(r[0], r[1], r[2], r[3], D, bt, bi, cnt);
+    if (INLINE && S.cb_rec) {  // records inline: one scalar load round trip per entry
+        for (unsigned e = S.cb_off[tile]; e < e1; ++e) {
+            const float4* r = S.cb_rec + 4 * (size_t)e;
+            const float4 a = r[0], b = r[1], c = r[2], d = r[3];  // key in d.z
+            if (!__any((bi < 0) | !(bt < d.z))) break;
+            RT_EV(cnt, 2);
+            camera_tri(a, b, c, d, D, bt, bi, cnt);
+        }
+    } else {
+        for (unsigned e = S.cb_off[tile]; e < e1; ++e) {
+            const int2 en = S.cb_ent[e];
+            if (!__any((bi < 0) | !(bt < __int_as_float(en.y)))) break;
+            RT_EV(cnt, 2);
+            const float4* r = S.tricam + 4 * en.x;
+            camera_tri(r[0], r[1], r[2], r[3], D, bt, bi, cnt);
+        }
     }
     best_t = bt;
     return bi;
@@ -282,7 +294,8 @@ template <int WAVE>
 __device__ __forceinline__ int closest_hit_primary(const SceneDev& S, const Vec3 O, const Vec3 D, float& t,
                                                    Counters& cnt, int tile = -1)
 {
-    if ((WAVE & 8) && tile >= 0 && wave_full()) return closest_hit_camera_list(S, tile, O, D, t, cnt);
+    if ((WAVE & 8) && tile >= 0 && wave_full())
+        return closest_hit_camera_list<(WAVE & 2) != 0>(S, tile, O, D, t, cnt);
     if ((WAVE & 3) > 0 && wave_full()) {
         const WaveCone wc = wave_cone(D, true);
         if (wc.ok) return closest_hit_camera_wave<(WAVE & 3) == 2>(S, wc, O, D, t, cnt);

@@ -390,6 +390,8 @@ struct rt_ctx {
     unsigned* d_cb_off = nullptr;
     unsigned* d_cb_flag = nullptr;
     int2* d_cb_ent = nullptr;
+    float4* d_cb_rec = nullptr;  // 4 x float4 per entry (rt_cb_expand)
+    bool cb_inline = false;      // d_cb_rec holds the current records
     size_t cb_cap = 0;          // entries allocated
     int cb_tiles_x = 0, cb_ntiles = 0;
     float cb_key[25] = {};      // cam_pos, orient, half_w, half_h, inv_w, inv_h, width, height (as float bits)
@@ -487,6 +489,7 @@ RT_EXPORT void rt_destroy(rt_ctx* c)
     hipFree(c->d_cb_off);
     hipFree(c->d_cb_flag);
     hipFree(c->d_cb_ent);
+    hipFree(c->d_cb_rec);
     hipFree(c->d_stats);
     hipFree(c->d_scratch);
     if (c->ev0) hipEventDestroy(c->ev0);
@@ -1208,7 +1211,8 @@ static SceneDev scene_dev(rt_ctx* c, bool lbuf, bool cbuf)
                     c->n_tri_opaque, c->n_plane_opaque, c->n_quad_opaque, c->n_translucent, c->shadow_split,
                     lbuf ? (c->lb_far ? 2 : 1) : 0, c->d_lb_off, c->d_lb_ent, c->d_lb_dcap, c->d_lb_meta,
                     (c->d_uni && !getenv("RT_AMD_NO_UNION")) ? c->d_uni : nullptr,
-                    c->d_cb_off, c->d_cb_ent, c->d_cb_flag, cbuf ? c->cb_tiles_x : 0};
+                    c->d_cb_off, c->d_cb_ent, c->d_cb_flag, cbuf ? c->cb_tiles_x : 0,
+                    c->cb_inline ? c->d_cb_rec : nullptr};
 }
 
 // Camera buffer for the frame's camera (synchronous: the list sizes come
@@ -1249,8 +1253,12 @@ static int cb_build(rt_ctx* c, const rt_frame* f, hipStream_t st)
     }
     if (run > c->cb_cap || !c->d_cb_ent) {
         hipFree(c->d_cb_ent);
+        hipFree(c->d_cb_rec);
         c->d_cb_ent = nullptr;
+        c->d_cb_rec = nullptr;
         HIP_TRY(c, hipMalloc(&c->d_cb_ent, std::max<size_t>(run, 1) * sizeof(int2)));
+        if (run * 4 * sizeof(float4) <= ((size_t)128 << 20))
+            HIP_TRY(c, hipMalloc(&c->d_cb_rec, std::max<size_t>(run, 1) * 4 * sizeof(float4)));
         c->cb_cap = std::max<size_t>(run, 1);
     }
     HIP_TRY(c, hipMemcpyAsync(c->d_cb_off, off.data(), off.size() * sizeof(unsigned), hipMemcpyHostToDevice, st));
@@ -1260,6 +1268,13 @@ static int cb_build(rt_ctx* c, const rt_frame* f, hipStream_t st)
     hipLaunchKernelGGL(rt_cb_keys, dim3((nt + 255) / 256), dim3(256), 0, st, (const unsigned*)c->d_cb_off, nt,
                        c->d_cb_ent);
     HIP_TRY(c, hipGetLastError());
+    // (d_cb_rec exists only if it was sized when the capacity last grew)
+    c->cb_inline = run > 0 && c->d_cb_rec && run * 4 * sizeof(float4) <= ((size_t)128 << 20);
+    if (c->cb_inline) {
+        hipLaunchKernelGGL(rt_cb_expand, dim3((unsigned)((run + 255) / 256)), dim3(256), 0, st,
+                           (const int2*)c->d_cb_ent, (unsigned)run, (const float4*)c->d_tricam, c->d_cb_rec);
+        HIP_TRY(c, hipGetLastError());
+    }
     HIP_TRY(c, hipStreamSynchronize(st));  // off[] (host) must outlive the copy
     cb_key_of(f, c->cb_key);
     c->cb_valid = true;

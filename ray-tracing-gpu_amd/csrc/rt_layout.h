@@ -117,6 +117,13 @@ struct SceneDev {
     const int2* __restrict__ cb_ent;
     const unsigned* __restrict__ cb_flag;
     int cb_tiles_x;
+    // The walk's copy of the entries: per entry the triangle's 64-byte
+    // tricam record with the entry's key in word 14 ([3].z), so one scalar
+    // load round trip per entry instead of two (cb_ent, then tricam);
+    // nullptr: the walk reads cb_ent and tricam (buffers past 128 MB, where
+    // the records' extra bytes cost more: C5 +3%, against C3 -4 to -5%).
+    // Walked inline by the big-list kernel only (small lists: no gain).
+    const float4* __restrict__ cb_rec;
 };
 
 struct FrameDev {
