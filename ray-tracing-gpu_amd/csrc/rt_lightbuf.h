@@ -165,6 +165,12 @@ __global__ __launch_bounds__(256) void rt_lb_super(const float4* __restrict__ co
 // key = dmin (cell lists) or dcap (dcap list).  (A per-lane cone test in
 // front of the exact test was measured to spare no wave any exact test: a
 // cell's list is already what its lanes' cones can reach.)
+// e2.y, e2.z of entry r: an 8-byte load (the entry's last 8 bytes are pad)
+__device__ __forceinline__ float2 lb_tail(const float4* r)
+{
+    return *reinterpret_cast<const float2*>(r + 2);
+}
+
 __device__ __forceinline__ void lb_write(float4* o, const float4* __restrict__ tri, int k, float key)
 {
     const float4 a = tri[3 * k], b = tri[3 * k + 1], c = tri[3 * k + 2];

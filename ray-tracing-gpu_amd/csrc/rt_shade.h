@@ -470,7 +470,8 @@ __device__ __forceinline__ bool lb_slot(const SceneDev& S, int slot, const Vec3 
             if (!__any(act)) break;
             ++cnt.tri;
             RT_EV(cnt, 4);
-            const float4 c1 = r[1], c2 = r[2];
+            const float4 c1 = r[1];
+            const float2 c2 = lb_tail(r);
             if (act) {
                 const Vec3 e1 = make3(c1.x, c1.y, c1.z), e2 = make3(c1.w, c2.x, c2.y);
                 const TriU u = tri_u(make3(c0.x, c0.y, c0.z), e1, e2, P, L);
@@ -488,7 +489,8 @@ __device__ __forceinline__ bool lb_slot(const SceneDev& S, int slot, const Vec3 
     }
     // The next entry's loads are issued before the current entry's exact
     // test (software pipelining of the per-lane gathers).
-    float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0, r2 = r0;
+    float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0;
+    float2 r2 = make_float2(0.f, 0.f);
 #ifdef RT_ABLATE_LBCELL  // timing-only build: no cell walk
     bool have = false;
 #else
@@ -498,7 +500,7 @@ __device__ __forceinline__ bool lb_slot(const SceneDev& S, int slot, const Vec3 
         const float4* r = S.lb_ent + kLbEnt * (size_t)e;
         r0 = r[0];
         r1 = r[1];
-        r2 = r[2];
+        r2 = lb_tail(r);
     }
     for (;;) {
         const bool act = have & !occ;
@@ -509,9 +511,10 @@ __device__ __forceinline__ bool lb_slot(const SceneDev& S, int slot, const Vec3 
             const float4* r = S.lb_ent + kLbEnt * (size_t)e;
             r0 = r[0];
             r1 = r[1];
-            r2 = r[2];
+            r2 = lb_tail(r);
         }
-        const float4 c0 = r0, c1 = r1, c2 = r2;
+        const float4 c0 = r0, c1 = r1;
+        const float2 c2 = r2;
         if (act) {
             if (!(c0.w < dist)) {
                 have = false;  // this and every later entry lie beyond P (dmin)
@@ -523,7 +526,7 @@ __device__ __forceinline__ bool lb_slot(const SceneDev& S, int slot, const Vec3 
                     const float4* r = S.lb_ent + kLbEnt * (size_t)e;
                     r0 = r[0];
                     r1 = r[1];
-                    r2 = r[2];
+                    r2 = lb_tail(r);
                 }
             }
         }
@@ -555,7 +558,8 @@ __device__ __forceinline__ bool lb_slot(const SceneDev& S, int slot, const Vec3 
         if (!__any(need)) break;
         ++cnt.tri;
         RT_EV(cnt, 5);
-        const float4 r1 = r[1], r2 = r[2];
+        const float4 r1 = r[1];
+        const float2 r2 = lb_tail(r);
         if (need) {
             const Vec3 e1 = make3(r1.x, r1.y, r1.z), e2 = make3(r1.w, r2.x, r2.y);
             const TriU u = tri_u(make3(r0.x, r0.y, r0.z), e1, e2, P, L);
