@@ -409,6 +409,7 @@ struct rt_ctx {
     double lb_build_ms = 0.0;
     float cam_key[3] = {0.f, 0.f, 0.f};
     bool cam_valid = false;
+    bool tricam_all = false;  // tricam holds every triangle for cam_key
     StatsDev* d_stats = nullptr;
     void* d_scratch = nullptr;  // staging for host outputs
     size_t scratch_bytes = 0;
@@ -1172,7 +1173,11 @@ static void frame_dev(const rt_frame* f, FrameDev& F)
 // triangle values, camera cone records, union / cluster records.
 static int camera_prepass(rt_ctx* c, const rt_frame* f, hipStream_t st, bool all_tricam)
 {
-    if (c->n_tri <= 0 || (c->cam_valid && std::memcmp(c->cam_key, f->cam_pos, sizeof c->cam_key) == 0)) return RT_OK;
+    // (a camera already prepared without every tricam record — a bounce
+    // frame of a big scene — is prepared again for the camera buffer)
+    if (c->n_tri <= 0 || (c->cam_valid && std::memcmp(c->cam_key, f->cam_pos, sizeof c->cam_key) == 0 &&
+                          (!all_tricam || c->tricam_all)))
+        return RT_OK;
     const float* cp = f->cam_pos;
     if (all_tricam || c->n_tri <= kTricamMaxTriangles) {
         hipLaunchKernelGGL(rt_camera_prepass, dim3((c->n_tri + 255) / 256), dim3(256), 0, st, c->d_tri, c->n_tri,
@@ -1198,6 +1203,7 @@ static int camera_prepass(rt_ctx* c, const rt_frame* f, hipStream_t st, bool all
     }
     std::memcpy(c->cam_key, f->cam_pos, sizeof c->cam_key);
     c->cam_valid = true;
+    c->tricam_all = all_tricam || c->n_tri <= kTricamMaxTriangles;
     c->cb_valid = false;
     return RT_OK;
 }

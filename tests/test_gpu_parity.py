@@ -219,6 +219,25 @@ def test_camera_buffer_follows_the_camera(monkeypatch):
         assert bits_equal(out.cpu().numpy(), w), k
 
 
+def test_camera_buffer_after_bounce_frame(tmp_path):
+    """A big scene rendered first with bounces (no camera buffer, so camera
+    records only for <= 256 triangles), then at depth 0 from the same
+    camera: the camera buffer must be built from complete records."""
+    from rt_amd import synth
+
+    path = synth.write_heightfield(str(tmp_path / "hfr.dat"), cols=40, rows=20, reflect=0.5)
+    s = rt_amd.Scene(path, 320, 240, 3)
+    c = rt_amd.Context(0)
+    c.upload(s)
+    c.render_float(s.frame)  # bounce kernel first
+    f0 = s.frame.copy()
+    f0.max_bounces = 0
+    got = c.render_float(f0)
+    ref = rt_amd.Context(0)
+    ref.upload(s)
+    assert bits_equal(got, ref.render_float(f0))
+
+
 def test_async_device_outputs(ctx):
     torch = pytest.importorskip("torch")
     s = rt_amd.Scene(scene(6), 128, 96, 3)
