@@ -217,20 +217,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(waves_per_e
     // row-major order, so neighbouring tiles — which read the same cells,
     // tile lists and records — share an L2.  A bijection for any grid size.
     int bx = (int)blockIdx.x, by = (int)blockIdx.y;
-#ifndef RT_NO_XCD_MAP
-    {
-        // chunks of K = 4 consecutive blocks dealt round-robin to the XCDs
-        // (C2 -2.3%, C3 -1.2% in A/B; whole-region runs per XCD were 1.8x
-        // slower on C3: the mesh rows then pile onto a few XCDs)
+    // Chunks of K consecutive blocks dealt round-robin to the XCDs, when the
+    // grid divides evenly (whole-region runs per XCD were 1.8x slower on C3:
+    // the mesh rows then pile onto a few XCDs).  Per kernel (A/B): the
+    // big-list kernel K = 8 (C5 -1.4% against 4), the small-list kernel
+    // none (C2 -2.5% against 4; the remap's code alone costs it).
+    constexpr unsigned K = (WAVE & 2) ? RT_XCD_CHUNK_BIG : RT_XCD_CHUNK_SMALL;
+    if constexpr (K > 0) {
         const unsigned nb = gridDim.x * gridDim.y, w = blockIdx.y * gridDim.x + blockIdx.x;
-        const unsigned K = RT_XCD_CHUNK, x = w % kXcds, i = w / kXcds;
+        const unsigned x = w % kXcds, i = w / kXcds;
         const unsigned lw = ((i / K) * kXcds + x) * K + i % K;
         if (lw < nb && (nb % (kXcds * K)) == 0) {
             bx = (int)(lw % gridDim.x);
             by = (int)(lw / gridDim.x);
         }
     }
-#endif
     const int px = bx * 16 + (wave & 1) * 8 + (lane & 7);
     const int ly0 = by * 16 + (wave >> 1) * 8;  // the wave's first output row
     const int ly = ly0 + (lane >> 3);

@@ -145,8 +145,11 @@ struct StatsDev {
 // launch spread over many addresses instead of serialising on one.
 constexpr int kStatSlots = 256;
 constexpr unsigned kXcds = 8;  // MI355X: 8 XCDs, one L2 each
-#ifndef RT_XCD_CHUNK
-#define RT_XCD_CHUNK 4
+#ifndef RT_XCD_CHUNK_BIG
+#define RT_XCD_CHUNK_BIG 8
+#endif
+#ifndef RT_XCD_CHUNK_SMALL
+#define RT_XCD_CHUNK_SMALL 0
 #endif
 
 // Per-lane tallies (RT_FLAG_STATS): rays, and the exact ray-primitive tests
