@@ -297,12 +297,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(waves_per_e
         }
     }
 #endif
-    if (F.flags & RT_FLAG_STATS) {
+    // Only the COUNT variant (the RT_FLAG_STATS launch, pick_kernel) tallies:
+    // in the timed kernels every counter is dead code.
+    if (COUNT && (F.flags & RT_FLAG_STATS)) {
         unsigned long long v[7] = {cnt.primary, cnt.bounce, cnt.shadow, cnt.skipped, cnt.tri, cnt.pla, cnt.qua};
         StatsDev* sl = stats + ((blockIdx.x + blockIdx.y * gridDim.x) % kStatSlots);
         unsigned long long* dst[7] = {&sl->primary, &sl->bounce, &sl->shadow, &sl->skipped,
                                       &sl->tri, &sl->pla, &sl->qua};
-        const int nv = COUNT ? 7 : 4;
+        const int nv = 7;
         if (wave_full()) {  // one atomic per counter per wave
 #pragma unroll
             for (int i = 0; i < 7; ++i)
