@@ -593,7 +593,8 @@ __device__ __forceinline__ void shadow_opaque_lb(const SceneDev& S, int l, const
     const bool cand = !occ & (mx >= 0.5f);  // a direction the lookup takes
     bool use = lb_slot<PIPE>(S, l, P, L, dist, cand, occ, cnt);
     if constexpr (PIPE) {  // big lists: lanes beyond the near buffer
-        if (S.lb_R == 2 && __any(cand & !use & !occ)) use |= lb_slot<PIPE>(S, S.n_lights + l, P, L, dist, cand & !use, occ, cnt);
+        if (S.lb_R == 2 && __any(cand & !use & !occ))
+            use |= lb_slot<PIPE>(S, S.n_lights + l, P, L, dist, cand & !use, occ, cnt);
     }
     const float slack = dist * 1e-6f;
     // lanes the buffer does not cover: every opaque triangle, culled per lane
