@@ -407,7 +407,7 @@ struct rt_ctx {
     float4* d_lb_dcap = nullptr;
     float4* d_lb_meta = nullptr;
     bool lb_ready = false;
-    bool lb_far = false;  // slots n_lights.. are the lights' far buffers
+    int lb_levels = 0;  // buffers per light: slot = level * n_lights + light
     size_t lb_entries = 0;
     double lb_build_ms = 0.0;
     float cam_key[3] = {0.f, 0.f, 0.f};
@@ -575,24 +575,26 @@ static int lb_mode()
 // levels (supercells of 16 x 16 cells, then cells), offsets by host scans.
 // Shadow-ray culling covers rays up to dcov = F x the light's farthest
 // triangle (the prepass sizes each pair's margin for it; lanes beyond take
-// the per-lane loop over every triangle).  Big lists: F = 3 for the light
-// buffer and F = 64 for its far buffer, which takes the lanes beyond
-// (A/B against F = 4 without a far buffer: C3 -11%, C5 -15%; F = 2 or 1.5
-// send so many lanes to the far buffer that C3 is 2.1x / 2.7x slower — and
-// without the far buffer F = 2 was 120x slower: the per-lane loop over
-// 50k triangles); a single F = 16 or 64 widens every cone (C3 2.3x / 8.8x
-// slower).  Small lists (<= 1,024 triangles, no clusters, no far buffer):
-// F = RT_DCOV_FACTOR_SMALL — far ground-plane points then stay
+// the next level, or the per-lane loop over every triangle).  Big lists: a
+// ladder of buffers per light, F = 1.5 then far buffers at 4, 16 and 64 —
+// each level's cones only as wide as its distance needs (A/B against one
+// buffer at 3 plus one at 64: C3 -10%, C5 -8.5%; a single buffer at 2
+// without far levels was 120x slower: lanes beyond fell into the per-lane
+// loop over 50k triangles; one buffer at 16 or 64 widens every cone: C3
+// 2.3x / 8.8x slower).  Small lists (<= 1,024 triangles, no clusters, one
+// level): F = RT_DCOV_FACTOR_SMALL — far ground-plane points then stay
 // in the buffer (A/B against 4: 16 / 32 / 64 / 256 = C2 -8 / -10 / -11 /
 // +1%, C4 -8 / -8 / -6 / +5%; C1 and the bounce scenes flat).
+// RT_AMD_DCOV_NEAR / RT_AMD_DCOV_FAR (a comma list) override the big-list
+// ladder at upload (tests, A/B).
 #ifndef RT_DCOV_FACTOR
-#define RT_DCOV_FACTOR 3.0
+#define RT_DCOV_FACTOR 1.5
 #endif
 #ifndef RT_DCOV_FACTOR_SMALL
 #define RT_DCOV_FACTOR_SMALL 32.0
 #endif
-#ifndef RT_DCOV_FACTOR_FAR
-#define RT_DCOV_FACTOR_FAR 64.0
+#ifndef RT_DCOV_FACTOR_FAR  // the far buffers' factors, comma-separated, rising
+#define RT_DCOV_FACTOR_FAR "4,16,64"
 #endif
 // Slots: one buffer per entry of `cones` (a light's cone records, built for
 // the distance dcov[j]): the lights, then (big lists) their far buffers.
@@ -875,7 +877,7 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
     c->d_lb_off = nullptr;
     c->d_lb_ent = c->d_lb_dcap = c->d_lb_meta = nullptr;
     c->lb_ready = false;
-    c->lb_far = false;
+    c->lb_levels = 0;
     c->lb_entries = 0;
     hipFree(c->d_uni);
     c->d_uni = nullptr;
@@ -959,7 +961,16 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
     const char* env_near = getenv("RT_AMD_DCOV_NEAR");
     const char* env_far = getenv("RT_AMD_DCOV_FAR");
     const double fac_near = env_near && *env_near ? atof(env_near) : RT_DCOV_FACTOR;
-    const double fac_far = env_far && *env_far ? atof(env_far) : RT_DCOV_FACTOR_FAR;
+    std::vector<double> fac_far;
+    {
+        std::string lv = env_far && *env_far ? env_far : RT_DCOV_FACTOR_FAR;
+        for (size_t a = 0; a <= lv.size();) {
+            size_t b = lv.find(',', a);
+            if (b == std::string::npos) b = lv.size();
+            if (b > a) fac_far.push_back(atof(lv.substr(a, b - a).c_str()));
+            a = b + 1;
+        }
+    }
     const double dfac = ntr > (size_t)kClusterMinTriangles ? fac_near : RT_DCOV_FACTOR_SMALL;
     for (int j = 0; j < nl && ntr > 0; ++j) {
         const float* l = s->lights + 7 * (size_t)j;
@@ -1013,25 +1024,29 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
         // Big lists: a far buffer per light, its cone records built for
         // RT_DCOV_FACTOR_FAR x the farthest triangle, for the lanes beyond the
         // near buffer's dcov (else the per-lane loop over every triangle).
+        // (one level per factor: slots level * n_lights + light)
         float4* d_cone_far = nullptr;
-        if (ntr > (size_t)kClusterMinTriangles) {
-            HIP_TRY(c, hipMalloc((void**)&d_cone_far, ntr * nl * kConeRec * sizeof(float4)));
-            for (int j = 0; j < nl; ++j) {
-                const float* l = s->lights + 7 * (size_t)j;
-                const double dfar = lb_dcov[j] / dfac * fac_far;
-                hipLaunchKernelGGL(rt_cone_prepass, dim3((unsigned)((ntr + 255) / 256)), dim3(256), 0, 0, c->d_tri,
-                                   c->d_trisph, c->d_trinrm, c->d_tricoef, (int)ntr, l[0], l[1], l[2], 0, (float)dfar,
-                                   d_cone_far + kConeRec * ntr * j);
-                HIP_TRY(c, hipGetLastError());
-                cones.push_back(d_cone_far + kConeRec * ntr * j);
-                dcov.push_back((double)(float)dfar);
-            }
+        const size_t nlev = ntr > (size_t)kClusterMinTriangles ? fac_far.size() : 0;
+        if (nlev > 0) {
+            HIP_TRY(c, hipMalloc((void**)&d_cone_far, nlev * ntr * nl * kConeRec * sizeof(float4)));
+            for (size_t v = 0; v < nlev; ++v)
+                for (int j = 0; j < nl; ++j) {
+                    const float* l = s->lights + 7 * (size_t)j;
+                    const double dfar = lb_dcov[j] / dfac * fac_far[v];
+                    float4* out = d_cone_far + kConeRec * ntr * (v * nl + j);
+                    hipLaunchKernelGGL(rt_cone_prepass, dim3((unsigned)((ntr + 255) / 256)), dim3(256), 0, 0,
+                                       c->d_tri, c->d_trisph, c->d_trinrm, c->d_tricoef, (int)ntr, l[0], l[1], l[2], 0,
+                                       (float)dfar, out);
+                    HIP_TRY(c, hipGetLastError());
+                    cones.push_back(out);
+                    dcov.push_back((double)(float)dfar);
+                }
             HIP_TRY(c, hipDeviceSynchronize());
         }
         const int rc = lb_build(c, (int)ntr, n_tri_o, cones, dcov);
         hipFree(d_cone_far);
         if (rc) return rc;
-        c->lb_far = c->lb_ready && d_cone_far != nullptr;
+        c->lb_levels = c->lb_ready ? 1 + (int)nlev : 0;
     }
     HIP_TRY(c, hipMalloc(&c->d_geom, geom.size() * sizeof(float)));
     HIP_TRY(c, hipMalloc(&c->d_mat, mat.size() * sizeof(float)));
@@ -1218,7 +1233,7 @@ static SceneDev scene_dev(rt_ctx* c, bool lbuf, bool cbuf)
                     use_tricam, c->n_tri <= kEdgeMaxTriangles, c->d_cone_cam, c->d_cone_light, c->d_clu_cam,
                     c->d_clu_light, c->n_clu, c->n_surf, c->n_lights, c->n_tri, c->n_plane, c->n_quad,
                     c->n_tri_opaque, c->n_plane_opaque, c->n_quad_opaque, c->n_translucent, c->shadow_split,
-                    lbuf ? (c->lb_far ? 2 : 1) : 0, c->d_lb_off, c->d_lb_ent, c->d_lb_dcap, c->d_lb_meta,
+                    lbuf ? c->lb_levels : 0, c->d_lb_off, c->d_lb_ent, c->d_lb_dcap, c->d_lb_meta,
                     (c->d_uni && !getenv("RT_AMD_NO_UNION")) ? c->d_uni : nullptr,
                     c->d_cb_off, c->d_cb_ent, c->d_cb_flag, cbuf ? c->cb_tiles_x : 0,
                     c->cb_inline ? c->d_cb_rec : nullptr};

@@ -96,9 +96,9 @@ struct SceneDev {
     // reach a ray whose direction falls in c (rt_lb_* kernels).
     // lb_off[meta.off + c] .. [+ c + 1] index lb_ent; lb_dcap holds, per
     // light, the triangles whose cull is not valid up to meta.dcov (sorted by
-    // that distance cap).  lb_R = 0: off; 1: one buffer per light (slots
-    // 0..n_lights-1 of lb_meta); 2: and a far buffer per light (slot
-    // n_lights + l, built for a larger distance, for the lanes beyond).
+    // that distance cap).  lb_R = 0: off; else the levels per light: slot
+    // level * n_lights + l of lb_meta, each level built for a larger
+    // distance than the last (the far buffers), for the lanes beyond it.
     int lb_R;
     const unsigned* __restrict__ lb_off;
     const float4* __restrict__ lb_ent;

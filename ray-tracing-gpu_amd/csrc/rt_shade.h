@@ -576,9 +576,9 @@ __device__ __forceinline__ bool lb_slot(const SceneDev& S, int slot, const Vec3 
 // One light's shadow rays against the OPAQUE surfaces with the light buffer
 // (shadow_split scenes).  occ: in = lanes without a shadow ray, out = also
 // the occluded ones (any-hit, so the order of the tests is free).  Lanes
-// within the light's buffer distance walk it (lb_slot); with a far buffer
-// (big lists, S.lb_R == 2) the lanes beyond walk that one; lanes no buffer
-// covers take the per-lane loop over every triangle.
+// within the light's buffer distance walk it (lb_slot); with far buffers
+// (big lists, S.lb_R levels) the lanes beyond walk the next level's; lanes
+// no buffer covers take the per-lane loop over every triangle.
 template <bool PIPE>
 __device__ __forceinline__ void shadow_opaque_lb(const SceneDev& S, int l, const Vec3 P, const Vec3 L, float dist,
                                                  bool& occ, Counters& cnt)
@@ -592,9 +592,11 @@ __device__ __forceinline__ void shadow_opaque_lb(const SceneDev& S, int l, const
     const float mx = fmaxf(fabsf(L.x), fmaxf(fabsf(L.y), fabsf(L.z)));
     const bool cand = !occ & (mx >= 0.5f);  // a direction the lookup takes
     bool use = lb_slot<PIPE>(S, l, P, L, dist, cand, occ, cnt);
-    if constexpr (PIPE) {  // big lists: lanes beyond the near buffer
-        if (S.lb_R == 2 && __any(cand & !use & !occ))
-            use |= lb_slot<PIPE>(S, S.n_lights + l, P, L, dist, cand & !use, occ, cnt);
+    if constexpr (PIPE) {  // big lists: lanes beyond a buffer take the next
+        for (int lv = 1; lv < S.lb_R; ++lv) {
+            if (!__any(cand & !use & !occ)) break;
+            use |= lb_slot<PIPE>(S, lv * S.n_lights + l, P, L, dist, cand & !use, occ, cnt);
+        }
     }
     const float slack = dist * 1e-6f;
     // lanes the buffer does not cover: every opaque triangle, culled per lane

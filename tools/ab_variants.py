@@ -49,7 +49,8 @@ def main():
     vs = []
     for spec in a.libs:
         lp, _, envs = spec.partition("@")
-        env = dict(kv.split("=", 1) for kv in envs.split(",") if kv)
+        # (a value's own commas are written ':', e.g. RT_AMD_DCOV_FAR=6:64)
+        env = {k: v.replace(":", ",") for k, v in (kv.split("=", 1) for kv in envs.split(",") if kv)}
         saved = {k: os.environ.get(k) for k in env}
         os.environ.update(env)
         L = load(lp)
