@@ -576,9 +576,10 @@ static int lb_mode()
 // Shadow-ray culling covers rays up to dcov = F x the light's farthest
 // triangle (the prepass sizes each pair's margin for it; lanes beyond take
 // the next level, or the per-lane loop over every triangle).  Big lists: a
-// ladder of buffers per light, F = 1.5 then far buffers at 4, 16 and 64 —
-// each level's cones only as wide as its distance needs (A/B against one
-// buffer at 3 plus one at 64: C3 -10%, C5 -8.5%; a single buffer at 2
+// ladder of buffers per light, F = 1.25 then far buffers at 2.5, 6, 16 and
+// 64 — each level's cones only as wide as its distance needs (A/B: 1.5 / 4 /
+// 16 / 64 against one buffer at 3 plus one at 64: C3 -10%, C5 -8.5%; this
+// ladder against that one: C3 -2%, C5 -5%; a single buffer at 2
 // without far levels was 120x slower: lanes beyond fell into the per-lane
 // loop over 50k triangles; one buffer at 16 or 64 widens every cone: C3
 // 2.3x / 8.8x slower).  Small lists (<= 1,024 triangles, no clusters, one
@@ -588,13 +589,13 @@ static int lb_mode()
 // RT_AMD_DCOV_NEAR / RT_AMD_DCOV_FAR (a comma list) override the big-list
 // ladder at upload (tests, A/B).
 #ifndef RT_DCOV_FACTOR
-#define RT_DCOV_FACTOR 1.5
+#define RT_DCOV_FACTOR 1.25
 #endif
 #ifndef RT_DCOV_FACTOR_SMALL
 #define RT_DCOV_FACTOR_SMALL 32.0
 #endif
 #ifndef RT_DCOV_FACTOR_FAR  // the far buffers' factors, comma-separated, rising
-#define RT_DCOV_FACTOR_FAR "4,16,64"
+#define RT_DCOV_FACTOR_FAR "2.5,6,16,64"
 #endif
 // Slots: one buffer per entry of `cones` (a light's cone records, built for
 // the distance dcov[j]): the lights, then (big lists) their far buffers.
