@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 3
+#define RT_ABI_VERSION 4
 
 enum {
     RT_OK = 0,
@@ -146,12 +146,59 @@ int rt_render(rt_ctx*, const rt_frame*, uint8_t* rgba8_out);
 int rt_render_float(rt_ctx*, const rt_frame*, float* rgb_out);
 /* Asynchronous, device pointers only, enqueued on `hip_stream` (a hipStream_t;
  * NULL = the HIP null stream, as in every HIP API).  Either output may be
- * NULL.  No host sync, no allocation: safe to capture in a hipGraph or to
- * enqueue ahead of an RCCL collective on the same stream.  It uses the
- * camera buffer only when it is current for the frame's camera (never
- * builds it): one synchronous render after a camera change makes the
- * following async renders take the fast path.  Same image either way. */
+ * NULL.  No host sync, no allocation.  It uses the camera buffer only when it
+ * is current for the frame's camera (never builds it): one synchronous render
+ * after a camera change makes the following async renders take the fast
+ * path.  Same image either way.
+ *
+ * Ordering (ABI 4).  The context keeps per-camera state on the device (camera
+ * records, cone records, the camera buffer).  Every write of that state is
+ * ordered after every render already enqueued on any stream that may read
+ * it, and every render after the write that produced its state, with HIP
+ * events — the caller needs no host sync between rt_render_async on any
+ * number of streams and the synchronous calls, in any order.  A stream
+ * passed here must stay alive until the next synchronous call on the context
+ * (rt_render*, rt_upload_scene, rt_sync, rt_destroy) returns.
+ *
+ * hipGraph capture.  When `hip_stream` is capturing, the call records only
+ * the trace kernel: the camera state must already be current for the frame
+ * (a synchronous render, or rt_prepare_camera, of that camera first), else
+ * RT_E_STATE.  A replay renders with the camera state current at replay
+ * time, so it is valid while no other camera is rendered on the context; no
+ * buffer a captured render references is freed before rt_upload_scene or
+ * rt_destroy. */
 int rt_render_async(rt_ctx*, const rt_frame*, uint8_t* rgba8_dev, float* rgb_dev, void* hip_stream);
+/* ABI 4: make the per-camera state (camera records, and the camera buffer
+ * where the frame's kernel uses one) current for `frame` without rendering.
+ * Synchronous, like rt_render. */
+int rt_prepare_camera(rt_ctx*, const rt_frame* frame);
+/* ABI 4: wait until everything enqueued through this context (any stream)
+ * has finished. */
+int rt_sync(rt_ctx*);
+
+/* ABI 4: context options.  A/B and test switches and tuning knobs; no option
+ * changes a single bit of any image.  Upload options take effect at the next
+ * rt_upload_scene, launch options at the next render.                      */
+enum {
+    RT_OPT_LIGHT_BUFFER = 1,    /* upload+launch: shadow rays through the light buffer:
+                                   1 every depth-0 scene with opaque triangles (default),
+                                   2 only above 1,024 triangles, 0 never (wave culling) */
+    RT_OPT_CAMERA_BUFFER = 2,   /* launch: per-camera tile lists, 1 (default) / 0 */
+    RT_OPT_UNION_PRETEST = 3,   /* launch: small lists' union cone pre-test, 1 (default) / 0 */
+    RT_OPT_LB_SCALE = 4,        /* upload: light-buffer cells per cone radius; 0 = auto (4,
+                                   at least 128 cells per face edge); > 0 sets R alone */
+    RT_OPT_DCOV_NEAR = 5,       /* upload: big lists' near light-buffer distance, x the
+                                   light's farthest triangle; 0 = default (1.25) */
+    RT_OPT_CB_INLINE_MAX_MB = 6 /* launch: camera-buffer entries carry inline camera
+                                   records while they fit this many MiB (default 128;
+                                   0 = never: the index walk) */
+};
+int rt_set_option(rt_ctx*, int32_t option, double value);
+int rt_get_option(rt_ctx*, int32_t option, double* value);
+/* ABI 4, upload: the far light-buffer ladder of big lists — rising distance
+ * factors (x the light's farthest triangle), n <= 8; n = 0: none; factors =
+ * NULL and n < 0: the default 2.5, 6, 16, 64. */
+int rt_set_far_ladder(rt_ctx*, const double* factors, int32_t n);
 int rt_last_stats(rt_ctx*, rt_stats* out);
 const char* rt_last_error(rt_ctx*);
 void rt_destroy(rt_ctx*);

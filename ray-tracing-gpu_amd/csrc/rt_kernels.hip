@@ -37,6 +37,7 @@
 #include <vector>
 
 #include "../../include/rt.h"
+#include "rt_scan.h"
 #include "rt_shade.h"
 
 #pragma clang fp contract(off)
@@ -396,6 +397,13 @@ struct rt_ctx {
     float4* d_cb_rec = nullptr;  // 4 x float4 per entry (rt_cb_expand)
     bool cb_inline = false;      // d_cb_rec holds the current records
     size_t cb_cap = 0;          // entries allocated
+    size_t cb_rec_cap = 0;      // inline records allocated (entries)
+    hipEvent_t ev_cb0 = nullptr, ev_cb1 = nullptr;  // around the last build's device work
+    double cb_host_ms = 0.0;
+    bool cb_timed = false;
+    void* d_scan = nullptr;     // u64 scratch of the build scans
+    size_t scan_words = 0;
+    unsigned long long* h_word = nullptr;  // pinned: totals read back by the builds
     int cb_tiles_x = 0, cb_ntiles = 0;
     float cb_key[25] = {};      // cam_pos, orient, half_w, half_h, inv_w, inv_h, width, height (as float bits)
     bool cb_valid = false;
@@ -416,6 +424,25 @@ struct rt_ctx {
     StatsDev* d_stats = nullptr;
     void* d_scratch = nullptr;  // staging for host outputs
     size_t scratch_bytes = 0;
+    // Ordering of the per-camera device state across streams (rt.h, ABI 4):
+    // the streams that received rt_render_async work since the last host
+    // sync of the context, and the stream + event of the last write of the
+    // per-camera state not yet host-synced (an async camera prepass).
+    std::vector<hipStream_t> async_streams;
+    hipEvent_t ev_fence = nullptr, ev_state = nullptr;
+    hipStream_t state_stream = nullptr;
+    bool state_pending = false;
+    bool captured = false;                // a render was captured into a hipGraph
+    std::vector<void*> retired;           // buffers a captured render may reference
+    // Options (rt_set_option; rt.h RT_OPT_*)
+    int opt_light_buffer = 1;
+    bool opt_camera_buffer = true;
+    bool opt_union = true;
+    double opt_lb_scale = 0.0;
+    double opt_dcov_near = 0.0;
+    double opt_cb_inline_mb = 128.0;
+    std::vector<double> far_ladder;       // big lists' far light buffers
+    double upload_parts_ms[4] = {0, 0, 0, 0};  // copy+records, prepasses, light buffer, total
     int n_surf = 0, n_lights = 0;
     int n_tri = 0, n_plane = 0, n_quad = 0;
     int n_tri_opaque = 0, n_plane_opaque = 0, n_quad_opaque = 0, n_translucent = 0;
@@ -459,7 +486,145 @@ RT_EXPORT int rt_create(int32_t dev, rt_ctx** out)
     HIP_TRY(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIP_TRY(c, hipEventCreate(&c->ev0));
     HIP_TRY(c, hipEventCreate(&c->ev1));
+    HIP_TRY(c, hipEventCreateWithFlags(&c->ev_fence, hipEventDisableTiming));
+    HIP_TRY(c, hipEventCreateWithFlags(&c->ev_state, hipEventDisableTiming));
+    HIP_TRY(c, hipEventCreate(&c->ev_cb0));
+    HIP_TRY(c, hipEventCreate(&c->ev_cb1));
+    HIP_TRY(c, hipHostMalloc((void**)&c->h_word, 2 * sizeof(unsigned long long), hipHostMallocDefault));
     HIP_TRY(c, hipMalloc(&c->d_stats, kStatSlots * sizeof(StatsDev)));
+    c->far_ladder = {2.5, 6.0, 16.0, 64.0};
+    return RT_OK;
+}
+
+// Free now, or — once a render was captured into a hipGraph — keep until
+// rt_upload_scene / rt_destroy (a replay may still reference it).
+static void release(rt_ctx* c, void* p)
+{
+    if (!p) return;
+    if (c->captured)
+        c->retired.push_back(p);
+    else
+        hipFree(p);
+}
+
+static void free_retired(rt_ctx* c)
+{
+    for (void* p : c->retired) hipFree(p);
+    c->retired.clear();
+    c->captured = false;
+}
+
+// ---- ordering of the per-camera state across streams (rt.h, ABI 4)
+// Make stream w wait for everything already enqueued on the streams that
+// received async renders (they may read the state w is about to rewrite).
+static int fence_async(rt_ctx* c, hipStream_t w)
+{
+    for (hipStream_t s : c->async_streams) {
+        if (s == w) continue;
+        HIP_TRY(c, hipEventRecord(c->ev_fence, s));
+        HIP_TRY(c, hipStreamWaitEvent(w, c->ev_fence, 0));
+    }
+    return RT_OK;
+}
+
+// A reader on stream r of state written on another stream and not yet
+// host-synced waits for that write.
+static int wait_state(rt_ctx* c, hipStream_t r)
+{
+    if (c->state_pending && c->state_stream != r) HIP_TRY(c, hipStreamWaitEvent(r, c->ev_state, 0));
+    return RT_OK;
+}
+
+static void note_async(rt_ctx* c, hipStream_t s)
+{
+    if (std::find(c->async_streams.begin(), c->async_streams.end(), s) == c->async_streams.end())
+        c->async_streams.push_back(s);
+}
+
+// Host sync of everything the context enqueued: afterwards no async render
+// or state write is in flight.
+static int sync_all(rt_ctx* c)
+{
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    for (hipStream_t s : c->async_streams) HIP_TRY(c, hipStreamSynchronize(s));
+    c->async_streams.clear();
+    c->state_pending = false;
+    c->state_stream = nullptr;
+    return RT_OK;
+}
+
+// Device scratch for the build scans (u64 words), grown on demand.
+static int ensure_scan(rt_ctx* c, size_t words)
+{
+    if (c->scan_words >= words) return RT_OK;
+    release(c, c->d_scan);
+    c->d_scan = nullptr;
+    c->scan_words = 0;
+    HIP_TRY(c, hipMalloc(&c->d_scan, words * sizeof(unsigned long long)));
+    c->scan_words = words;
+    return RT_OK;
+}
+
+RT_EXPORT int rt_sync(rt_ctx* c)
+{
+    if (!c) return RT_E_ARG;
+    if (!c->stream) return RT_E_STATE;
+    HIP_TRY(c, hipSetDevice(c->device));
+    return sync_all(c);
+}
+
+RT_EXPORT int rt_set_option(rt_ctx* c, int32_t opt, double v)
+{
+    if (!c || !(v == v)) return RT_E_ARG;
+    switch (opt) {
+    case RT_OPT_LIGHT_BUFFER:
+        if (v != 0 && v != 1 && v != 2) return RT_E_ARG;
+        c->opt_light_buffer = (int)v;
+        return RT_OK;
+    case RT_OPT_CAMERA_BUFFER: c->opt_camera_buffer = v != 0; return RT_OK;
+    case RT_OPT_UNION_PRETEST: c->opt_union = v != 0; return RT_OK;
+    case RT_OPT_LB_SCALE:
+        if (v < 0 || v > 1e6) return RT_E_ARG;
+        c->opt_lb_scale = v;
+        return RT_OK;
+    case RT_OPT_DCOV_NEAR:
+        if (v < 0 || (v > 0 && v < 1.0) || v > 1e6) return RT_E_ARG;
+        c->opt_dcov_near = v;
+        return RT_OK;
+    case RT_OPT_CB_INLINE_MAX_MB:
+        if (v < 0) return RT_E_ARG;
+        c->opt_cb_inline_mb = v;
+        return RT_OK;
+    default: return RT_E_ARG;
+    }
+}
+
+RT_EXPORT int rt_get_option(rt_ctx* c, int32_t opt, double* v)
+{
+    if (!c || !v) return RT_E_ARG;
+    switch (opt) {
+    case RT_OPT_LIGHT_BUFFER: *v = c->opt_light_buffer; return RT_OK;
+    case RT_OPT_CAMERA_BUFFER: *v = c->opt_camera_buffer ? 1 : 0; return RT_OK;
+    case RT_OPT_UNION_PRETEST: *v = c->opt_union ? 1 : 0; return RT_OK;
+    case RT_OPT_LB_SCALE: *v = c->opt_lb_scale; return RT_OK;
+    case RT_OPT_DCOV_NEAR: *v = c->opt_dcov_near; return RT_OK;
+    case RT_OPT_CB_INLINE_MAX_MB: *v = c->opt_cb_inline_mb; return RT_OK;
+    default: return RT_E_ARG;
+    }
+}
+
+RT_EXPORT int rt_set_far_ladder(rt_ctx* c, const double* f, int32_t n)
+{
+    if (!c || n > 8) return RT_E_ARG;
+    if (n < 0) {
+        if (f) return RT_E_ARG;
+        c->far_ladder = {2.5, 6.0, 16.0, 64.0};
+        return RT_OK;
+    }
+    if (n > 0 && !f) return RT_E_ARG;
+    for (int i = 0; i < n; ++i)
+        if (!(f[i] >= 1.0 && f[i] <= 1e6) || (i > 0 && !(f[i] > f[i - 1]))) return RT_E_ARG;
+    c->far_ladder.assign(f, f + n);
     return RT_OK;
 }
 
@@ -468,8 +633,9 @@ RT_EXPORT void rt_destroy(rt_ctx* c)
     if (!c) return;
     if (c->stream) {
         (void)hipSetDevice(c->device);
-        (void)hipStreamSynchronize(c->stream);
+        (void)sync_all(c);
     }
+    free_retired(c);
     hipFree(c->d_geom);
     hipFree(c->d_mat);
     hipFree(c->d_lights);
@@ -498,6 +664,12 @@ RT_EXPORT void rt_destroy(rt_ctx* c)
     hipFree(c->d_scratch);
     if (c->ev0) hipEventDestroy(c->ev0);
     if (c->ev1) hipEventDestroy(c->ev1);
+    if (c->ev_fence) hipEventDestroy(c->ev_fence);
+    if (c->ev_state) hipEventDestroy(c->ev_state);
+    if (c->ev_cb0) hipEventDestroy(c->ev_cb0);
+    if (c->ev_cb1) hipEventDestroy(c->ev_cb1);
+    if (c->h_word) hipHostFree(c->h_word);
+    hipFree(c->d_scan);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
 }
@@ -556,19 +728,6 @@ static void cluster_order(std::vector<float>& tri, int n_opaque)
     tri.swap(out);
 }
 
-// RT_AMD_LIGHTBUF (diagnostic/A-B switch): 0 = never build or use the light
-// buffer (wave-level shadow culling), 2 = only for lists above
-// kClusterMinTriangles; unset/1 = every depth-0 scene with opaque
-// triangles (same-box A/B since the exact dmin and the camera buffer: C1
-// -8%, C2 -6%, C4 -6% against the wave path).  RT_AMD_LB_SCALE scales the
-// cell count.
-static int lb_mode()
-{
-    const char* v = getenv("RT_AMD_LIGHTBUF");
-    if (!v || !*v) return 1;
-    return atoi(v);
-}
-
 // Light buffer of every light (shadow_opaque_lb, lb_cone): resolution from
 // the median angular radius of the light's triangle cones (cell half-width
 // ~ that radius), nearest-first cell lists built on the device in two
@@ -586,16 +745,13 @@ static int lb_mode()
 // level): F = RT_DCOV_FACTOR_SMALL — far ground-plane points then stay
 // in the buffer (A/B against 4: 16 / 32 / 64 / 256 = C2 -8 / -10 / -11 /
 // +1%, C4 -8 / -8 / -6 / +5%; C1 and the bounce scenes flat).
-// RT_AMD_DCOV_NEAR / RT_AMD_DCOV_FAR (a comma list) override the big-list
-// ladder at upload (tests, A/B).
+// RT_OPT_DCOV_NEAR and rt_set_far_ladder override the big-list ladder at
+// upload (tests, A/B).
 #ifndef RT_DCOV_FACTOR
 #define RT_DCOV_FACTOR 1.25
 #endif
 #ifndef RT_DCOV_FACTOR_SMALL
 #define RT_DCOV_FACTOR_SMALL 32.0
-#endif
-#ifndef RT_DCOV_FACTOR_FAR  // the far buffers' factors, comma-separated, rising
-#define RT_DCOV_FACTOR_FAR "2.5,6,16,64"
 #endif
 // Slots: one buffer per entry of `cones` (a light's cone records, built for
 // the distance dcov[j]): the lights, then (big lists) their far buffers.
@@ -605,27 +761,33 @@ static int lb_mode()
 static int lb_build(rt_ctx* c, int ntr, int n_opaque, const std::vector<const float4*>& cones,
                     const std::vector<double>& dcov)
 {
+    hipStream_t st = c->stream;
     const int nl = (int)cones.size();
     const auto t0 = std::chrono::steady_clock::now();
-    const char* sc = getenv("RT_AMD_LB_SCALE");
     // cells of ~1/4 the median cone radius: best of 1-8 on C3 and C5; and
     // no coarser than 128 cells per face edge (small scenes: C2 -3.3%, C4
     // -2.5% against their 16-48, flat from 192 to 512).  An explicit
-    // RT_AMD_LB_SCALE (A/B, the stress tests' coarse cells) sets R alone.
-    const bool scale_set = sc && *sc;
-    const double scale = scale_set ? atof(sc) : 4.0;
+    // RT_OPT_LB_SCALE (A/B, the stress tests' coarse cells) sets R alone.
+    const bool scale_set = c->opt_lb_scale > 0.0;
+    const double scale = scale_set ? c->opt_lb_scale : 4.0;
     const int r_min = scale_set ? kLbGroup : RT_LB_RMIN;
-    struct Build {
+    // Slot j's pieces in the concatenated device arrays: its triangles in
+    // dmin order (perm) and its dcap list (dperm); its supercell counts /
+    // offsets (nsup + 1 words from sob) and cell offsets (ncell + 1 words
+    // from ob: the slot's lb_off) — each slot's last word stays 0 as a
+    // count, so ONE exclusive scan over a whole array gives every slot its
+    // absolute offsets, the last word its end.
+    struct Slot {
         int R = 16;
-        std::vector<int> dperm;
-        std::vector<unsigned> soff, ccount;
-        int* d_slists = nullptr;
-        unsigned* d_soff = nullptr;
+        size_t perm0 = 0, nperm = 0, dperm0 = 0, ndperm = 0, sob = 0, ob = 0;
+        unsigned nsup = 0, ncell = 0;
     };
-    std::vector<Build> B((size_t)nl);
-    std::vector<float4> h((size_t)ntr * 2);
+    std::vector<Slot> B((size_t)nl);
+    std::vector<int> perm_all, dperm_all;
+    size_t sob = 0, ob = 0;
     int* d_perm = nullptr;
-    unsigned* d_cnt = nullptr;
+    unsigned* d_soff = nullptr;
+    int* d_slists = nullptr;
     int rc = RT_OK;
     auto fail = [&](hipError_t e, const char* what) {
         if (rc == RT_OK) rc = hip_fail(c, e, what);
@@ -636,19 +798,22 @@ static int lb_build(rt_ctx* c, int ntr, int n_opaque, const std::vector<const fl
         if (e_ != hipSuccess) { fail(e_, #call); goto done; } \
     } while (0)
     {
-        size_t total = 0, off_words = 0, dcap_total = 0;
-        LB_TRY(hipMalloc(&d_perm, std::max<size_t>(ntr, 1) * sizeof(int)));
+        // 1. the cone records of every slot (c0, c1 per triangle): one sync
+        std::vector<float4> h((size_t)nl * ntr * 2);
+        for (int j = 0; j < nl; ++j)
+            LB_TRY(hipMemcpyAsync(h.data() + (size_t)j * ntr * 2, cones[j], (size_t)ntr * 2 * sizeof(float4),
+                                  hipMemcpyDeviceToHost, st));
+        LB_TRY(hipStreamSynchronize(st));
         for (int j = 0; j < nl; ++j) {
-            Build& b = B[j];
-            const float4* cone = cones[j];
-            LB_TRY(hipMemcpy(h.data(), cone, h.size() * sizeof(float4), hipMemcpyDeviceToHost));
+            Slot& b = B[j];
+            const float4* hj = h.data() + (size_t)j * ntr * 2;
             std::vector<double> T;
-            std::vector<int> perm;
+            std::vector<int> perm, dperm;
             for (int k = 0; k < n_opaque; ++k) {
-                const float4 c0 = h[2 * k], c1 = h[2 * k + 1];
+                const float4 c0 = hj[2 * k], c1 = hj[2 * k + 1];
                 if (c0.w > 0.0f && c0.w <= 1.0f) T.push_back(std::acos((double)c0.w));
                 if (c0.w > 0.0f && c1.x < (float)dcov[j]) perm.push_back(k);
-                if (!(c1.z >= (float)dcov[j])) b.dperm.push_back(k);
+                if (!(c1.z >= (float)dcov[j])) dperm.push_back(k);
             }
             if (!T.empty()) {
                 std::nth_element(T.begin(), T.begin() + T.size() / 2, T.end());
@@ -657,95 +822,116 @@ static int lb_build(rt_ctx* c, int ntr, int n_opaque, const std::vector<const fl
                 b.R = std::min(1024, std::max(r_min, b.R));
             }
             std::sort(perm.begin(), perm.end(), [&](int x, int y) {
-                return h[2 * x + 1].x < h[2 * y + 1].x || (h[2 * x + 1].x == h[2 * y + 1].x && x < y);
+                return hj[2 * x + 1].x < hj[2 * y + 1].x || (hj[2 * x + 1].x == hj[2 * y + 1].x && x < y);
             });
-            auto key = [&](int k) { const float z = h[2 * k + 1].z; return z == z ? z : -INFINITY; };
-            std::sort(b.dperm.begin(), b.dperm.end(),
+            auto key = [&](int k) { const float z = hj[2 * k + 1].z; return z == z ? z : -INFINITY; };
+            std::sort(dperm.begin(), dperm.end(),
                       [&](int x, int y) { return key(x) < key(y) || (key(x) == key(y) && x < y); });
-            const int G = b.R / kLbGroup;
-            const unsigned nsup = 6u * G * G, ncell = 6u * b.R * b.R;
-            if (!perm.empty()) LB_TRY(hipMemcpy(d_perm, perm.data(), perm.size() * sizeof(int), hipMemcpyHostToDevice));
-            hipFree(d_cnt);
-            d_cnt = nullptr;
-            LB_TRY(hipMalloc(&d_cnt, std::max(nsup, ncell) * sizeof(unsigned)));
-            hipLaunchKernelGGL(rt_lb_super, dim3(nsup), dim3(256), 0, 0, cone, ntr, d_perm, (int)perm.size(), b.R,
-                               (float)dcov[j], nullptr, d_cnt, nullptr);
-            LB_TRY(hipGetLastError());
-            b.soff.assign(nsup + 1, 0u);
-            LB_TRY(hipMemcpy(b.soff.data() + 1, d_cnt, nsup * sizeof(unsigned), hipMemcpyDeviceToHost));
-            for (unsigned q = 0; q < nsup; ++q) b.soff[q + 1] += b.soff[q];
-            LB_TRY(hipMalloc(&b.d_soff, (nsup + 1) * sizeof(unsigned)));
-            LB_TRY(hipMemcpy(b.d_soff, b.soff.data(), (nsup + 1) * sizeof(unsigned), hipMemcpyHostToDevice));
-            LB_TRY(hipMalloc(&b.d_slists, std::max(b.soff[nsup], 1u) * sizeof(int)));
-            hipLaunchKernelGGL(rt_lb_super, dim3(nsup), dim3(256), 0, 0, cone, ntr, d_perm, (int)perm.size(), b.R,
-                               (float)dcov[j], b.d_soff, nullptr, b.d_slists);
-            LB_TRY(hipGetLastError());
-            hipLaunchKernelGGL(rt_lb_cells, dim3(nsup), dim3(256), 0, 0, cone, ntr, c->d_tri, b.R, (float)dcov[j],
-                               b.d_soff, b.d_slists, nullptr, d_cnt, nullptr);
-            LB_TRY(hipGetLastError());
-            b.ccount.resize(ncell);
-            LB_TRY(hipMemcpy(b.ccount.data(), d_cnt, ncell * sizeof(unsigned), hipMemcpyDeviceToHost));
-            for (unsigned q = 0; q < ncell; ++q) total += b.ccount[q];
-            off_words += ncell + 1;
-            dcap_total += b.dperm.size();
+            b.perm0 = perm_all.size();
+            b.nperm = perm.size();
+            perm_all.insert(perm_all.end(), perm.begin(), perm.end());
+            b.dperm0 = dperm_all.size();
+            b.ndperm = dperm.size();
+            dperm_all.insert(dperm_all.end(), dperm.begin(), dperm.end());
+            const unsigned G = (unsigned)(b.R / kLbGroup);
+            b.nsup = 6u * G * G;
+            b.ncell = 6u * (unsigned)b.R * (unsigned)b.R;
+            b.sob = sob;
+            sob += b.nsup + 1;
+            b.ob = ob;
+            ob += b.ncell + 1;
         }
+        // 2. device arrays; supercell lists (counts, scan, fill)
+        const size_t np = perm_all.size() + dperm_all.size();
+        LB_TRY(hipMalloc(&d_perm, std::max<size_t>(np, 1) * sizeof(int)));
+        if (!perm_all.empty())
+            LB_TRY(hipMemcpyAsync(d_perm, perm_all.data(), perm_all.size() * sizeof(int), hipMemcpyHostToDevice, st));
+        if (!dperm_all.empty())
+            LB_TRY(hipMemcpyAsync(d_perm + perm_all.size(), dperm_all.data(), dperm_all.size() * sizeof(int),
+                                  hipMemcpyHostToDevice, st));
+        LB_TRY(hipMalloc(&d_soff, sob * sizeof(unsigned) + sizeof(unsigned)));
+        LB_TRY(hipMalloc(&c->d_lb_off, ob * sizeof(unsigned) + sizeof(unsigned)));
+        {
+            const int src = ensure_scan(c, scan_scratch(std::max(sob, ob)));
+            if (src) {
+                rc = src;
+                goto done;
+            }
+        }
+        LB_TRY(hipMemsetAsync(d_soff, 0, sob * sizeof(unsigned), st));
+        LB_TRY(hipMemsetAsync(c->d_lb_off, 0, ob * sizeof(unsigned), st));
+        for (int j = 0; j < nl; ++j) {
+            const Slot& b = B[j];
+            hipLaunchKernelGGL(rt_lb_super, dim3(b.nsup), dim3(256), 0, st, cones[j], ntr, d_perm + b.perm0,
+                               (int)b.nperm, b.R, (float)dcov[j], nullptr, d_soff + b.sob, nullptr);
+            LB_TRY(hipGetLastError());
+        }
+        unsigned long long* tot = nullptr;
+        LB_TRY(scan_u32(d_soff, (unsigned)sob, d_soff, (unsigned long long*)c->d_scan, st, &tot));
+        LB_TRY(hipMemcpyAsync(c->h_word, tot, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+        LB_TRY(hipStreamSynchronize(st));
+        const unsigned long long nsl = *c->h_word;
+        if (nsl > 0xFFFFFFF0ull) {
+            c->err = "light buffer too large";
+            goto done;
+        }
+        LB_TRY(hipMalloc(&d_slists, std::max<size_t>(nsl, 1) * sizeof(int)));
+        for (int j = 0; j < nl; ++j) {
+            const Slot& b = B[j];
+            hipLaunchKernelGGL(rt_lb_super, dim3(b.nsup), dim3(256), 0, st, cones[j], ntr, d_perm + b.perm0,
+                               (int)b.nperm, b.R, (float)dcov[j], d_soff + b.sob, nullptr, d_slists);
+            LB_TRY(hipGetLastError());
+        }
+        // 3. cell lists (counts, scan into lb_off, fill) and the dcap lists
+        for (int j = 0; j < nl; ++j) {
+            const Slot& b = B[j];
+            hipLaunchKernelGGL(rt_lb_cells, dim3(b.nsup), dim3(256), 0, st, cones[j], ntr, c->d_tri, b.R,
+                               (float)dcov[j], d_soff + b.sob, d_slists, nullptr, c->d_lb_off + b.ob, nullptr);
+            LB_TRY(hipGetLastError());
+        }
+        LB_TRY(scan_u32(c->d_lb_off, (unsigned)ob, c->d_lb_off, (unsigned long long*)c->d_scan, st, &tot));
+        LB_TRY(hipMemcpyAsync(c->h_word, tot, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+        LB_TRY(hipStreamSynchronize(st));
+        const unsigned long long total = *c->h_word;
         if (total >= 0xFFFFFFF0ull / 4) {  // entry indices are 32-bit
             c->err = "light buffer too large";
             goto done;
         }
-        LB_TRY(hipMalloc(&c->d_lb_off, off_words * sizeof(unsigned)));
         LB_TRY(hipMalloc(&c->d_lb_ent, std::max<size_t>(total, 1) * kLbEnt * sizeof(float4)));
-        LB_TRY(hipMalloc(&c->d_lb_dcap, std::max<size_t>(dcap_total, 1) * kLbEnt * sizeof(float4)));
+        LB_TRY(hipMalloc(&c->d_lb_dcap, std::max<size_t>(dperm_all.size(), 1) * kLbEnt * sizeof(float4)));
         LB_TRY(hipMalloc(&c->d_lb_meta, std::max(nl, 1) * 2 * sizeof(float4)));
         std::vector<float4> meta((size_t)std::max(nl, 1) * 2);
-        size_t obase = 0, ebase = 0, dbase = 0;
         for (int j = 0; j < nl; ++j) {
-            Build& b = B[j];
-            const float4* cone = cones[j];
-            const unsigned G = b.R / kLbGroup, nsup = 6u * G * G, ncell = 6u * b.R * b.R;
-            std::vector<unsigned> off(ncell + 1);
-            size_t run = ebase;
-            for (unsigned q = 0; q < ncell; ++q) {
-                off[q] = (unsigned)run;
-                run += b.ccount[q];
-            }
-            off[ncell] = (unsigned)run;
-            LB_TRY(hipMemcpy(c->d_lb_off + obase, off.data(), off.size() * sizeof(unsigned), hipMemcpyHostToDevice));
-            hipLaunchKernelGGL(rt_lb_cells, dim3(nsup), dim3(256), 0, 0, cone, ntr, c->d_tri, b.R, (float)dcov[j],
-                               b.d_soff, b.d_slists, c->d_lb_off + obase, nullptr, c->d_lb_ent);
+            const Slot& b = B[j];
+            hipLaunchKernelGGL(rt_lb_cells, dim3(b.nsup), dim3(256), 0, st, cones[j], ntr, c->d_tri, b.R,
+                               (float)dcov[j], d_soff + b.sob, d_slists, c->d_lb_off + b.ob, nullptr, c->d_lb_ent);
             LB_TRY(hipGetLastError());
-            if (!b.dperm.empty()) {
-                LB_TRY(hipMemcpy(d_perm, b.dperm.data(), b.dperm.size() * sizeof(int), hipMemcpyHostToDevice));
-                hipLaunchKernelGGL(rt_lb_dcap, dim3((unsigned)((b.dperm.size() + 255) / 256)), dim3(256), 0, 0, cone,
-                                   c->d_tri, d_perm, (int)b.dperm.size(), c->d_lb_dcap + kLbEnt * dbase);
+            if (b.ndperm) {
+                hipLaunchKernelGGL(rt_lb_dcap, dim3((unsigned)((b.ndperm + 255) / 256)), dim3(256), 0, st, cones[j],
+                                   c->d_tri, d_perm + perm_all.size() + b.dperm0, (int)b.ndperm,
+                                   c->d_lb_dcap + kLbEnt * b.dperm0);
                 LB_TRY(hipGetLastError());
-                LB_TRY(hipDeviceSynchronize());  // d_perm is reused by the next light
             }
-            unsigned ob = (unsigned)obase, db = (unsigned)dbase, nd = (unsigned)b.dperm.size();
+            unsigned obj = (unsigned)b.ob, db = (unsigned)b.dperm0, nd = (unsigned)b.ndperm;
             float4 m0, m1 = make_float4((float)dcov[j], 0.f, 0.f, 0.f);
-            std::memcpy(&m0.x, &ob, 4);
+            std::memcpy(&m0.x, &obj, 4);
             std::memcpy(&m0.y, &db, 4);
             std::memcpy(&m0.z, &nd, 4);
             std::memcpy(&m0.w, &b.R, 4);
             meta[2 * j] = m0;
             meta[2 * j + 1] = m1;
-            obase += ncell + 1;
-            ebase = run;
-            dbase += b.dperm.size();
         }
-        LB_TRY(hipMemcpy(c->d_lb_meta, meta.data(), meta.size() * sizeof(float4), hipMemcpyHostToDevice));
-        LB_TRY(hipDeviceSynchronize());
+        LB_TRY(hipMemcpyAsync(c->d_lb_meta, meta.data(), meta.size() * sizeof(float4), hipMemcpyHostToDevice, st));
+        LB_TRY(hipStreamSynchronize(st));  // meta (host) outlives the copy; the temporaries are freed below
         c->lb_ready = true;
         c->lb_entries = total;
     }
 done:
 #undef LB_TRY
-    for (Build& b : B) {
-        hipFree(b.d_slists);
-        hipFree(b.d_soff);
-    }
+    if (rc != RT_OK || !c->lb_ready) (void)hipStreamSynchronize(st);
+    hipFree(d_slists);
+    hipFree(d_soff);
     hipFree(d_perm);
-    hipFree(d_cnt);
     c->lb_build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     if (rc == RT_OK && !c->lb_ready) {  // too large: run without it
         hipFree(c->d_lb_off);
@@ -766,6 +952,14 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
     if (s->n_lights > 0 && !s->lights) return RT_E_ARG;
     if (!c->stream) return RT_E_STATE;
     HIP_TRY(c, hipSetDevice(c->device));
+    // nothing in flight may still read the buffers replaced below
+    if (int rc = sync_all(c)) return rc;
+    free_retired(c);
+    const auto tu0 = std::chrono::steady_clock::now();
+    auto since = [](std::chrono::steady_clock::time_point t) {
+        return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+    };
+    hipStream_t st = c->stream;
     const int n = s->n_surfaces, nl = s->n_lights;
     std::vector<float> geom((size_t)std::max(n, 1) * 16, 0.0f), mat((size_t)std::max(n, 1) * 12, 0.0f),
         lig((size_t)std::max(nl, 1) * 8, 0.0f);
@@ -884,6 +1078,7 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
     c->d_uni = nullptr;
     c->cb_valid = false;  // buffers are kept (reallocated on demand)
     c->cam_valid = false;
+    c->lb_build_ms = 0.0;
     c->d_geom = c->d_mat = c->d_lights = c->d_tri = c->d_plane = c->d_quad = nullptr;
     c->d_translucent = nullptr;
     c->uploaded = false;
@@ -956,22 +1151,13 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
     HIP_TRY(c, up((void**)&c->d_tricoef, coef.data(), coef.size() * sizeof(float)));
     HIP_TRY(c, hipMalloc((void**)&c->d_cone_cam, std::max<size_t>(ntr, 1) * kConeRec * sizeof(float4)));
     HIP_TRY(c, hipMalloc((void**)&c->d_cone_light, std::max<size_t>(ntr * nl, 1) * kConeRec * sizeof(float4)));
+    c->upload_parts_ms[0] = since(tu0);
+    const auto tp0 = std::chrono::steady_clock::now();
     std::vector<double> lb_dcov((size_t)std::max(nl, 0), 0.0);
-    // RT_AMD_DCOV_NEAR / RT_AMD_DCOV_FAR override the big-list factors (tests:
-    // force lanes into the far buffer and beyond it)
-    const char* env_near = getenv("RT_AMD_DCOV_NEAR");
-    const char* env_far = getenv("RT_AMD_DCOV_FAR");
-    const double fac_near = env_near && *env_near ? atof(env_near) : RT_DCOV_FACTOR;
-    std::vector<double> fac_far;
-    {
-        std::string lv = env_far && *env_far ? env_far : RT_DCOV_FACTOR_FAR;
-        for (size_t a = 0; a <= lv.size();) {
-            size_t b = lv.find(',', a);
-            if (b == std::string::npos) b = lv.size();
-            if (b > a) fac_far.push_back(atof(lv.substr(a, b - a).c_str()));
-            a = b + 1;
-        }
-    }
+    // RT_OPT_DCOV_NEAR / rt_set_far_ladder override the big-list factors
+    // (tests: force lanes into the far buffers and beyond them)
+    const double fac_near = c->opt_dcov_near > 0.0 ? c->opt_dcov_near : RT_DCOV_FACTOR;
+    const std::vector<double> fac_far = c->far_ladder;
     const double dfac = ntr > (size_t)kClusterMinTriangles ? fac_near : RT_DCOV_FACTOR_SMALL;
     for (int j = 0; j < nl && ntr > 0; ++j) {
         const float* l = s->lights + 7 * (size_t)j;
@@ -982,7 +1168,7 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
             for (int a = 0; a < 3; ++a) d2 += ((double)sph[4 * k + a] - l[a]) * ((double)sph[4 * k + a] - l[a]);
             far = std::max(far, std::sqrt(d2) + sph[4 * k + 3]);
         }
-        hipLaunchKernelGGL(rt_cone_prepass, dim3((unsigned)((ntr + 255) / 256)), dim3(256), 0, 0, c->d_tri, c->d_trisph,
+        hipLaunchKernelGGL(rt_cone_prepass, dim3((unsigned)((ntr + 255) / 256)), dim3(256), 0, st, c->d_tri, c->d_trisph,
                            c->d_trinrm, c->d_tricoef, (int)ntr, l[0], l[1], l[2], 0, (float)(dfac * far),
                            c->d_cone_light + kConeRec * ntr * j);
         HIP_TRY(c, hipGetLastError());
@@ -993,7 +1179,7 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
         HIP_TRY(c, hipMalloc((void**)&c->d_clu_cam, (size_t)c->n_clu * 4 * sizeof(float4)));
         HIP_TRY(c, hipMalloc((void**)&c->d_clu_light, std::max<size_t>((size_t)c->n_clu * nl, 1) * 2 * sizeof(float4)));
         for (int j = 0; j < nl; ++j) {
-            hipLaunchKernelGGL(rt_cluster_prepass, dim3((unsigned)((c->n_clu + 63) / 64)), dim3(64), 0, 0,
+            hipLaunchKernelGGL(rt_cluster_prepass, dim3((unsigned)((c->n_clu + 63) / 64)), dim3(64), 0, st,
                                c->d_cone_light + kConeRec * ntr * j, (int)ntr, c->n_clu,
                                c->d_clu_light + 2 * (size_t)c->n_clu * j);
             HIP_TRY(c, hipGetLastError());
@@ -1003,7 +1189,7 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
         // union records: [camera (filled when the camera is set)] [light 0] ...
         HIP_TRY(c, hipMalloc((void**)&c->d_uni, (size_t)(nl + 1) * 2 * sizeof(float4)));
         for (int j = 0; j < nl && n_tri_o > 0; ++j) {
-            hipLaunchKernelGGL(rt_cluster_prepass, dim3(1), dim3(64), 0, 0, c->d_cone_light + kConeRec * ntr * j,
+            hipLaunchKernelGGL(rt_cluster_prepass, dim3(1), dim3(64), 0, st, c->d_cone_light + kConeRec * ntr * j,
                                n_tri_o, 1, c->d_uni + 2 * (1 + (size_t)j), n_tri_o);
             HIP_TRY(c, hipGetLastError());
         }
@@ -1013,11 +1199,14 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
                 nev[2 * j] = make_float4(0.f, 0.f, 0.f, 2.0f);
                 nev[2 * j + 1] = make_float4(INFINITY, 0.f, INFINITY, 0.f);
             }
-            if (nl) HIP_TRY(c, hipMemcpy(c->d_uni + 2, nev.data(), nev.size() * sizeof(float4), hipMemcpyHostToDevice));
+            if (nl) HIP_TRY(c, hipMemcpyAsync(c->d_uni + 2, nev.data(), nev.size() * sizeof(float4), hipMemcpyHostToDevice, st));
+            HIP_TRY(c, hipStreamSynchronize(st));  // nev outlives the copy
         }
     }
-    HIP_TRY(c, hipDeviceSynchronize());
-    const int lbm = lb_mode();  // built only where launch() will use it
+    HIP_TRY(c, hipStreamSynchronize(st));
+    c->upload_parts_ms[1] = since(tp0);
+    const auto tl0 = std::chrono::steady_clock::now();
+    const int lbm = c->opt_light_buffer;  // built only where launch() will use it
     if (ntr > 0 && nl > 0 && n_tri_o > 0 && opaque && (lbm == 1 || (lbm == 2 && ntr > (size_t)kClusterMinTriangles))) {
         std::vector<const float4*> cones;
         for (int j = 0; j < nl; ++j) cones.push_back(c->d_cone_light + kConeRec * ntr * j);
@@ -1035,20 +1224,20 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
                     const float* l = s->lights + 7 * (size_t)j;
                     const double dfar = lb_dcov[j] / dfac * fac_far[v];
                     float4* out = d_cone_far + kConeRec * ntr * (v * nl + j);
-                    hipLaunchKernelGGL(rt_cone_prepass, dim3((unsigned)((ntr + 255) / 256)), dim3(256), 0, 0,
+                    hipLaunchKernelGGL(rt_cone_prepass, dim3((unsigned)((ntr + 255) / 256)), dim3(256), 0, st,
                                        c->d_tri, c->d_trisph, c->d_trinrm, c->d_tricoef, (int)ntr, l[0], l[1], l[2], 0,
                                        (float)dfar, out);
                     HIP_TRY(c, hipGetLastError());
                     cones.push_back(out);
                     dcov.push_back((double)(float)dfar);
                 }
-            HIP_TRY(c, hipDeviceSynchronize());
         }
         const int rc = lb_build(c, (int)ntr, n_tri_o, cones, dcov);
         hipFree(d_cone_far);
         if (rc) return rc;
         c->lb_levels = c->lb_ready ? 1 + (int)nlev : 0;
     }
+    c->upload_parts_ms[2] = since(tl0);
     HIP_TRY(c, hipMalloc(&c->d_geom, geom.size() * sizeof(float)));
     HIP_TRY(c, hipMalloc(&c->d_mat, mat.size() * sizeof(float)));
     HIP_TRY(c, hipMalloc(&c->d_lights, lig.size() * sizeof(float)));
@@ -1067,6 +1256,7 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
     c->shadow_split = opaque ? 1 : 0;
     c->k_max = kmax;
     c->uploaded = true;
+    c->upload_parts_ms[3] = since(tu0);
     return RT_OK;
 }
 
@@ -1146,14 +1336,6 @@ static int frame_rows(const rt_frame* f)
     return f->row_end - f->row_begin;
 }
 
-// RT_AMD_CAMBUF (A/B switch): 0 = no camera buffer; unset/1 = for depth-0
-// scenes with triangles.
-static bool cb_mode()
-{
-    const char* v = getenv("RT_AMD_CAMBUF");
-    return !(v && *v == '0');
-}
-
 static void cb_key_of(const rt_frame* f, float* key)
 {
     std::memcpy(key, f->cam_pos, 3 * sizeof(float));
@@ -1188,15 +1370,20 @@ static void frame_dev(const rt_frame* f, FrameDev& F)
     F.band_index = f->band_index;
 }
 
+// Does frame f need the per-camera prepasses (the camera position moved)?
+// A camera already prepared without every tricam record — a bounce frame
+// of a big scene — is prepared again for the camera buffer.
+static bool camera_needs_prepass(const rt_ctx* c, const rt_frame* f, bool all_tricam)
+{
+    return c->n_tri > 0 && !(c->cam_valid && std::memcmp(c->cam_key, f->cam_pos, sizeof c->cam_key) == 0 &&
+                             (!all_tricam || c->tricam_all));
+}
+
 // Per-camera prepasses (when the camera position moved): camera-ray
 // triangle values, camera cone records, union / cluster records.
 static int camera_prepass(rt_ctx* c, const rt_frame* f, hipStream_t st, bool all_tricam)
 {
-    // (a camera already prepared without every tricam record — a bounce
-    // frame of a big scene — is prepared again for the camera buffer)
-    if (c->n_tri <= 0 || (c->cam_valid && std::memcmp(c->cam_key, f->cam_pos, sizeof c->cam_key) == 0 &&
-                          (!all_tricam || c->tricam_all)))
-        return RT_OK;
+    if (!camera_needs_prepass(c, f, all_tricam)) return RT_OK;
     const float* cp = f->cam_pos;
     if (all_tricam || c->n_tri <= kTricamMaxTriangles) {
         hipLaunchKernelGGL(rt_camera_prepass, dim3((c->n_tri + 255) / 256), dim3(256), 0, st, c->d_tri, c->n_tri,
@@ -1235,76 +1422,82 @@ static SceneDev scene_dev(rt_ctx* c, bool lbuf, bool cbuf)
                     c->d_clu_light, c->n_clu, c->n_surf, c->n_lights, c->n_tri, c->n_plane, c->n_quad,
                     c->n_tri_opaque, c->n_plane_opaque, c->n_quad_opaque, c->n_translucent, c->shadow_split,
                     lbuf ? c->lb_levels : 0, c->d_lb_off, c->d_lb_ent, c->d_lb_dcap, c->d_lb_meta,
-                    (c->d_uni && !getenv("RT_AMD_NO_UNION")) ? c->d_uni : nullptr,
+                    (c->d_uni && c->opt_union) ? c->d_uni : nullptr,
                     c->d_cb_off, c->d_cb_ent, c->d_cb_flag, cbuf ? c->cb_tiles_x : 0,
                     c->cb_inline ? c->d_cb_rec : nullptr};
 }
 
-// Camera buffer for the frame's camera (synchronous: the list sizes come
-// back to the host for the offsets).  Needs the camera prepass done.
+// Camera buffer for the frame's camera, on stream st: per-tile counts, a
+// device scan into the offsets, one 8-byte read of the total (the entry
+// array's size), then the fill, keys and inline records.  Needs the camera
+// prepass done and st ordered after every render that may read the buffers.
 static int cb_build(rt_ctx* c, const rt_frame* f, hipStream_t st)
 {
     const auto t0 = std::chrono::steady_clock::now();
     const int tx = (f->width + 7) / 8, ty = (f->height + 7) / 8, nt = tx * ty;
     if (nt > c->cb_ntiles || !c->d_cb_off) {
-        hipFree(c->d_cb_off);
-        hipFree(c->d_cb_flag);
+        release(c, c->d_cb_off);
+        release(c, c->d_cb_flag);
         c->d_cb_off = nullptr;
         c->d_cb_flag = nullptr;
+        c->cb_ntiles = 0;
         HIP_TRY(c, hipMalloc(&c->d_cb_off, (size_t)(nt + 1) * sizeof(unsigned)));
         HIP_TRY(c, hipMalloc(&c->d_cb_flag, (size_t)std::max(nt, 1) * sizeof(unsigned)));
         c->cb_ntiles = nt;
     }
+    if (int rc = ensure_scan(c, scan_scratch((size_t)nt))) return rc;
+    c->cb_valid = false;
     c->cb_tiles_x = tx;
     SceneDev S = scene_dev(c, false, true);
     FrameDev F;
     frame_dev(f, F);
     dim3 grid((tx + 1) / 2, (ty + 1) / 2);
-    unsigned* cnt = c->d_cb_off + 1;  // counts land one slot up, scanned in place on the host
-    hipLaunchKernelGGL(rt_cb_build<false>, grid, dim3(256), 0, st, S, F, (const unsigned*)nullptr, cnt, c->d_cb_flag,
-                       (int2*)nullptr);
+    HIP_TRY(c, hipEventRecord(c->ev_cb0, st));
+    hipLaunchKernelGGL(rt_cb_build<false>, grid, dim3(256), 0, st, S, F, (const unsigned*)nullptr, c->d_cb_off,
+                       c->d_cb_flag, (int2*)nullptr);
     HIP_TRY(c, hipGetLastError());
-    std::vector<unsigned> off((size_t)nt + 1, 0u);
-    HIP_TRY(c, hipMemcpyAsync(off.data() + 1, cnt, (size_t)nt * sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    unsigned long long* tot = nullptr;
+    HIP_TRY(c, scan_u32(c->d_cb_off, (unsigned)nt, c->d_cb_off, (unsigned long long*)c->d_scan, st, &tot));
+    HIP_TRY(c, hipMemcpyAsync(c->h_word, tot, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
     HIP_TRY(c, hipStreamSynchronize(st));
-    size_t run = 0;
-    for (int t = 0; t < nt; ++t) {
-        run += off[t + 1];
-        if (run > 0xFFFFFFF0ull) {
-            c->err = "camera buffer too large";
-            return RT_E_UNSUPPORTED;
-        }
-        off[t + 1] = (unsigned)run;
+    const unsigned long long run = *c->h_word;
+    if (run > 0xFFFFFFF0ull) {
+        c->err = "camera buffer too large";
+        return RT_E_UNSUPPORTED;
     }
+    const bool want_inline = run > 0 && (double)run * 4 * sizeof(float4) <= c->opt_cb_inline_mb * 1048576.0;
     if (run > c->cb_cap || !c->d_cb_ent) {
-        hipFree(c->d_cb_ent);
-        hipFree(c->d_cb_rec);
+        release(c, c->d_cb_ent);
         c->d_cb_ent = nullptr;
-        c->d_cb_rec = nullptr;
+        c->cb_cap = 0;
         HIP_TRY(c, hipMalloc(&c->d_cb_ent, std::max<size_t>(run, 1) * sizeof(int2)));
-        if (run * 4 * sizeof(float4) <= ((size_t)128 << 20))
-            HIP_TRY(c, hipMalloc(&c->d_cb_rec, std::max<size_t>(run, 1) * 4 * sizeof(float4)));
         c->cb_cap = std::max<size_t>(run, 1);
     }
-    HIP_TRY(c, hipMemcpyAsync(c->d_cb_off, off.data(), off.size() * sizeof(unsigned), hipMemcpyHostToDevice, st));
+    if (want_inline && (run > c->cb_rec_cap || !c->d_cb_rec)) {
+        release(c, c->d_cb_rec);
+        c->d_cb_rec = nullptr;
+        c->cb_rec_cap = 0;
+        HIP_TRY(c, hipMalloc(&c->d_cb_rec, std::max<size_t>(run, 1) * 4 * sizeof(float4)));
+        c->cb_rec_cap = std::max<size_t>(run, 1);
+    }
     hipLaunchKernelGGL(rt_cb_build<true>, grid, dim3(256), 0, st, S, F, (const unsigned*)c->d_cb_off, (unsigned*)nullptr,
                        c->d_cb_flag, c->d_cb_ent);
     HIP_TRY(c, hipGetLastError());
     hipLaunchKernelGGL(rt_cb_keys, dim3((nt + 255) / 256), dim3(256), 0, st, (const unsigned*)c->d_cb_off, nt,
                        c->d_cb_ent);
     HIP_TRY(c, hipGetLastError());
-    // (d_cb_rec exists only if it was sized when the capacity last grew)
-    c->cb_inline = run > 0 && c->d_cb_rec && run * 4 * sizeof(float4) <= ((size_t)128 << 20);
+    c->cb_inline = want_inline;
     if (c->cb_inline) {
         hipLaunchKernelGGL(rt_cb_expand, dim3((unsigned)((run + 255) / 256)), dim3(256), 0, st,
                            (const int2*)c->d_cb_ent, (unsigned)run, (const float4*)c->d_tricam, c->d_cb_rec);
         HIP_TRY(c, hipGetLastError());
     }
-    HIP_TRY(c, hipStreamSynchronize(st));  // off[] (host) must outlive the copy
+    HIP_TRY(c, hipEventRecord(c->ev_cb1, st));
     cb_key_of(f, c->cb_key);
     c->cb_valid = true;
     c->cb_entries = run;
-    c->cb_build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    c->cb_host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    c->cb_timed = true;
     return RT_OK;
 }
 
@@ -1316,35 +1509,78 @@ static bool cb_matches(const rt_ctx* c, const rt_frame* f)
     return std::memcmp(key, c->cb_key, sizeof key) == 0;
 }
 
-// allow_build: synchronous renders may (re)build the camera buffer; the
-// async path (no host sync, capturable) uses it only when it is current.
+static bool frame_ok(const rt_frame* f)
+{
+    return !(f->width <= 0 || f->height <= 0 || f->row_begin < 0 || f->row_end > f->height ||
+             f->row_begin > f->row_end || f->max_bounces < 0 ||
+             (f->band_rows != 0 && rt_band_rows(f->height, f->band_rows, f->band_count, f->band_index) < 0));
+}
+
+// Make the per-camera state current for frame f, ordered on stream st.
+// sync_path: a synchronous call on c->stream (fenced behind every async
+// render at its start), which may also build the camera buffer.  Async:
+// a camera prepass fences st behind the other streams' renders and marks
+// the state as written on st; otherwise st waits for a pending write made
+// on another stream.  Capturing: nothing may be written (RT_E_STATE).
+static int prepare_state(rt_ctx* c, const rt_frame* f, hipStream_t st, bool sync_path, bool capturing, bool cb_want)
+{
+    if (!sync_path) {
+        if (int rc = wait_state(c, st)) return rc;
+    }
+    const bool need_prep = camera_needs_prepass(c, f, cb_want);
+    const bool need_cb = sync_path && cb_want && !(cb_matches(c, f) && !need_prep);
+    if (capturing) {
+        if (need_prep) {
+            c->err = "hipGraph capture: the frame's camera is not prepared (rt_render or rt_prepare_camera first)";
+            return RT_E_STATE;
+        }
+        return RT_OK;
+    }
+    if (need_prep) {
+        if (!sync_path) {
+            if (int rc = fence_async(c, st)) return rc;
+        }
+        if (int rc = camera_prepass(c, f, st, cb_want)) return rc;
+        if (!sync_path) {
+            HIP_TRY(c, hipEventRecord(c->ev_state, st));
+            c->state_stream = st;
+            c->state_pending = true;
+        }
+    }
+    if (need_cb) {
+        if (int rc = cb_build(c, f, st)) return rc;
+    }
+    return RT_OK;
+}
+
+// sync_path: rt_render / rt_render_float on c->stream (may build the camera
+// buffer); else rt_render_async on the caller's stream (never builds it).
 static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_dev, hipStream_t st, bool timed,
-                  bool allow_build = false)
+                  bool sync_path)
 {
     if (!c || !f) return RT_E_ARG;
     if (!c->uploaded) {
         c->err = "render before rt_upload_scene";
         return RT_E_STATE;
     }
-    if (f->width <= 0 || f->height <= 0 || f->row_begin < 0 || f->row_end > f->height ||
-        f->row_begin > f->row_end || f->max_bounces < 0 ||
-        (f->band_rows != 0 && rt_band_rows(f->height, f->band_rows, f->band_count, f->band_index) < 0)) {
+    if (!frame_ok(f)) {
         c->err = "bad rt_frame geometry";
         return RT_E_ARG;
     }
+    bool capturing = false;
+    if (!sync_path) {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        HIP_TRY(c, hipStreamIsCapturing(st, &cs));
+        capturing = cs != hipStreamCaptureStatusNone;
+    }
     const int depth = reachable_depth(c, f);
     int cap = 0, lb = 1;
-    const int mode = lb_mode();
+    const int mode = c->opt_light_buffer;
     const bool lbuf = c->lb_ready && (mode == 1 || (mode == 2 && c->n_tri > kClusterMinTriangles));
-    const bool cb_want = depth == 0 && c->n_tri > 0 && cb_mode();
+    const bool cb_want = depth == 0 && c->n_tri > 0 && c->opt_camera_buffer;
     const int rows = frame_rows(f);
     if (rows > 0) {
-        const int rc = camera_prepass(c, f, st, cb_want);
-        if (rc) return rc;
-        if (cb_want && allow_build && !cb_matches(c, f)) {
-            const int rc2 = cb_build(c, f, st);
-            if (rc2) return rc2;
-        }
+        if (int rc = prepare_state(c, f, st, sync_path, capturing, cb_want)) return rc;
     }
     const bool cbuf = cb_want && cb_matches(c, f);
     kernel_fn k = (f->flags & RT_FLAG_STATS) ? pick_kernel<true>(depth, c->n_tri, c->n_lights, lbuf, cbuf, cap, lb)
@@ -1367,12 +1603,21 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
     void* args[] = {&S, &F, &rgba_dev, &rgb_dev, &stats};
     HIP_TRY(c, hipLaunchKernel((const void*)k, grid, dim3(256), args, 0, st));
     if (timed) HIP_TRY(c, hipEventRecord(c->ev1, st));
+    if (capturing)
+        c->captured = true;
+    else if (!sync_path)
+        note_async(c, st);
     return RT_OK;
 }
 
 static int finish_sync(rt_ctx* c, const rt_frame* f, hipStream_t st, bool timed)
 {
     HIP_TRY(c, hipStreamSynchronize(st));
+    // c->stream waited for every async render enqueued before this call
+    // (fence_async), so none is in flight any more
+    c->async_streams.clear();
+    c->state_pending = false;
+    c->state_stream = nullptr;
     if (timed) {
         float ms = 0.f;
         HIP_TRY(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
@@ -1415,7 +1660,7 @@ static bool is_device_ptr(const void* p)
 static int ensure_scratch(rt_ctx* c, size_t bytes)
 {
     if (c->scratch_bytes >= bytes) return RT_OK;
-    hipFree(c->d_scratch);
+    release(c, c->d_scratch);
     c->d_scratch = nullptr;
     c->scratch_bytes = 0;
     HIP_TRY(c, hipMalloc(&c->d_scratch, bytes));
@@ -1427,6 +1672,10 @@ static int render_sync(rt_ctx* c, const rt_frame* f, void* out, bool as_float)
 {
     if (!c || !f || !out) return RT_E_ARG;
     HIP_TRY(c, hipSetDevice(c->device));
+    // every state write and render of this call comes after the async
+    // renders already enqueued on other streams
+    if (int rc = fence_async(c, c->stream)) return rc;
+    if (int rc = wait_state(c, c->stream)) return rc;
     const size_t px = (size_t)f->width * (size_t)std::max(0, frame_rows(f));
     const size_t bytes = px * (as_float ? 12 : 4);
     const bool dev = is_device_ptr(out);
@@ -1450,7 +1699,32 @@ RT_EXPORT int rt_render_float(rt_ctx* c, const rt_frame* f, float* rgb_out) { re
 RT_EXPORT int rt_render_async(rt_ctx* c, const rt_frame* f, uint8_t* rgba8_dev, float* rgb_dev, void* stream)
 {
     if (!c || !f) return RT_E_ARG;
-    return launch(c, f, (unsigned*)rgba8_dev, rgb_dev, (hipStream_t)stream, false);
+    HIP_TRY(c, hipSetDevice(c->device));
+    return launch(c, f, (unsigned*)rgba8_dev, rgb_dev, (hipStream_t)stream, false, false);
+}
+
+RT_EXPORT int rt_prepare_camera(rt_ctx* c, const rt_frame* f)
+{
+    if (!c || !f) return RT_E_ARG;
+    if (!c->uploaded) {
+        c->err = "rt_prepare_camera before rt_upload_scene";
+        return RT_E_STATE;
+    }
+    if (!frame_ok(f)) {
+        c->err = "bad rt_frame geometry";
+        return RT_E_ARG;
+    }
+    HIP_TRY(c, hipSetDevice(c->device));
+    if (int rc = fence_async(c, c->stream)) return rc;
+    if (int rc = wait_state(c, c->stream)) return rc;
+    const int depth = reachable_depth(c, f);
+    const bool cb_want = depth == 0 && c->n_tri > 0 && c->opt_camera_buffer;
+    if (int rc = prepare_state(c, f, c->stream, true, false, cb_want)) return rc;
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    c->async_streams.clear();
+    c->state_pending = false;
+    c->state_stream = nullptr;
+    return RT_OK;
 }
 
 RT_EXPORT int rt_last_stats(rt_ctx* c, rt_stats* out)
@@ -1515,14 +1789,36 @@ RT_EXPORT int rt_debug_lb_info(rt_ctx* c, double* out, int n)
 }
 
 // Diagnostic (not in include/rt.h): camera-buffer summary: out[0] = current
-// (0/1), out[1] = entries, out[2] = last build ms, out[3] = tiles.
+// (0/1), out[1] = entries, out[2] = last build ms (device time of its
+// kernels, from its first to its last, plus nothing of the host), out[3] =
+// tiles, out[4] = inline records (0/1), out[5] = the build's host wall time
+// up to its last enqueue (ms).
 RT_EXPORT int rt_debug_cb_info(rt_ctx* c, double* out, int n)
 {
     if (!c || !out || n < 4) return RT_E_ARG;
+    if (c->cb_timed) {
+        float ms = 0.f;
+        HIP_TRY(c, hipEventSynchronize(c->ev_cb1));
+        HIP_TRY(c, hipEventElapsedTime(&ms, c->ev_cb0, c->ev_cb1));
+        c->cb_build_ms = ms;
+        c->cb_timed = false;
+    }
     out[0] = c->cb_valid ? 1.0 : 0.0;
     out[1] = (double)c->cb_entries;
     out[2] = c->cb_build_ms;
     out[3] = (double)c->cb_ntiles;
+    if (n > 4) out[4] = c->cb_inline ? 1.0 : 0.0;
+    if (n > 5) out[5] = c->cb_host_ms;
+    return RT_OK;
+}
+
+// Diagnostic (not in include/rt.h): the last rt_upload_scene's host wall
+// time by part (ms): out[0] records + device copies, out[1] cone / cluster
+// prepasses, out[2] light buffer (incl. its far ladder), out[3] total.
+RT_EXPORT int rt_debug_upload_info(rt_ctx* c, double* out, int n)
+{
+    if (!c || !out || n < 4) return RT_E_ARG;
+    for (int i = 0; i < 4; ++i) out[i] = c->upload_parts_ms[i];
     return RT_OK;
 }
 

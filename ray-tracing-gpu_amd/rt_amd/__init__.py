@@ -24,7 +24,7 @@ import numpy as np
 
 __all__ = [
     "RtError", "SceneFlat", "Frame", "Stats", "Scene", "Context", "CScene", "lib", "band_rows", "frame_rows",
-    "LIB_PATH", "TRIANGLE", "PLANE", "QUADRIC", "FLAG_STATS",
+    "LIB_PATH", "TRIANGLE", "PLANE", "QUADRIC", "FLAG_STATS", "OPTIONS",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -32,6 +32,9 @@ LIB_PATH = os.environ.get("RT_AMD_LIB", os.path.join(os.path.dirname(_HERE), "li
 
 TRIANGLE, PLANE, QUADRIC = 0, 1, 2
 FLAG_STATS = 1
+# rt.h RT_OPT_* (ABI 4): A/B and test switches, none changes an image bit
+OPTIONS = {"light_buffer": 1, "camera_buffer": 2, "union_pretest": 3, "lb_scale": 4, "dcov_near": 5,
+           "cb_inline_max_mb": 6}
 _ERRORS = {-1: "RT_E_ARG", -2: "RT_E_IO", -3: "RT_E_PARSE", -4: "RT_E_STATE", -5: "RT_E_HIP",
            -6: "RT_E_UNSUPPORTED"}
 
@@ -96,6 +99,11 @@ SIGNATURES = {
     "rt_render": (ctypes.c_int, [_VP, ctypes.POINTER(Frame), _VP]),
     "rt_render_float": (ctypes.c_int, [_VP, ctypes.POINTER(Frame), _VP]),
     "rt_render_async": (ctypes.c_int, [_VP, ctypes.POINTER(Frame), _VP, _VP, _VP]),
+    "rt_prepare_camera": (ctypes.c_int, [_VP, ctypes.POINTER(Frame)]),
+    "rt_sync": (ctypes.c_int, [_VP]),
+    "rt_set_option": (ctypes.c_int, [_VP, ctypes.c_int32, ctypes.c_double]),
+    "rt_get_option": (ctypes.c_int, [_VP, ctypes.c_int32, ctypes.POINTER(ctypes.c_double)]),
+    "rt_set_far_ladder": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_double), ctypes.c_int32]),
     "rt_last_stats": (ctypes.c_int, [_VP, ctypes.POINTER(Stats)]),
     "rt_last_error": (ctypes.c_char_p, [_VP]),
     "rt_destroy": (None, [_VP]),
@@ -193,7 +201,7 @@ class Scene:
 class Context:
     """One HIP device: uploaded scene + render entry points."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, **options):
         L = lib()
         self._h = _VP()
         rc = L.rt_create(device, ctypes.byref(self._h))
@@ -203,6 +211,36 @@ class Context:
                 L.rt_destroy(self._h)
                 self._h = None
             raise RtError("rt_create", rc, msg)
+        for k, v in options.items():
+            if k == "far_ladder":
+                self.set_far_ladder(v)
+            else:
+                self.set_option(k, v)
+
+    def set_option(self, name, value: float):
+        """rt_set_option: `name` is a key of OPTIONS (or the RT_OPT_* number)."""
+        opt = OPTIONS[name] if isinstance(name, str) else int(name)
+        _check("rt_set_option", lib().rt_set_option(self._h, opt, float(value)), self._err)
+
+    def get_option(self, name) -> float:
+        opt = OPTIONS[name] if isinstance(name, str) else int(name)
+        v = ctypes.c_double()
+        _check("rt_get_option", lib().rt_get_option(self._h, opt, ctypes.byref(v)), self._err)
+        return v.value
+
+    def set_far_ladder(self, factors=None):
+        """rt_set_far_ladder: the big lists' far light buffers (None = default)."""
+        if factors is None:
+            _check("rt_set_far_ladder", lib().rt_set_far_ladder(self._h, None, -1), self._err)
+            return
+        arr = (ctypes.c_double * max(1, len(factors)))(*factors)
+        _check("rt_set_far_ladder", lib().rt_set_far_ladder(self._h, arr, len(factors)), self._err)
+
+    def prepare_camera(self, frame: Frame):
+        _check("rt_prepare_camera", lib().rt_prepare_camera(self._h, ctypes.byref(frame)), self._err)
+
+    def sync(self):
+        _check("rt_sync", lib().rt_sync(self._h), self._err)
 
     def _err(self) -> str:
         return (lib().rt_last_error(self._h) or b"").decode()

@@ -36,7 +36,7 @@ def test_header_symbols_exported():
 
 
 def test_abi_version():
-    assert rt_amd.lib().rt_abi_version() == 3
+    assert rt_amd.lib().rt_abi_version() == 4
 
 
 def test_struct_layouts_match_header():
@@ -73,6 +73,11 @@ def test_null_arguments_are_errors():
     assert L.rt_render_float(None, None, None) == -1
     assert L.rt_render_async(None, None, None, None, None) == -1
     assert L.rt_last_stats(None, None) == -1
+    assert L.rt_prepare_camera(None, None) == -1
+    assert L.rt_sync(None) == -1
+    assert L.rt_set_option(None, 1, 0.0) == -1
+    assert L.rt_get_option(None, 1, None) == -1
+    assert L.rt_set_far_ladder(None, None, 0) == -1
     assert L.rt_last_error(None) == b"null context"
     L.rt_destroy(None)
     L.rt_scene_destroy(None)

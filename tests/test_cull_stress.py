@@ -85,25 +85,15 @@ def test_gpu_matches_oracle_random_views(oracle, tmp_path, seed):
 
 
 # The light buffer (shadow cells, rt_kernels.hip shadow_opaque_lb) at cell
-# resolutions from coarse to fine (RT_AMD_LB_SCALE: R from 16 up to the
+# resolutions from coarse to fine (RT_OPT_LB_SCALE: R from 16 up to the
 # 1,024 cap), so cell borders, face edges and the per-light list all meet
 # the stress geometry.
-@pytest.fixture
-def lightbuf(monkeypatch):
-    def on(scale=None):
-        monkeypatch.setenv("RT_AMD_LIGHTBUF", "1")
-        if scale is not None:
-            monkeypatch.setenv("RT_AMD_LB_SCALE", str(scale))
-    return on
-
-
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,seed,w,h,depth", [c for c in CASES if c[4] == 0])
-def test_gpu_lightbuf_matches_reference(cull_golden, lightbuf, tmp_path, name, seed, w, h, depth):
+def test_gpu_lightbuf_matches_reference(cull_golden, tmp_path, name, seed, w, h, depth):
     import rt_amd
 
-    lightbuf()
-    ctx = rt_amd.Context(0)
+    ctx = rt_amd.Context(0, light_buffer=1)
     s = rt_amd.Scene(_path(tmp_path, seed, depth), w, h, depth)
     ctx.upload(s)
     got = ctx.render_float(s.frame)
@@ -113,14 +103,13 @@ def test_gpu_lightbuf_matches_reference(cull_golden, lightbuf, tmp_path, name, s
 @pytest.mark.gpu
 @pytest.mark.parametrize("scale", [0.25, 1.0, 4.0, 64.0])
 @pytest.mark.parametrize("seed", [100, 101, 104, 106, 107, 110, 111])
-def test_gpu_lightbuf_random_views(oracle, lightbuf, tmp_path, seed, scale):
+def test_gpu_lightbuf_random_views(oracle, tmp_path, seed, scale):
     import rt_amd
 
-    lightbuf(scale)
     n_small = 1200 if seed >= 106 else 60
     path = cull_scenes.write(str(tmp_path / f"lb{seed}.dat"), seed, 0.0, n_small)
     w, h = 96, 72
-    ctx = rt_amd.Context(0)
+    ctx = rt_amd.Context(0, light_buffer=1, lb_scale=scale)
     s = rt_amd.Scene(path, w, h, 0)
     ctx.upload(s)
     got = ctx.render_float(s.frame)
@@ -130,15 +119,14 @@ def test_gpu_lightbuf_random_views(oracle, lightbuf, tmp_path, seed, scale):
 
 
 # The wave-level shadow culling (the path with the light buffer switched
-# off: RT_AMD_LIGHTBUF=0), which the default no longer takes for these
+# off: RT_OPT_LIGHT_BUFFER 0), which the default no longer takes for these
 # scenes, against the same reference goldens.
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,seed,w,h,depth", [c for c in CASES if c[4] == 0])
-def test_gpu_wave_culling_matches_reference(cull_golden, monkeypatch, tmp_path, name, seed, w, h, depth):
+def test_gpu_wave_culling_matches_reference(cull_golden, tmp_path, name, seed, w, h, depth):
     import rt_amd
 
-    monkeypatch.setenv("RT_AMD_LIGHTBUF", "0")
-    ctx = rt_amd.Context(0)
+    ctx = rt_amd.Context(0, light_buffer=0)
     s = rt_amd.Scene(_path(tmp_path, seed, depth), w, h, depth)
     ctx.upload(s)
     assert bits_equal(ctx.render_float(s.frame), cull_golden[name])

@@ -91,15 +91,15 @@ def test_heightfield_windows(ctx, golden_images, heightfield_path):
         check(full[r0:r1, c0:c1], golden_images[k], 0)
 
 
-@pytest.mark.parametrize("near,far", [(1.5, 64.0), (1.5, 1.6)])
-def test_heightfield_far_buffer(monkeypatch, golden_images, heightfield_path, near, far):
+@pytest.mark.parametrize("near,far", [(1.5, [64.0]), (1.5, [1.6]), (1.05, [1.1, 1.3, 2.0, 4.0]),
+                                      (1.02, [1.05, 1.1, 1.2, 1.4, 1.8, 2.5, 4.0, 8.0]), (1.25, [])])
+def test_heightfield_far_buffer(golden_images, heightfield_path, near, far):
     """Big lists: lanes beyond the light buffer's distance walk the light's
-    far buffer, lanes beyond that the per-lane loop over every triangle.
-    Both distances shrunk (RT_AMD_DCOV_NEAR/FAR x the farthest triangle) so
-    that many lanes take each path: still the reference's bits."""
-    monkeypatch.setenv("RT_AMD_DCOV_NEAR", str(near))
-    monkeypatch.setenv("RT_AMD_DCOV_FAR", str(far))
-    c = rt_amd.Context(0)
+    far buffers level by level, lanes beyond the last the per-lane loop over
+    every triangle.  The distances shrunk (RT_OPT_DCOV_NEAR, rt_set_far_ladder,
+    x the farthest triangle) so that many lanes take every level: still the
+    reference's bits."""
+    c = rt_amd.Context(0, dcov_near=near, far_ladder=far)
     full = render(c, heightfield_path, 1920, 1080, 1)
     keys = [k for k in golden_images.files if k.startswith("hf_1080p_d1_win_")]
     assert keys
@@ -188,7 +188,7 @@ def test_bad_band_layout_rejected(ctx):
             ctx.render(f)
 
 
-def test_camera_buffer_follows_the_camera(monkeypatch):
+def test_camera_buffer_follows_the_camera():
     """The camera buffer (per-tile lists, built per camera by synchronous
     renders) must never serve a stale camera: after the camera moves, the
     async path renders without it until a synchronous render rebuilds it —
@@ -200,11 +200,9 @@ def test_camera_buffer_follows_the_camera(monkeypatch):
         f = s.frame.copy()
         f.cam_pos[0] += dx
         frames.append(f)
-    monkeypatch.setenv("RT_AMD_CAMBUF", "0")
-    ref = rt_amd.Context(0)
+    ref = rt_amd.Context(0, camera_buffer=0)
     ref.upload(s)
     want = [ref.render_float(f) for f in frames]
-    monkeypatch.delenv("RT_AMD_CAMBUF")
     c = rt_amd.Context(0)
     c.upload(s)
     out = torch.zeros((120, 160, 3), dtype=torch.float32, device="cuda")

@@ -4,9 +4,9 @@ RTLD_LOCAL so their identical symbol names do not collide.
 
     python tools/ab_variants.py --config c2 lib/var/librt_amd_base.so lib/var/librt_amd_nosl.so ...
 
-A variant may carry environment settings for its upload and first
-(synchronous) render, e.g. lib/librt_amd.so@RT_AMD_LB_SCALE=2 (several:
-@A=1,B=2); they are restored afterwards.
+A variant may carry context options (rt_set_option, names as in
+rt_amd.OPTIONS) set before its upload, e.g. lib/librt_amd.so@lb_scale=2
+(several: @a=1,b=2; the far light-buffer ladder as far=6:64).
 """
 import argparse
 import ctypes
@@ -49,10 +49,7 @@ def main():
     vs = []
     for spec in a.libs:
         lp, _, envs = spec.partition("@")
-        # (a value's own commas are written ':', e.g. RT_AMD_DCOV_FAR=6:64)
-        env = {k: v.replace(":", ",") for k, v in (kv.split("=", 1) for kv in envs.split(",") if kv)}
-        saved = {k: os.environ.get(k) for k in env}
-        os.environ.update(env)
+        opts = dict(kv.split("=", 1) for kv in envs.split(",") if kv)
         L = load(lp)
         sc = ctypes.c_void_p()
         assert L.rt_scene_create(ctypes.byref(sc)) == 0
@@ -65,6 +62,13 @@ def main():
         L.rt_scene_get_frame(sc, ctypes.byref(fr))
         ctx = ctypes.c_void_p()
         assert L.rt_create(0, ctypes.byref(ctx)) == 0
+        for k, v in opts.items():
+            if k == "far":
+                fs = [float(x) for x in v.split(":") if x]
+                arr = (ctypes.c_double * max(1, len(fs)))(*fs)
+                assert L.rt_set_far_ladder(ctx, arr, len(fs)) == 0
+            else:
+                assert L.rt_set_option(ctx, rt_amd.OPTIONS[k], float(v)) == 0
         assert L.rt_upload_scene(ctx, ctypes.byref(flat)) == 0
         # one synchronous render first: it builds what is built per camera
         # (the camera buffer) exactly as bench.py's counted render does
@@ -73,11 +77,6 @@ def main():
         L.rt_render_async(ctx, ctypes.byref(fr), out.data_ptr(), None, None)
         torch.cuda.synchronize()
         img = out.clone()
-        for k, v in saved.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
         same = True if ref is None else bool(torch.equal(img, ref))
         ref = img if ref is None else ref
         vs.append(dict(lib=os.path.basename(lp) + ("@" + envs if envs else ""), L=L, ctx=ctx, fr=fr, sc=sc, times=[], same_as_first=same))

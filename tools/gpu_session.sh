@@ -20,11 +20,14 @@ run() {  # name seconds cmd...
 }
 for s in $STEPS; do
   case $s in
-    tests) run pytest_gpu 600 python -m pytest tests -m gpu -x -q -rA ;;
+    tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -rA --timeout 300 --timeout-method thread ;;
+    tests_k) run pytest_gpu_k 600 python -u -m pytest tests -m gpu -x -v -rA --timeout 300 --timeout-method thread -k "$TESTK" ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 400 python bench.py ;;
     bench_all)
       for c in c1 c2 c3 c4 c4s7 c4s9 c5; do run bench_$c 400 python bench.py --config $c --steps 10 --cpu-seconds 5; done ;;
+    bench_big)
+      for c in ${CONFIGS:-c3 c5}; do run bench_$c 400 python bench.py --config $c --steps 10 --no-cpu-baseline; done ;;
     bench_one) run bench_${CONFIG:-c2} 400 python bench.py --config ${CONFIG:-c2} --steps 20 --no-cpu-baseline ;;
     listpmc) run list_counters 120 rocprofv3 -L ;;
     pmc)

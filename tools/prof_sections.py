@@ -62,7 +62,7 @@ def main():
     L.rt_debug_prof(buf)
     L.rt_debug_prof_events(ev)
     waves = ((W + 7) // 8) * ((H + 7) // 8) * a.frames
-    ev_names = EVENTS_LB if lbinfo and os.environ.get("RT_AMD_LIGHTBUF") != "0" else EVENTS
+    ev_names = EVENTS_LB if lbinfo else EVENTS
     tot = sum(buf[:8]) or 1
     print(json.dumps({"config": a.config, "frames": a.frames,
                       "share": {n: round(buf[i] / tot, 4) for i, n in enumerate(NAMES)},
