@@ -290,6 +290,11 @@ def main():
                     help="skip the PCIe-inclusive rt_render leg (profiling runs: only the timed launches)")
     ap.add_argument("--partition", default="auto", choices=["auto", "slabs", "bands"],
                     help="N>1: row slabs, cyclic 16-row bands, or bands when slabs are >10%% imbalanced")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="N>1 collective backend: nccl (= RCCL over xGMI, the benchmark) or gloo (the "
+                         "gather staged through host memory; lets several ranks share one GPU for tests)")
+    ap.add_argument("--frame-sha", action="store_true",
+                    help="rank 0 adds the SHA-256 of the last assembled RGBA8 frame (bottom row first)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -298,19 +303,24 @@ def main():
     import numpy as np
     import torch
 
-    torch.cuda.set_device(local)
+    # one GPU per rank (ranks beyond the visible GPUs share them: gloo only)
+    device = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(device)
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group("gloo")
     import rt_amd
 
     name, W, H, depth = CONFIGS[args.config]
     path = scene_path(name)
     scene = rt_amd.Scene(path, W, H, depth)
     t_cold = time.perf_counter()
-    ctx = rt_amd.Context(local)
+    ctx = rt_amd.Context(device)
     torch.cuda.synchronize()
     t_up = time.perf_counter()
     ctx.upload(scene)  # device copy + cone/cluster prepasses + light-buffer build (synchronous)
@@ -352,6 +362,9 @@ def main():
     partition, imbalance = "slabs", None
     if world > 1 and args.partition != "slabs":
         tmp = torch.zeros((max(rows, 1), W, 4), dtype=torch.uint8, device="cuda")
+        # the timed loop's kernel: one synchronous render first builds this
+        # camera's camera buffer, which the async renders below then use
+        ctx.prepare_camera(frame)
         for _ in range(2):
             ctx.render_async(frame, tmp.data_ptr(), 0, stream)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -361,7 +374,7 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         t = e0.elapsed_time(e1) / 5
-        tmax = torch.tensor([t], dtype=torch.float64, device="cuda")
+        tmax = torch.tensor([t], dtype=torch.float64, device="cuda" if args.dist_backend == "nccl" else "cpu")
         tsum = tmax.clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         dist.all_reduce(tsum)
@@ -434,15 +447,22 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    frame_sha = None
+    if args.frame_sha and rank == 0:
+        import hashlib
+
+        last = gather.frame(args.steps - 1 + args.warmup) if gather else single[:H]
+        frame_sha = hashlib.sha256(last.contiguous().cpu().numpy().tobytes()).hexdigest()
     if per_launch:
         kernel_ms = sum(a.elapsed_time(b) for a, b in events) / args.steps
     else:
         kernel_ms = events[0][0].elapsed_time(events[0][1]) / args.steps
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        cdev = "cuda" if args.dist_backend == "nccl" else "cpu"
+        t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        c = torch.tensor([st.primary_rays, st.bounce_rays, st.shadow_rays], dtype=torch.float64, device="cuda")
+        c = torch.tensor([st.primary_rays, st.bounce_rays, st.shadow_rays], dtype=torch.float64, device=cdev)
         dist.all_reduce(c)
         tot_primary, tot_bounce, tot_shadow = (float(x) for x in c.tolist())
     else:
@@ -484,7 +504,8 @@ def main():
             "config": {"workload": f"{name} {W}x{H} max_bounces={depth}", "width": W, "height": H,
                        "max_bounces": depth, "surfaces": int(types.shape[0]),
                        "parallelism": (f"row-band16 x{world}" if band else f"row-slab x{world}") +
-                                      (" + RCCL gather to rank 0 (double-buffered)" if world > 1 else ""),
+                                      ((" + RCCL gather to rank 0 (double-buffered)" if args.dist_backend == "nccl"
+                                        else " + gloo gather to rank 0 through host memory") if world > 1 else ""),
                        "slab_imbalance": round(imbalance, 3) if imbalance is not None else None},
             "total_rays_per_s_M": round((tot_primary + tot_bounce + tot_shadow) * args.steps / elapsed / 1e6, 3),
             "rays_per_frame": {"primary": int(tot_primary), "bounce": int(tot_bounce), "shadow": int(tot_shadow)},
@@ -506,6 +527,8 @@ def main():
                          "tests_executed": int(run_tests), "tests_brute_force": int(brute_tests),
                          "brute_force_equiv_tflops": round(brute / (kernel_ms * 1e-3) / 1e12, 3)},
         }
+        if frame_sha:
+            out["frame_rgba8_sha256"] = frame_sha
         if world == 1 and not args.no_host_boundary:
             out["host_boundary"] = host_boundary(ctx, frame, W)
             fc = frame_costs(scene, frame, W, cold)

@@ -16,6 +16,12 @@ slabs meet in ONE gather over xGMI:
 
 Slabs are equal-height (the last one padded) so a frame is one contiguous
 buffer of ``world * rows`` rows in row order — no permutation pass.
+
+With the gloo backend (CPU collectives: tests, and several ranks sharing one
+GPU, which RCCL refuses) the same gather is staged through host tensors:
+each rank copies its slab to the host, gloo gathers the host slabs to rank 0,
+and rank 0 copies the frame back into HBM.  RCCL is the default and the only
+backend the benchmark's numbers are quoted on.
 """
 from __future__ import annotations
 
@@ -90,6 +96,13 @@ class RootGather:
         dtype = dtype or torch.uint8
         shape_full = (self.world * self.rows, width, channels)
         shape_slab = (self.rows, width, channels)
+        # gloo moves host tensors only: stage the device slabs through them
+        self.host = str(device) != "cpu" and dist.get_backend() == "gloo"
+        if self.host:
+            self.h_slabs = [torch.zeros(shape_slab, dtype=dtype) for _ in range(depth)]
+            self.h_full = ([torch.zeros(shape_full, dtype=dtype) for _ in range(depth)] if self.rank == 0 else [])
+            self.h_views = ([[f[r * self.rows:(r + 1) * self.rows] for r in range(self.world)] for f in self.h_full]
+                            if self.rank == 0 else [])
         self.staging = []
         if self.rank == 0:
             self.frames = [torch.zeros(shape_full, dtype=dtype, device=device) for _ in range(depth)]
@@ -118,6 +131,13 @@ class RootGather:
         if self.world == 1:
             return
         d, b = self.dist, k % self.depth
+        if self.host:
+            import torch
+
+            self.h_slabs[b].copy_(self.slabs[b])  # waits for the render on the current stream
+            views = self.h_views[b] if self.rank == 0 else None
+            self.pending[b] = [d.gather(self.h_slabs[b], gather_list=views, dst=0, async_op=True)]
+            return
         views = self.views[b] if self.rank == 0 else None
         self.pending[b] = [d.gather(self.slabs[b], gather_list=views, dst=0, async_op=True)]
 
@@ -127,6 +147,8 @@ class RootGather:
             for w in self.pending[b]:
                 w.wait()
             self.pending[b] = None
+            if self.host and self.rank == 0:
+                (self.staging if self.band_rows else self.frames)[b].copy_(self.h_full[b])
             if self.band_rows and self.rank == 0:
                 # staging[rank][local band][row] -> frame[global band = local * world + rank][row]
                 br, W, C = self.band_rows, self.W, self.C
