@@ -1,0 +1,111 @@
+"""C5 at its full size — the 50k-triangle heightfield at 7680x4320, depth 3
+(BASELINE.json configs[4]) — against windows made by the reference's own
+code (tests/golden/c5.npz, make_c5_golden.py).  Paths that only this scale
+takes are asserted to have run: the camera buffer without inline records
+(the entries' records exceed 128 MiB), the five-level light-buffer ladder,
+and the 8-way cyclic bands and slabs of a 4,320-row frame, reassembled bit
+for bit.  A CPU test pins the oracle restatement on two of the windows."""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+import rt_amd
+from conftest import GOLDEN, bits_equal
+
+W, H, DEPTH = 7680, 4320, 3
+
+
+@pytest.fixture(scope="module")
+def c5_golden():
+    with np.load(os.path.join(GOLDEN, "c5.npz")) as z:
+        return {k: z[k] for k in z.files}
+
+
+def _win(k):
+    return tuple(map(int, k.rsplit("_win_", 1)[1].split("_")))
+
+
+def test_oracle_matches_reference_c5_windows(oracle, c5_golden, heightfield_path):
+    """The C restatement against the reference build on two C5 windows (one
+    over the mesh, one straddling a slab and a band boundary)."""
+    for k in ("hf_4320p_d3_win_2168_2184_3832_3864", "hf_4320p_d3_win_1080_1096_1912_1944"):
+        r0, r1, c0, c1 = _win(k)
+        got = oracle.render(heightfield_path, W, H, DEPTH, window=(r0, r1, c0, c1), threads=8)
+        assert bits_equal(got, c5_golden[k]), k
+
+
+def _cb_info(ctx):
+    L = rt_amd.lib()
+    L.rt_debug_cb_info.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+    info = (ctypes.c_double * 6)()
+    assert L.rt_debug_cb_info(ctx._h, info, 6) == 0
+    return list(info)
+
+
+def _lb_levels(ctx, n_lights):
+    L = rt_amd.lib()
+    L.rt_debug_lb_info.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+    info = (ctypes.c_double * 64)()
+    assert L.rt_debug_lb_info(ctx._h, info, 64) == 0
+    return info[0], info[1]
+
+
+@pytest.mark.gpu
+def test_c5_full_frame_windows_bands_and_slabs(c5_golden, heightfield_path):
+    from rt_amd.dist import slab_rows
+
+    s = rt_amd.Scene(heightfield_path, W, H, DEPTH)
+    ctx = rt_amd.Context(0)
+    ctx.upload(s)
+    built, entries = _lb_levels(ctx, 2)
+    assert built == 1.0 and entries > 10_000_000  # the five-level ladder of both lights
+    full = ctx.render_float(s.frame)
+    info = _cb_info(ctx)
+    assert info[0] == 1.0 and info[3] == (W // 8) * (H // 8)
+    assert info[4] == 0.0, "C5 must walk the camera buffer by index (records > 128 MiB)"
+    assert info[1] * 64 > 128 * 2**20
+    for k, want in c5_golden.items():
+        r0, r1, c0, c1 = _win(k)
+        assert bits_equal(full[r0:r1, c0:c1], want), k
+    # 8 cyclic 16-row bands, as bench.py --partition bands renders them
+    got = np.empty_like(full)
+    n, br = 8, 16
+    for r in range(n):
+        f = s.frame.copy()
+        f.band_rows, f.band_count, f.band_index = br, n, r
+        part = ctx.render_float(f)
+        assert part.shape[0] == rt_amd.band_rows(H, br, n, r)
+        q = part.shape[0] // br
+        # local band j -> frame band j * n + r
+        got.reshape(H // br, br, W, 3)[r::n][:q] = part.reshape(q, br, W, 3)
+    assert bits_equal(got, full)
+    del got
+    # 8 slabs, both the equal 540-row split and slab_rows' 8-row multiples
+    for rows in (H // n, slab_rows(H, n, 0)[2]):
+        parts = []
+        for r in range(n):
+            f = s.frame.copy()
+            f.row_begin, f.row_end = min(H, r * rows), min(H, (r + 1) * rows)
+            parts.append(ctx.render_float(f))
+        assert bits_equal(np.concatenate(parts, 0), full), rows
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("inline_mb", [0, 128])
+def test_camera_buffer_index_and_inline_walks(golden_images, heightfield_path, inline_mb):
+    """RT_OPT_CB_INLINE_MAX_MB 0 forces the walk by index (C5's) on C3's
+    frame, 128 keeps the inline records: both give the reference's bits."""
+    s = rt_amd.Scene(heightfield_path, 1920, 1080, 1)
+    ctx = rt_amd.Context(0, cb_inline_max_mb=inline_mb)
+    ctx.upload(s)
+    full = ctx.render_float(s.frame)
+    assert _cb_info(ctx)[4] == (1.0 if inline_mb else 0.0)
+    keys = [k for k in golden_images.files if k.startswith("hf_1080p_d1_win_")]
+    assert keys
+    for k in keys:
+        r0, r1, c0, c1 = _win(k)
+        assert bits_equal(full[r0:r1, c0:c1], golden_images[k]), k
