@@ -1,7 +1,7 @@
 // rt_main.cpp — headless counterpart of the reference's Main.cpp entry point.
 //
-//   rt_render <scene.dat> [-x W] [-y H] [-d depth] [-o out.ppm] [-g device]
-//             [-n frames] [-s]
+//   rt_render <scene.dat> [-x W] [-y H] [-d depth] [-o out.ppm] [-g gpus]
+//             [--device first] [--bands] [-n frames] [-s]
 //
 // Kept from Main.cpp:51-199: argv[1] is the scene file, -x / -y set the
 // resolution (default 512x256, Var.cpp:4-5), the same [ETAT]/[ERREUR] log
@@ -12,13 +12,23 @@
 // the render core has no such restriction; there is no GLUT window — the
 // frame is written as a binary PPM (top row first) instead; -d sets
 // m_NbRebondsMax (default 0 = the shipped executable, whose recursion is
-// commented out), -g picks the HIP device, -n renders N frames (the scene is
-// prepared once, unlike LancerRayons which re-runs Pretraitement), -s prints
-// ray counters.
+// commented out); -n renders N frames (the scene is prepared once, unlike
+// LancerRayons which re-runs Pretraitement); -s prints ray counters.
+// Multi-GPU from the command line: -g N renders the frame
+// with N contexts, one per GPU from --device on (wrapping round when there
+// are fewer GPUs: contexts then share one), one host thread each, every
+// context rendering its row slab (or, with --bands, its cyclic 16-row
+// bands) straight into its part of the host frame; the parts are assembled
+// in host memory — the same partition as bench.py's ranks, without a
+// collective.
+#include <hip/hip_runtime_api.h>
+
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/rt.h"
@@ -35,19 +45,27 @@ int main(int argc, char** argv)
         std::fprintf(stderr, "[ERREUR]: Aucune fichier de scene ne fut passe en argument !\n");
         return 1;
     }
-    int W = 512, H = 256, depth = 0, dev = 0, frames = 1;
-    bool stats = false;
+    int W = 512, H = 256, depth = 0, dev0 = 0, frames = 1, gpus = 1;
+    bool stats = false, bands = false;
     const char* out = nullptr;
     for (int i = 2; i < argc; ++i) {
         if (argv[i][0] != '-') continue;
         auto next = [&](int& v) {
             if (i + 1 < argc) v = std::atoi(argv[++i]);
         };
+        if (std::strcmp(argv[i], "--device") == 0) {
+            next(dev0);
+            continue;
+        }
+        if (std::strcmp(argv[i], "--bands") == 0) {
+            bands = true;
+            continue;
+        }
         switch (argv[i][1]) {
         case 'x': next(W); break;
         case 'y': next(H); break;
         case 'd': next(depth); break;
-        case 'g': next(dev); break;
+        case 'g': next(gpus); break;
         case 'n': next(frames); break;
         case 's': stats = true; break;
         case 'o':
@@ -55,6 +73,7 @@ int main(int argc, char** argv)
             break;
         }
     }
+    if (W <= 0 || H <= 0 || gpus <= 0 || frames <= 0) return fail("arguments", RT_E_ARG, "-x/-y/-g/-n must be > 0");
     if (((W - 1) & W) || ((H - 1) & H))
         std::fprintf(stderr, "[ATTENTION]: Resolution %dx%d n'est pas une puissance de deux "
                              "(accepted: the render core has no such restriction)\n", W, H);
@@ -67,32 +86,77 @@ int main(int argc, char** argv)
     std::printf("[ETAT]: Traitement du fichier de donnees de la scene...\n");
     if ((rc = rt_scene_load_file(scene, argv[1]))) return fail("TraiterFichierDeScene", rc, rt_scene_error(scene));
     if ((rc = rt_scene_prepare(scene))) return fail("Initialiser", rc, rt_scene_error(scene));
-
-    rt_ctx* ctx = nullptr;
-    if ((rc = rt_create(dev, &ctx))) return fail("rt_create", rc, ctx ? rt_last_error(ctx) : "");
     rt_scene_flat flat;
     rt_scene_get_flat(scene, &flat);
-    if ((rc = rt_upload_scene(ctx, &flat))) return fail("rt_upload_scene", rc, rt_last_error(ctx));
     rt_frame frame;
     rt_scene_get_frame(scene, &frame);
     if (stats) frame.flags |= RT_FLAG_STATS;
 
-    std::vector<uint8_t> img((size_t)W * H * 4);
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail("rt_create", RT_E_HIP, "no HIP device");
+    // one context per GPU share; part r = rows of slab r, or band set r
+    const int band = bands ? 16 : 0;
+    std::vector<rt_ctx*> ctx((size_t)gpus, nullptr);
+    std::vector<rt_frame> part((size_t)gpus, frame);
+    std::vector<std::vector<uint8_t>> img((size_t)gpus);
+    const int slab = (H + gpus - 1) / gpus;
+    for (int r = 0; r < gpus; ++r) {
+        if ((rc = rt_create((dev0 + r) % ndev, &ctx[r]))) return fail("rt_create", rc, ctx[r] ? rt_last_error(ctx[r]) : "");
+        if ((rc = rt_upload_scene(ctx[r], &flat))) return fail("rt_upload_scene", rc, rt_last_error(ctx[r]));
+        rt_frame& f = part[r];
+        int rows;
+        if (band) {
+            f.band_rows = band;
+            f.band_count = gpus;
+            f.band_index = r;
+            rows = rt_band_rows(H, band, gpus, r);
+        } else {
+            f.row_begin = std::min(H, r * slab);
+            f.row_end = std::min(H, (r + 1) * slab);
+            rows = f.row_end - f.row_begin;
+        }
+        img[r].resize((size_t)std::max(rows, 0) * W * 4);
+    }
     std::printf("[ETAT]: Lancer de rayons...\n");
     double total = 0.0;
-    for (int f = 0; f < frames; ++f) {
+    std::vector<int> rcs((size_t)gpus, 0);
+    for (int k = 0; k < frames; ++k) {
         const auto t0 = std::chrono::steady_clock::now();
-        if ((rc = rt_render(ctx, &frame, img.data()))) return fail("LancerRayons", rc, rt_last_error(ctx));
+        if (gpus == 1) {
+            rcs[0] = rt_render(ctx[0], &part[0], img[0].data());
+        } else {
+            std::vector<std::thread> th;
+            for (int r = 0; r < gpus; ++r)
+                th.emplace_back([&, r] { rcs[r] = img[r].empty() ? 0 : rt_render(ctx[r], &part[r], img[r].data()); });
+            for (auto& t : th) t.join();
+        }
         const auto t1 = std::chrono::steady_clock::now();
+        for (int r = 0; r < gpus; ++r)
+            if (rcs[r]) return fail("LancerRayons", rcs[r], rt_last_error(ctx[r]));
         total += std::chrono::duration<double>(t1 - t0).count();
     }
+    // the frame, bottom row first (memory row 0 = bottom scanline)
+    std::vector<uint8_t> full((size_t)W * H * 4);
+    for (int r = 0; r < gpus; ++r) {
+        const size_t rowb = (size_t)W * 4;
+        if (band) {
+            const int q = (int)(img[r].size() / rowb) / band;
+            for (int j = 0; j < q; ++j) {
+                const int y0 = (j * gpus + r) * band;
+                const int n = std::min(band, H - y0);
+                if (n > 0) std::memcpy(&full[(size_t)y0 * rowb], &img[r][(size_t)j * band * rowb], (size_t)n * rowb);
+            }
+        } else if (!img[r].empty()) {
+            std::memcpy(&full[(size_t)part[r].row_begin * rowb], img[r].data(), img[r].size());
+        }
+    }
     rt_stats st;
-    rt_last_stats(ctx, &st);
-    std::printf("[ETAT]: Termine! --> Temps total de rendu : %.6f secondes (%d frame(s), kernel %.3f ms)\n",
-                total, frames, st.kernel_ms);
+    rt_last_stats(ctx[0], &st);
+    std::printf("[ETAT]: Termine! --> Temps total de rendu : %.6f secondes (%d frame(s), %d GPU(s)%s, kernel %.3f ms)\n",
+                total, frames, gpus, band ? " bands" : "", st.kernel_ms);
     if (stats)
         std::printf("[STATS]: primary=%llu bounce=%llu shadow=%llu shadow_tests_skipped=%llu stack=%d "
-                    "tests: triangle=%llu plane=%llu quadric=%llu\n",
+                    "tests: triangle=%llu plane=%llu quadric=%llu (context 0)\n",
                     (unsigned long long)st.primary_rays, (unsigned long long)st.bounce_rays,
                     (unsigned long long)st.shadow_rays, (unsigned long long)st.shadow_tests_skipped,
                     st.stack_depth, (unsigned long long)st.triangle_tests, (unsigned long long)st.plane_tests,
@@ -101,12 +165,12 @@ int main(int argc, char** argv)
         FILE* f = std::fopen(out, "wb");
         if (!f) return fail("fopen", -1, out);
         std::fprintf(f, "P6\n%d %d\n255\n", W, H);
-        for (int y = H - 1; y >= 0; --y)  // memory row 0 = bottom scanline
-            for (int x = 0; x < W; ++x) std::fwrite(&img[((size_t)y * W + x) * 4], 1, 3, f);
+        for (int y = H - 1; y >= 0; --y)  // PPM: top row first
+            for (int x = 0; x < W; ++x) std::fwrite(&full[((size_t)y * W + x) * 4], 1, 3, f);
         std::fclose(f);
         std::printf("[ETAT]: Image ecrite dans %s\n", out);
     }
-    rt_destroy(ctx);
+    for (rt_ctx* c : ctx) rt_destroy(c);
     rt_scene_destroy(scene);
     return 0;
 }

@@ -12,7 +12,8 @@ import numpy as np
 import pytest
 
 import rt_amd
-from conftest import bits_equal, scene
+from conftest import GOLDEN, bits_equal, scene
+from loader_quirks import QUIRK_RES, QUIRKS
 
 
 def product_dump(path, w, h, depth=0):
@@ -68,72 +69,26 @@ def test_frame_defaults():
     assert f.max_bounces == 3 and np.float32(f.min_energy) == np.float32(0.01) and f.scene_ior == 1.0
 
 
-QUIRKS = {
-    # indented comment lines are NOT comments (Trim result discarded, Scene.cpp:254);
-    # this one carries 'color:' inside a surface, with a failing %i -> stale R,G,B
-    "stale_rgb": """background: 10 20 30
-Plane: p
-  v_linear: 0 1 0
-  v_const: 45
-  color: 100 150 200
-Quad: q
-  v_quad: 1 1 1
-  v_const: -100
-     * --- color: R G B ---
-Lumiere: l
-  position: 10 100 10
-  intens: 0.9
-  color: 255 128 0
-""",
-    # keywords match anywhere; 'Poly:' inside a line starts a triangle
-    "substring_keywords": """origin: 0 0 300
-eye: 0 0 0
-xx Poly: t1
-  point: 0 -50 -50 0
-  point: 1 50 -50 0
-  point: 2 0 50 0
-  color: 200 20 20
-  rotate: 10 20 30
-  translate: 1 2 3
-  scale: 2 1 0.5
-Lumiere: l
-  position: 0 0 400
-  intens: 1
-""",
-    # last line without a trailing newline; CRLF line endings
-    "crlf_no_eol": "background: 1 2 3\r\nPlane: p\r\n  v_linear: 0 1 0\r\n  v_const: 45\r\n  color: 9 9 9",
-    # stale Val0..2: 'ambient:' with no number reuses the previous float
-    "stale_float": """Quad: s
-  v_quad: 1 1 1
-  v_const: -400
-  diffus: 0.25
-  ambient:
-  specular: 0.5 12
-  refract: 0.5 1.3
-  reflect: 0.7
-Lumiere: l
-  position: 0 300 300
-  intens: 1
-""",
-    # octal/hex through %i, exactly like the reference's sscanf
-    "octal_hex": """background: 010 0x10 7
-Poly: t
-  point: 0 0 0 0
-  point: 1 1 0 0
-  point: 2 0 1 0
-  color: 0x7f 017 255
-""",
-}
+@pytest.fixture(scope="module")
+def quirk_golden():
+    with np.load(os.path.join(GOLDEN, "loader_quirks.npz")) as z:
+        return {k: z[k] for k in z.files}
 
 
 @pytest.mark.parametrize("name", sorted(QUIRKS))
-def test_loader_quirks_match_oracle(oracle, tmp_path, name):
+def test_loader_quirks_match_reference(quirk_golden, oracle, tmp_path, name):
+    """TraiterFichierDeScene's quirks (Scene.cpp:231-501) on crafted files:
+    the product's loader + Pretraitement against the reference build's
+    (tests/golden/loader_quirks.npz, made by make_loader_golden.py with the
+    reference's own CMatrice4 rotate/translate/scale, CCouleur and
+    Pretraitement), and the oracle restatement against the same fixture."""
     p = tmp_path / f"{name}.dat"
     p.write_bytes(QUIRKS[name].encode())
-    s, c, l, _ = product_dump(str(p), 40, 30)
-    so, co, lo = oracle.dump(str(p), 40, 30)
-    assert bits_equal(s, so) and cam_eq(c, co) and bits_equal(l, lo)
-    assert s.shape[0] >= 1
+    s, c, l, _ = product_dump(str(p), *QUIRK_RES)
+    gs, gc, gl = (quirk_golden[f"{name}_{k}"] for k in ("surf", "cam", "lights"))
+    assert bits_equal(s, gs) and cam_eq(c, gc) and bits_equal(l, gl)
+    so, co, lo = oracle.dump(str(p), *QUIRK_RES)
+    assert bits_equal(so, gs) and cam_eq(co, gc) and bits_equal(lo, gl)
 
 
 def test_stale_rgb_semantics(tmp_path):
