@@ -401,6 +401,8 @@ struct rt_ctx {
     hipEvent_t ev_cb0 = nullptr, ev_cb1 = nullptr;  // around the last build's device work
     double cb_host_ms = 0.0;
     bool cb_timed = false;
+    unsigned* d_cb_bstat = nullptr;  // block pre-cull: blocks, blocks walked per tile, staged members
+    bool cb_blocks = false;     // the last build used rt_cb_block
     void* d_scan = nullptr;     // u64 scratch of the build scans
     size_t scan_words = 0;
     unsigned long long* h_word = nullptr;  // pinned: totals read back by the builds
@@ -492,6 +494,7 @@ RT_EXPORT int rt_create(int32_t dev, rt_ctx** out)
     HIP_TRY(c, hipEventCreate(&c->ev_cb1));
     HIP_TRY(c, hipHostMalloc((void**)&c->h_word, 2 * sizeof(unsigned long long), hipHostMallocDefault));
     HIP_TRY(c, hipMalloc(&c->d_stats, kStatSlots * sizeof(StatsDev)));
+    HIP_TRY(c, hipMalloc(&c->d_cb_bstat, 4 * sizeof(unsigned)));
     c->far_ladder = {2.5, 6.0, 16.0, 64.0};
     return RT_OK;
 }
@@ -670,6 +673,7 @@ RT_EXPORT void rt_destroy(rt_ctx* c)
     if (c->ev_cb1) hipEventDestroy(c->ev_cb1);
     if (c->h_word) hipHostFree(c->h_word);
     hipFree(c->d_scan);
+    hipFree(c->d_cb_bstat);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
 }
@@ -1452,10 +1456,26 @@ static int cb_build(rt_ctx* c, const rt_frame* f, hipStream_t st)
     FrameDev F;
     frame_dev(f, F);
     dim3 grid((tx + 1) / 2, (ty + 1) / 2);
+    // big lists: the block pre-cull (rt_cb_block: 8 x 8 tiles per workgroup
+    // at 4K and wider, 4 x 4 below — blocks of similar angular size)
+    const bool blocks = c->n_clu > 0;
+    const int blk = f->width >= 3840 ? 8 : 4;
+    dim3 bgrid((tx + blk - 1) / blk, (ty + blk - 1) / blk);
     HIP_TRY(c, hipEventRecord(c->ev_cb0, st));
-    hipLaunchKernelGGL(rt_cb_build<false>, grid, dim3(256), 0, st, S, F, (const unsigned*)nullptr, c->d_cb_off,
-                       c->d_cb_flag, (int2*)nullptr);
+    if (blocks) {
+        HIP_TRY(c, hipMemsetAsync(c->d_cb_bstat, 0, 4 * sizeof(unsigned), st));
+        if (blk == 8)
+            hipLaunchKernelGGL((rt_cb_block<false, 8>), bgrid, dim3(256), 0, st, S, F, (const unsigned*)nullptr,
+                               c->d_cb_off, c->d_cb_flag, (int2*)nullptr, c->d_cb_bstat);
+        else
+            hipLaunchKernelGGL((rt_cb_block<false, 4>), bgrid, dim3(256), 0, st, S, F, (const unsigned*)nullptr,
+                               c->d_cb_off, c->d_cb_flag, (int2*)nullptr, c->d_cb_bstat);
+    } else {
+        hipLaunchKernelGGL(rt_cb_build<false>, grid, dim3(256), 0, st, S, F, (const unsigned*)nullptr, c->d_cb_off,
+                           c->d_cb_flag, (int2*)nullptr);
+    }
     HIP_TRY(c, hipGetLastError());
+    c->cb_blocks = blocks;
     unsigned long long* tot = nullptr;
     HIP_TRY(c, scan_u32(c->d_cb_off, (unsigned)nt, c->d_cb_off, (unsigned long long*)c->d_scan, st, &tot));
     HIP_TRY(c, hipMemcpyAsync(c->h_word, tot, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
@@ -1480,10 +1500,17 @@ static int cb_build(rt_ctx* c, const rt_frame* f, hipStream_t st)
         HIP_TRY(c, hipMalloc(&c->d_cb_rec, std::max<size_t>(run, 1) * 4 * sizeof(float4)));
         c->cb_rec_cap = std::max<size_t>(run, 1);
     }
-    hipLaunchKernelGGL(rt_cb_build<true>, grid, dim3(256), 0, st, S, F, (const unsigned*)c->d_cb_off, (unsigned*)nullptr,
-                       c->d_cb_flag, c->d_cb_ent);
+    if (blocks && blk == 8)
+        hipLaunchKernelGGL((rt_cb_block<true, 8>), bgrid, dim3(256), 0, st, S, F, (const unsigned*)c->d_cb_off,
+                           (unsigned*)nullptr, c->d_cb_flag, c->d_cb_ent, (unsigned*)nullptr);
+    else if (blocks)
+        hipLaunchKernelGGL((rt_cb_block<true, 4>), bgrid, dim3(256), 0, st, S, F, (const unsigned*)c->d_cb_off,
+                           (unsigned*)nullptr, c->d_cb_flag, c->d_cb_ent, (unsigned*)nullptr);
+    else
+        hipLaunchKernelGGL(rt_cb_build<true>, grid, dim3(256), 0, st, S, F, (const unsigned*)c->d_cb_off,
+                           (unsigned*)nullptr, c->d_cb_flag, c->d_cb_ent);
     HIP_TRY(c, hipGetLastError());
-    hipLaunchKernelGGL(rt_cb_keys, dim3((nt + 255) / 256), dim3(256), 0, st, (const unsigned*)c->d_cb_off, nt,
+    hipLaunchKernelGGL(rt_cb_keys_wave, dim3((nt + 3) / 4), dim3(256), 0, st, (const unsigned*)c->d_cb_off, nt,
                        c->d_cb_ent);
     HIP_TRY(c, hipGetLastError());
     c->cb_inline = want_inline;
@@ -1792,7 +1819,8 @@ RT_EXPORT int rt_debug_lb_info(rt_ctx* c, double* out, int n)
 // (0/1), out[1] = entries, out[2] = last build ms (device time of its
 // kernels, from its first to its last, plus nothing of the host), out[3] =
 // tiles, out[4] = inline records (0/1), out[5] = the build's host wall time
-// up to its last enqueue (ms).
+// up to its last enqueue (ms); out[6..8] = block pre-cull blocks, blocks
+// that fell back to the per-tile walk, members staged over all blocks.
 RT_EXPORT int rt_debug_cb_info(rt_ctx* c, double* out, int n)
 {
     if (!c || !out || n < 4) return RT_E_ARG;
@@ -1809,6 +1837,13 @@ RT_EXPORT int rt_debug_cb_info(rt_ctx* c, double* out, int n)
     out[3] = (double)c->cb_ntiles;
     if (n > 4) out[4] = c->cb_inline ? 1.0 : 0.0;
     if (n > 5) out[5] = c->cb_host_ms;
+    if (n > 8) {  // block pre-cull: blocks, blocks whose tiles walked every cluster, staged members
+        unsigned b[4] = {0, 0, 0, 0};
+        if (c->cb_blocks) HIP_TRY(c, hipMemcpy(b, c->d_cb_bstat, sizeof b, hipMemcpyDeviceToHost));
+        out[6] = b[0];
+        out[7] = b[1];
+        out[8] = b[2];
+    }
     return RT_OK;
 }
 
