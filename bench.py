@@ -48,6 +48,22 @@ CONFIGS = {
 }
 
 
+def product_src_sha256() -> str:
+    """Hash of the product's kernel sources and build flags (the code the PMC
+    counters in profiles/pmc.json were collected on)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    pkg = os.path.join(REPO, "ray-tracing-gpu_amd")
+    for rel in sorted(os.listdir(os.path.join(pkg, "csrc"))):
+        with open(os.path.join(pkg, "csrc", rel), "rb") as f:
+            h.update(rel.encode() + b"\0" + f.read())
+    for path in (os.path.join(pkg, "Makefile"), os.path.join(REPO, "include", "rt.h")):
+        with open(path, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
 def scene_path(name: str) -> str:
     if name == "heightfield":
         from rt_amd import synth
@@ -485,11 +501,13 @@ def main():
         if os.path.exists(tfile):
             with open(tfile) as f:
                 rec = json.load(f).get(f"{args.config}_n{world}")
-            if rec:
+            if rec and rec.get("src_sha256") == product_src_sha256():
                 traffic = rec.get("hbm_bytes_per_launch")
                 if rec.get("SQ_INSTS_VALU"):
                     valu_busy = round(rec["SQ_INSTS_VALU"] * 2 / (1024 * kernel_ms * 1e-3 * 2.4e9), 3)
                 pmc_src = rec.get("source")
+            elif rec:  # counters of other kernel sources: not this kernel's
+                pmc_src = "stale: " + rec.get("source", "") + " (collected on other sources)"
         alg_bytes = 4 * W * rt_amd.frame_rows(frame) + scene_bytes
         out = {
             "metric": "Mray/s and ms/frame at 1920x1080 depth=3, 1/2/4/8 MI355X vs host CPU",

@@ -9,6 +9,8 @@ import os
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+from bench import product_src_sha256  # noqa: E402
 
 
 def main(src, *configs):
@@ -19,11 +21,13 @@ def main(src, *configs):
         d = json.load(open(f))
         out[f"{c}_n1"] = {"hbm_bytes_per_launch": d.get("hbm_bytes_per_launch"),
                           "SQ_INSTS_VALU": d.get("SQ_INSTS_VALU"), "SQ_INSTS_SALU": d.get("SQ_INSTS_SALU"),
-                          "SQ_WAVES": d.get("SQ_WAVES"), "source": os.path.relpath(f, REPO)}
+                          "SQ_WAVES": d.get("SQ_WAVES"), "source": os.path.relpath(f, REPO),
+                          "src_sha256": product_src_sha256()}
     out["_note"] = ("Per timed rt_trace_kernel launch, from rocprofv3 --pmc passes (one counter group per run): "
                     "hbm_bytes_per_launch = FETCH_SIZE*1024*2 + WRITE_SIZE*1024 (gfx950 x2 FETCH correction, "
                     "MI355X_MICROARCH.md; an upper bound for this kernel's scalar reads), SQ_INSTS_VALU = VALU "
-                    "wave-instructions.")
+                    "wave-instructions.  src_sha256 = the product sources the counters were collected on; bench.py drops "
+                    "the measured fields when the tree's sources differ.")
     json.dump(out, open(out_path, "w"), indent=1, sort_keys=True)
     print(json.dumps(out, indent=1, sort_keys=True))
 
