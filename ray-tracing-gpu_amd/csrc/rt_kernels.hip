@@ -390,6 +390,11 @@ struct rt_ctx {
     float4* d_clu_light = nullptr;
     int n_clu = 0;
     float4* d_uni = nullptr;  // union records (small lists): camera, then one per light
+    // Camera state of rt_render_sequence_async: two slots of the per-camera
+    // records, apart from the state above, alternating frame by frame.
+    struct CamSlot {
+        float4 *tricam = nullptr, *cone_cam = nullptr, *clu_cam = nullptr, *uni = nullptr;
+    } seq[2];
     // camera buffer (rt_cb_build): per-tile lists for the camera of cb_key
     unsigned* d_cb_off = nullptr;
     unsigned* d_cb_flag = nullptr;
@@ -663,6 +668,12 @@ RT_EXPORT void rt_destroy(rt_ctx* c)
     hipFree(c->d_cb_flag);
     hipFree(c->d_cb_ent);
     hipFree(c->d_cb_rec);
+    for (auto& q : c->seq) {
+        hipFree(q.tricam);
+        hipFree(q.cone_cam);
+        hipFree(q.clu_cam);
+        hipFree(q.uni);
+    }
     hipFree(c->d_stats);
     hipFree(c->d_scratch);
     if (c->ev0) hipEventDestroy(c->ev0);
@@ -1207,6 +1218,23 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
             HIP_TRY(c, hipStreamSynchronize(st));  // nev outlives the copy
         }
     }
+    // the sequence slots (rt_render_sequence_async): per-camera records of
+    // their own; the union records' light part is the scene's
+    for (auto& q : c->seq) {
+        hipFree(q.tricam);
+        hipFree(q.cone_cam);
+        hipFree(q.clu_cam);
+        hipFree(q.uni);
+        q = rt_ctx::CamSlot{};
+        if (ntr == 0) continue;
+        HIP_TRY(c, hipMalloc((void**)&q.tricam, (ntr <= (size_t)kTricamMaxTriangles ? ntr : 1) * 4 * sizeof(float4)));
+        HIP_TRY(c, hipMalloc((void**)&q.cone_cam, ntr * kConeRec * sizeof(float4)));
+        if (c->n_clu > 0) HIP_TRY(c, hipMalloc((void**)&q.clu_cam, (size_t)c->n_clu * 4 * sizeof(float4)));
+        if (c->d_uni) {
+            HIP_TRY(c, hipMalloc((void**)&q.uni, (size_t)(nl + 1) * 2 * sizeof(float4)));
+            HIP_TRY(c, hipMemcpyAsync(q.uni, c->d_uni, (size_t)(nl + 1) * 2 * sizeof(float4), hipMemcpyDeviceToDevice, st));
+        }
+    }
     HIP_TRY(c, hipStreamSynchronize(st));
     c->upload_parts_ms[1] = since(tp0);
     const auto tl0 = std::chrono::steady_clock::now();
@@ -1383,34 +1411,42 @@ static bool camera_needs_prepass(const rt_ctx* c, const rt_frame* f, bool all_tr
                              (!all_tricam || c->tricam_all));
 }
 
-// Per-camera prepasses (when the camera position moved): camera-ray
-// triangle values, camera cone records, union / cluster records.
-static int camera_prepass(rt_ctx* c, const rt_frame* f, hipStream_t st, bool all_tricam)
+// The per-camera records of camera position cp into one set of buffers:
+// camera-ray triangle values, camera cone records, union / cluster records.
+static int camera_records(rt_ctx* c, const float* cp, hipStream_t st, bool all_tricam, float4* tricam,
+                          float4* cone_cam, float4* uni, float4* clu_cam)
 {
-    if (!camera_needs_prepass(c, f, all_tricam)) return RT_OK;
-    const float* cp = f->cam_pos;
     if (all_tricam || c->n_tri <= kTricamMaxTriangles) {
         hipLaunchKernelGGL(rt_camera_prepass, dim3((c->n_tri + 255) / 256), dim3(256), 0, st, c->d_tri, c->n_tri,
-                           cp[0], cp[1], cp[2], c->d_tricam);
+                           cp[0], cp[1], cp[2], tricam);
         HIP_TRY(c, hipGetLastError());
     }
     hipLaunchKernelGGL(rt_cone_prepass, dim3((c->n_tri + 255) / 256), dim3(256), 0, st, c->d_tri, c->d_trisph,
-                       c->d_trinrm, c->d_tricoef, c->n_tri, cp[0], cp[1], cp[2], 1, 0.0f, c->d_cone_cam);
+                       c->d_trinrm, c->d_tricoef, c->n_tri, cp[0], cp[1], cp[2], 1, 0.0f, cone_cam);
     HIP_TRY(c, hipGetLastError());
-    if (c->d_uni) {
-        hipLaunchKernelGGL(rt_cluster_prepass, dim3(1), dim3(64), 0, st, c->d_cone_cam, c->n_tri, 1, c->d_uni,
-                           c->n_tri);
+    if (uni) {
+        hipLaunchKernelGGL(rt_cluster_prepass, dim3(1), dim3(64), 0, st, cone_cam, c->n_tri, 1, uni, c->n_tri);
         HIP_TRY(c, hipGetLastError());
     }
     if (c->n_clu > 0) {
-        float4* tmp = c->d_clu_cam + 2 * (size_t)c->n_clu;  // second half: unsorted
-        hipLaunchKernelGGL(rt_cluster_prepass, dim3((unsigned)((c->n_clu + 63) / 64)), dim3(64), 0, st,
-                           c->d_cone_cam, c->n_tri, c->n_clu, tmp);
+        float4* tmp = clu_cam + 2 * (size_t)c->n_clu;  // second half: unsorted
+        hipLaunchKernelGGL(rt_cluster_prepass, dim3((unsigned)((c->n_clu + 63) / 64)), dim3(64), 0, st, cone_cam,
+                           c->n_tri, c->n_clu, tmp);
         HIP_TRY(c, hipGetLastError());
         hipLaunchKernelGGL(rt_cluster_sort, dim3((unsigned)((c->n_clu + 255) / 256)), dim3(256), 0, st, tmp,
-                           c->n_clu, c->d_clu_cam);
+                           c->n_clu, clu_cam);
         HIP_TRY(c, hipGetLastError());
     }
+    return RT_OK;
+}
+
+// Per-camera prepasses (when the camera position moved), into the
+// context's state.
+static int camera_prepass(rt_ctx* c, const rt_frame* f, hipStream_t st, bool all_tricam)
+{
+    if (!camera_needs_prepass(c, f, all_tricam)) return RT_OK;
+    if (int rc = camera_records(c, f->cam_pos, st, all_tricam, c->d_tricam, c->d_cone_cam, c->d_uni, c->d_clu_cam))
+        return rc;
     std::memcpy(c->cam_key, f->cam_pos, sizeof c->cam_key);
     c->cam_valid = true;
     c->tricam_all = all_tricam || c->n_tri <= kTricamMaxTriangles;
@@ -1728,6 +1764,65 @@ RT_EXPORT int rt_render_async(rt_ctx* c, const rt_frame* f, uint8_t* rgba8_dev, 
     if (!c || !f) return RT_E_ARG;
     HIP_TRY(c, hipSetDevice(c->device));
     return launch(c, f, (unsigned*)rgba8_dev, rgb_dev, (hipStream_t)stream, false, false);
+}
+
+RT_EXPORT int rt_render_sequence_async(rt_ctx* c, const rt_frame* frames, int32_t n, uint8_t* rgba8_dev,
+                                       size_t rgba8_stride, float* rgb_dev, size_t rgb_stride, void* stream)
+{
+    if (!c || (n > 0 && !frames) || n < 0) return RT_E_ARG;
+    if (!c->uploaded) {
+        c->err = "render before rt_upload_scene";
+        return RT_E_STATE;
+    }
+    HIP_TRY(c, hipSetDevice(c->device));
+    hipStream_t st = (hipStream_t)stream;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    HIP_TRY(c, hipStreamIsCapturing(st, &cs));
+    const bool capturing = cs != hipStreamCaptureStatusNone;
+    // everything is checked before anything is enqueued
+    for (int i = 0; i < n; ++i) {
+        const rt_frame* f = frames + i;
+        if (!frame_ok(f) || (f->flags & RT_FLAG_STATS)) {
+            c->err = "bad rt_frame geometry (or RT_FLAG_STATS) in a sequence";
+            return RT_E_ARG;
+        }
+        int cap = 0, lb = 1;
+        if (!pick_kernel<false>(reachable_depth(c, f), c->n_tri, c->n_lights, false, false, cap, lb)) {
+            c->err = "reachable bounce depth exceeds the compiled stack (32)";
+            return RT_E_UNSUPPORTED;
+        }
+    }
+    const int mode = c->opt_light_buffer;
+    const bool lbuf = c->lb_ready && (mode == 1 || (mode == 2 && c->n_tri > kClusterMinTriangles));
+    for (int i = 0; i < n; ++i) {
+        const rt_frame* f = frames + i;
+        const rt_ctx::CamSlot& q = c->seq[i & 1];
+        const int rows = frame_rows(f);
+        if (rows == 0) continue;
+        if (c->n_tri > 0) {
+            if (int rc = camera_records(c, f->cam_pos, st, false, q.tricam, q.cone_cam, q.uni, q.clu_cam)) return rc;
+        }
+        int cap = 0, lb = 1;
+        kernel_fn k = pick_kernel<false>(reachable_depth(c, f), c->n_tri, c->n_lights, lbuf, false, cap, lb);
+        SceneDev S = scene_dev(c, lbuf, false);
+        S.tricam = q.tricam;
+        S.cone_cam = q.cone_cam;
+        S.clu_cam = q.clu_cam;
+        S.uni = (q.uni && c->opt_union) ? q.uni : nullptr;
+        FrameDev F;
+        frame_dev(f, F);
+        unsigned* rgba = rgba8_dev ? (unsigned*)(rgba8_dev + (size_t)i * rgba8_stride) : nullptr;
+        float* rgb = rgb_dev ? (float*)((char*)rgb_dev + (size_t)i * rgb_stride) : nullptr;
+        StatsDev* stats = c->d_stats;
+        void* args[] = {&S, &F, &rgba, &rgb, &stats};
+        dim3 grid((f->width + 15) / 16, (rows + 15) / 16);
+        HIP_TRY(c, hipLaunchKernel((const void*)k, grid, dim3(256), args, 0, st));
+    }
+    if (capturing)
+        c->captured = true;
+    else if (n > 0)
+        note_async(c, st);
+    return RT_OK;
 }
 
 RT_EXPORT int rt_prepare_camera(rt_ctx* c, const rt_frame* f)

@@ -24,7 +24,7 @@ import numpy as np
 
 __all__ = [
     "RtError", "SceneFlat", "Frame", "Stats", "Scene", "Context", "CScene", "lib", "band_rows", "frame_rows",
-    "LIB_PATH", "TRIANGLE", "PLANE", "QUADRIC", "FLAG_STATS", "OPTIONS",
+    "LIB_PATH", "TRIANGLE", "PLANE", "QUADRIC", "FLAG_STATS", "OPTIONS", "camera_path",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -100,6 +100,8 @@ SIGNATURES = {
     "rt_render_float": (ctypes.c_int, [_VP, ctypes.POINTER(Frame), _VP]),
     "rt_render_async": (ctypes.c_int, [_VP, ctypes.POINTER(Frame), _VP, _VP, _VP]),
     "rt_prepare_camera": (ctypes.c_int, [_VP, ctypes.POINTER(Frame)]),
+    "rt_render_sequence_async": (ctypes.c_int, [_VP, ctypes.POINTER(Frame), ctypes.c_int32, _VP, ctypes.c_size_t, _VP,
+                                                ctypes.c_size_t, _VP]),
     "rt_sync": (ctypes.c_int, [_VP]),
     "rt_set_option": (ctypes.c_int, [_VP, ctypes.c_int32, ctypes.c_double]),
     "rt_get_option": (ctypes.c_int, [_VP, ctypes.c_int32, ctypes.POINTER(ctypes.c_double)]),
@@ -236,6 +238,14 @@ class Context:
         arr = (ctypes.c_double * max(1, len(factors)))(*factors)
         _check("rt_set_far_ladder", lib().rt_set_far_ladder(self._h, arr, len(factors)), self._err)
 
+    def render_sequence_async(self, frames, rgba_dev_ptr: int = 0, rgba_stride: int = 0, rgb_dev_ptr: int = 0,
+                              rgb_stride: int = 0, stream: int = 0):
+        """rt_render_sequence_async: a camera path enqueued on `stream`."""
+        arr = (Frame * max(1, len(frames)))(*frames)
+        _check("rt_render_sequence_async",
+               lib().rt_render_sequence_async(self._h, arr, len(frames), rgba_dev_ptr or None, rgba_stride,
+                                              rgb_dev_ptr or None, rgb_stride, stream or None), self._err)
+
     def prepare_camera(self, frame: Frame):
         _check("rt_prepare_camera", lib().rt_prepare_camera(self._h, ctypes.byref(frame)), self._err)
 
@@ -281,6 +291,28 @@ class Context:
             self.close()
         except Exception:
             pass
+
+
+def camera_path(frame: Frame, n: int, yaw_deg: float = 0.5, step=(0.4, 0.0, -0.25)):
+    """n frames of a camera path from `frame`: each step yaws the camera by
+    yaw_deg about its own up axis (orientation rows U, V, N — Scene.cpp:
+    624-660) and moves it by `step` (world units); returns new Frames."""
+    out = []
+    o = np.array(frame.orient[:], np.float64).reshape(4, 4)
+    pos = np.array(frame.cam_pos[:], np.float64)
+    for k in range(n):
+        a = np.deg2rad(yaw_deg * k)
+        U, N = o[0, :3], o[2, :3]
+        m = o.copy()
+        m[0, :3] = np.cos(a) * U - np.sin(a) * N
+        m[2, :3] = np.sin(a) * U + np.cos(a) * N
+        f = frame.copy()
+        for i, v in enumerate(m.astype(np.float32).ravel()):
+            f.orient[i] = float(v)
+        p = (pos + k * np.array(step)).astype(np.float32)
+        f.cam_pos[0], f.cam_pos[1], f.cam_pos[2] = (float(x) for x in p)
+        out.append(f)
+    return out
 
 
 class CScene:

@@ -181,3 +181,59 @@ def test_options_round_trip_and_validation():
         ctx.set_far_ladder([2.0] * 9)
     ctx.set_far_ladder([2.0, 8.0])
     ctx.set_far_ladder(None)
+
+
+@pytest.mark.parametrize("which,w,h,depth", [("scene2", 320, 240, 0), ("heightfield", 480, 320, 1),
+                                             ("scene7", 200, 150, 3), ("scene9", 160, 120, 5)])
+def test_sequence_matches_cold_renders(which, w, h, depth, heightfield_path):
+    """rt_render_sequence_async over a camera path (yaw + translation per
+    frame): every frame equals a fresh context's synchronous render."""
+    path = heightfield_path if which == "heightfield" else scene(int(which[-1]))
+    s = rt_amd.Scene(path, w, h, depth)
+    frames = rt_amd.camera_path(s.frame, 5, yaw_deg=1.5, step=(2.0, 0.5, -1.0))
+    cold = rt_amd.Context(0)
+    cold.upload(s)
+    want = [cold.render_float(f) for f in frames]
+    ctx = rt_amd.Context(0)
+    ctx.upload(s)
+    out = torch.zeros((len(frames), h, w, 3), dtype=torch.float32, device="cuda")
+    ctx.render_sequence_async(frames, 0, 0, out.data_ptr(), h * w * 12, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    for i, f in enumerate(want):
+        assert bits_equal(out[i].cpu().numpy(), f), i
+    # the camera of the last frame is not left "current" by a sequence: a
+    # synchronous render of it afterwards prepares it and is exact too
+    assert bits_equal(ctx.render_float(frames[-1]), want[-1])
+
+
+def test_sequence_graph_replay_is_self_contained():
+    """A camera path captured into a hipGraph replays the reference's frames
+    even after other cameras and sequences were rendered on the context."""
+    w, h = 320, 240
+    s = rt_amd.Scene(scene(2), w, h, 0)
+    frames = rt_amd.camera_path(s.frame, 6, yaw_deg=2.0, step=(1.5, 0.0, -2.0))
+    other = rt_amd.camera_path(s.frame, 3, yaw_deg=-3.0, step=(-4.0, 1.0, 3.0))
+    cold = rt_amd.Context(0)
+    cold.upload(s)
+    want = [cold.render(f) for f in frames]
+    want_other = [cold.render(f) for f in other]
+    ctx = rt_amd.Context(0)
+    ctx.upload(s)
+    out = torch.zeros((len(frames), h, w, 4), dtype=torch.uint8, device="cuda")
+    tmp = torch.zeros((len(other), h, w, 4), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        ctx.render_sequence_async(frames, out.data_ptr(), h * w * 4, 0, 0, torch.cuda.current_stream().cuda_stream)
+    for rep in range(3):
+        out.zero_()
+        g.replay()
+        # other work on the same context between replays, no host sync
+        ctx.render_async(other[rep], tmp[rep].data_ptr(), 0, torch.cuda.current_stream().cuda_stream)
+        ctx.render_sequence_async(other, tmp.data_ptr(), h * w * 4, 0, 0, torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        for i, f in enumerate(want):
+            assert np.array_equal(out[i].cpu().numpy(), f), (rep, i)
+        for i, f in enumerate(want_other):
+            assert np.array_equal(tmp[i].cpu().numpy(), f), (rep, i)
+        assert np.array_equal(ctx.render(other[rep]), want_other[rep])
