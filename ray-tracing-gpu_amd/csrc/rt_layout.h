@@ -174,12 +174,14 @@ struct Counters {
     } while (0)
 __device__ unsigned long long rt_prof_acc[8];
 #define RT_EV(cnt, i) (++(cnt).ev[i])
+#define RT_EVN(cnt, i, n) ((cnt).ev[i] += (n))
 __device__ unsigned long long rt_prof_ev[8];
 // per-tile record (16 x u32: total clocks lo/hi, 8 section clocks >> 8, events 1 2 4 5 6 7)
 __device__ unsigned* rt_prof_tiles;
 __device__ int rt_prof_ntiles;
 #else
 #define RT_EV(cnt, i) ((void)0)
+#define RT_EVN(cnt, i, n) ((void)0)
 #define RT_MARK(cnt, i) \
     do {                \
     } while (0)

@@ -533,6 +533,7 @@ __device__ __forceinline__ bool lb_slot(const SceneDev& S, int slot, const Vec3 
         if (__any(go)) {
             ++cnt.tri;
             RT_EV(cnt, 4);
+            RT_EVN(cnt, 7, (unsigned)__popcll(__ballot(go)));  // lanes doing a test (RT_PROF)
             if (go) {
                 const Vec3 e1 = make3(c1.x, c1.y, c1.z), e2 = make3(c1.w, c2.x, c2.y);
                 const TriU u = tri_u(make3(c0.x, c0.y, c0.z), e1, e2, P, L);
@@ -611,7 +612,6 @@ __device__ __forceinline__ void shadow_opaque_lb(const SceneDev& S, int l, const
             if (!__any(reach)) continue;
             const TriRec tr = load_tri(S, k);
             ++cnt.tri;
-            RT_EV(cnt, 7);
             const TriU r = tri_u(tr.p0, tr.e1, tr.e2, P, L);
             if (!__any(r.ok && !o2)) continue;
             float t;

@@ -25,7 +25,7 @@ sys.path.insert(0, REPO)
 EVENTS = ["cam_cluster_batches", "cam_member_batches", "cam_exact", "shadow_cluster_ballots",
           "shadow_member_batches", "shadow_exact", "shadow_clusters_by_dcap_only", "shadow_clusters_by_cone"]
 # with the light buffer (shadow_opaque_lb), events 3-7 are its own
-EVENTS_LB = ["lb_one_cell_walks", "lb_multi_cell_walks", EVENTS[2]] + ["lb_walk_iters", "lb_walk_exact", "lb_dcap_iters", "lb_fallback_waves", "lb_fallback_exact"]
+EVENTS_LB = ["lb_one_cell_walks", "lb_multi_cell_walks", EVENTS[2]] + ["lb_walk_iters", "lb_walk_exact", "lb_dcap_iters", "lb_fallback_waves", "lb_walk_active_lanes"]
 NAMES = ["setup", "primary", "shade_setup", "shadow_cull", "shadow_exact_tri", "lambert_phong", "store", "shadow_planes"]
 
 
