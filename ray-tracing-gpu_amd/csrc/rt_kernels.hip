@@ -34,6 +34,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/rt.h"
@@ -819,11 +820,15 @@ static int lb_build(rt_ctx* c, int ntr, int n_opaque, const std::vector<const fl
             LB_TRY(hipMemcpyAsync(h.data() + (size_t)j * ntr * 2, cones[j], (size_t)ntr * 2 * sizeof(float4),
                                   hipMemcpyDeviceToHost, st));
         LB_TRY(hipStreamSynchronize(st));
-        for (int j = 0; j < nl; ++j) {
+        // per slot on its own host thread (independent): cell resolution from
+        // the median cone angle, the triangles in dmin order, the dcap list
+        std::vector<std::vector<int>> perms((size_t)nl), dperms((size_t)nl);
+        auto prep = [&](int j) {
             Slot& b = B[j];
             const float4* hj = h.data() + (size_t)j * ntr * 2;
             std::vector<double> T;
-            std::vector<int> perm, dperm;
+            std::vector<int>& perm = perms[j];
+            std::vector<int>& dperm = dperms[j];
             for (int k = 0; k < n_opaque; ++k) {
                 const float4 c0 = hj[2 * k], c1 = hj[2 * k + 1];
                 if (c0.w > 0.0f && c0.w <= 1.0f) T.push_back(std::acos((double)c0.w));
@@ -842,12 +847,22 @@ static int lb_build(rt_ctx* c, int ntr, int n_opaque, const std::vector<const fl
             auto key = [&](int k) { const float z = hj[2 * k + 1].z; return z == z ? z : -INFINITY; };
             std::sort(dperm.begin(), dperm.end(),
                       [&](int x, int y) { return key(x) < key(y) || (key(x) == key(y) && x < y); });
+        };
+        if (nl > 1 && (size_t)n_opaque * nl > 20000) {
+            std::vector<std::thread> th;
+            for (int j = 0; j < nl; ++j) th.emplace_back(prep, j);
+            for (auto& t : th) t.join();
+        } else {
+            for (int j = 0; j < nl; ++j) prep(j);
+        }
+        for (int j = 0; j < nl; ++j) {
+            Slot& b = B[j];
             b.perm0 = perm_all.size();
-            b.nperm = perm.size();
-            perm_all.insert(perm_all.end(), perm.begin(), perm.end());
+            b.nperm = perms[j].size();
+            perm_all.insert(perm_all.end(), perms[j].begin(), perms[j].end());
             b.dperm0 = dperm_all.size();
-            b.ndperm = dperm.size();
-            dperm_all.insert(dperm_all.end(), dperm.begin(), dperm.end());
+            b.ndperm = dperms[j].size();
+            dperm_all.insert(dperm_all.end(), dperms[j].begin(), dperms[j].end());
             const unsigned G = (unsigned)(b.R / kLbGroup);
             b.nsup = 6u * G * G;
             b.ncell = 6u * (unsigned)b.R * (unsigned)b.R;
