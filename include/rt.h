@@ -190,6 +190,18 @@ int rt_prepare_camera(rt_ctx*, const rt_frame* frame);
  * has finished. */
 int rt_sync(rt_ctx*);
 
+/* ABI 4: the CPU backend (the reference's CPU branch of
+ * LancerRayons, Scene.cpp:1535-1563, which it chose on
+ * CVar::g_ComputerShadersON, Var.cpp:11).  Explicit only: a context made by
+ * rt_create_cpu (threads <= 0: all cores; no HIP call is made) takes
+ * rt_upload_scene and renders with rt_cpu_render / rt_cpu_render_float into
+ * host memory — the HIP path's images, bit for bit, by brute force on host
+ * threads.  The HIP render entry points return RT_E_STATE on a CPU context,
+ * and rt_create never returns one: a missing GPU is an error, never a switch. */
+int rt_create_cpu(int32_t threads, rt_ctx** out);
+int rt_cpu_render(rt_ctx*, const rt_frame*, uint8_t* rgba8_out);
+int rt_cpu_render_float(rt_ctx*, const rt_frame*, float* rgb_out);
+
 /* ABI 4: context options.  A/B and test switches and tuning knobs; no option
  * changes a single bit of any image.  Upload options take effect at the next
  * rt_upload_scene, launch options at the next render.                      */

@@ -38,6 +38,7 @@
 #include <vector>
 
 #include "../../include/rt.h"
+#include "rt_cpu.hpp"
 #include "rt_scan.h"
 #include "rt_shade.h"
 
@@ -372,6 +373,10 @@ using namespace rt;
 
 struct rt_ctx {
     int device = 0;
+    // CPU backend (rt_create_cpu): no HIP object is ever made for it
+    bool cpu = false;
+    int cpu_threads = 0;
+    void* cpu_scene = nullptr;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     float4* d_geom = nullptr;
@@ -577,6 +582,7 @@ static int ensure_scan(rt_ctx* c, size_t words)
 RT_EXPORT int rt_sync(rt_ctx* c)
 {
     if (!c) return RT_E_ARG;
+    if (c->cpu) return RT_OK;  // CPU renders are synchronous
     if (!c->stream) return RT_E_STATE;
     HIP_TRY(c, hipSetDevice(c->device));
     return sync_all(c);
@@ -637,9 +643,32 @@ RT_EXPORT int rt_set_far_ladder(rt_ctx* c, const double* f, int32_t n)
     return RT_OK;
 }
 
+RT_EXPORT int rt_create_cpu(int32_t threads, rt_ctx** out)
+{
+    if (!out) return RT_E_ARG;
+    rt_ctx* c = new rt_ctx();
+    c->cpu = true;
+    c->cpu_threads = threads;
+    *out = c;
+    return RT_OK;
+}
+
+// The HIP entry points refuse a CPU context (and the CPU ones a HIP context
+// without a host scene): the backend is the caller's explicit choice.
+static int not_cpu(rt_ctx* c)
+{
+    c->err = "a CPU context (rt_create_cpu) renders with rt_cpu_render / rt_cpu_render_float";
+    return RT_E_STATE;
+}
+
 RT_EXPORT void rt_destroy(rt_ctx* c)
 {
     if (!c) return;
+    if (c->cpu) {
+        cpu_free(c->cpu_scene);
+        delete c;
+        return;
+    }
     if (c->stream) {
         (void)hipSetDevice(c->device);
         (void)sync_all(c);
@@ -980,6 +1009,18 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
     if (!c || !s || s->n_surfaces < 0 || s->n_lights < 0) return RT_E_ARG;
     if (s->n_surfaces > 0 && (!s->type || !s->geom || !s->material)) return RT_E_ARG;
     if (s->n_lights > 0 && !s->lights) return RT_E_ARG;
+    if (c->cpu) {
+        c->uploaded = false;
+        const int rc = cpu_upload(&c->cpu_scene, s);
+        if (rc) {
+            c->err = "unknown surface type";
+            return rc;
+        }
+        c->n_surf = s->n_surfaces;
+        c->n_lights = s->n_lights;
+        c->uploaded = true;
+        return RT_OK;
+    }
     if (!c->stream) return RT_E_STATE;
     HIP_TRY(c, hipSetDevice(c->device));
     // nothing in flight may still read the buffers replaced below
@@ -1749,6 +1790,7 @@ static int ensure_scratch(rt_ctx* c, size_t bytes)
 static int render_sync(rt_ctx* c, const rt_frame* f, void* out, bool as_float)
 {
     if (!c || !f || !out) return RT_E_ARG;
+    if (c->cpu) return not_cpu(c);
     HIP_TRY(c, hipSetDevice(c->device));
     // every state write and render of this call comes after the async
     // renders already enqueued on other streams
@@ -1777,6 +1819,7 @@ RT_EXPORT int rt_render_float(rt_ctx* c, const rt_frame* f, float* rgb_out) { re
 RT_EXPORT int rt_render_async(rt_ctx* c, const rt_frame* f, uint8_t* rgba8_dev, float* rgb_dev, void* stream)
 {
     if (!c || !f) return RT_E_ARG;
+    if (c->cpu) return not_cpu(c);
     HIP_TRY(c, hipSetDevice(c->device));
     return launch(c, f, (unsigned*)rgba8_dev, rgb_dev, (hipStream_t)stream, false, false);
 }
@@ -1785,6 +1828,7 @@ RT_EXPORT int rt_render_sequence_async(rt_ctx* c, const rt_frame* frames, int32_
                                        size_t rgba8_stride, float* rgb_dev, size_t rgb_stride, void* stream)
 {
     if (!c || (n > 0 && !frames) || n < 0) return RT_E_ARG;
+    if (c->cpu) return not_cpu(c);
     if (!c->uploaded) {
         c->err = "render before rt_upload_scene";
         return RT_E_STATE;
@@ -1843,6 +1887,7 @@ RT_EXPORT int rt_render_sequence_async(rt_ctx* c, const rt_frame* frames, int32_
 RT_EXPORT int rt_prepare_camera(rt_ctx* c, const rt_frame* f)
 {
     if (!c || !f) return RT_E_ARG;
+    if (c->cpu) return not_cpu(c);
     if (!c->uploaded) {
         c->err = "rt_prepare_camera before rt_upload_scene";
         return RT_E_STATE;
@@ -1862,6 +1907,38 @@ RT_EXPORT int rt_prepare_camera(rt_ctx* c, const rt_frame* f)
     c->state_pending = false;
     c->state_stream = nullptr;
     return RT_OK;
+}
+
+static int cpu_render_sync(rt_ctx* c, const rt_frame* f, uint8_t* rgba, float* rgb)
+{
+    if (!c || !f || (!rgba && !rgb)) return RT_E_ARG;
+    if (!c->cpu) {
+        c->err = "rt_cpu_render needs a CPU context (rt_create_cpu)";
+        return RT_E_STATE;
+    }
+    if (!c->uploaded) {
+        c->err = "render before rt_upload_scene";
+        return RT_E_STATE;
+    }
+    if (!frame_ok(f)) {
+        c->err = "bad rt_frame geometry";
+        return RT_E_ARG;
+    }
+    c->last = rt_stats{};
+    double ms = 0.0;
+    const int rc = cpu_render(c->cpu_scene, c->cpu_threads, f, frame_rows(f), rgba, rgb, &ms);
+    c->last.kernel_ms = (float)ms;
+    return rc;
+}
+
+RT_EXPORT int rt_cpu_render(rt_ctx* c, const rt_frame* f, uint8_t* rgba8_out)
+{
+    return cpu_render_sync(c, f, rgba8_out, nullptr);
+}
+
+RT_EXPORT int rt_cpu_render_float(rt_ctx* c, const rt_frame* f, float* rgb_out)
+{
+    return cpu_render_sync(c, f, nullptr, rgb_out);
 }
 
 RT_EXPORT int rt_last_stats(rt_ctx* c, rt_stats* out)

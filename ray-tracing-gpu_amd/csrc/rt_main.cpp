@@ -2,6 +2,7 @@
 //
 //   rt_render <scene.dat> [-x W] [-y H] [-d depth] [-o out.ppm] [-g gpus]
 //             [--device first] [--bands] [-n frames] [-s]
+//             [--backend hip|cpu] [--threads N]
 //
 // Kept from Main.cpp:51-199: argv[1] is the scene file, -x / -y set the
 // resolution (default 512x256, Var.cpp:4-5), the same [ETAT]/[ERREUR] log
@@ -20,7 +21,9 @@
 // context rendering its row slab (or, with --bands, its cyclic 16-row
 // bands) straight into its part of the host frame; the parts are assembled
 // in host memory — the same partition as bench.py's ranks, without a
-// collective.
+// collective.  --backend cpu renders on host threads instead (rt_create_cpu,
+// the reference's CPU branch, chosen there by CVar::g_ComputerShadersON):
+// the same image, the GPU never touched.
 #include <hip/hip_runtime_api.h>
 
 #include <chrono>
@@ -39,14 +42,27 @@ static int fail(const char* what, int rc, const char* msg)
     return 1;
 }
 
+// The frame (memory row 0 = bottom scanline) as a binary PPM, top row first.
+static int write_ppm(const char* path, int W, int H, const std::vector<uint8_t>& img)
+{
+    FILE* f = std::fopen(path, "wb");
+    if (!f) return 1;
+    std::fprintf(f, "P6\n%d %d\n255\n", W, H);
+    for (int y = H - 1; y >= 0; --y)
+        for (int x = 0; x < W; ++x) std::fwrite(&img[((size_t)y * W + x) * 4], 1, 3, f);
+    std::fclose(f);
+    std::printf("[ETAT]: Image ecrite dans %s\n", path);
+    return 0;
+}
+
 int main(int argc, char** argv)
 {
     if (argc < 2) {
         std::fprintf(stderr, "[ERREUR]: Aucune fichier de scene ne fut passe en argument !\n");
         return 1;
     }
-    int W = 512, H = 256, depth = 0, dev0 = 0, frames = 1, gpus = 1;
-    bool stats = false, bands = false;
+    int W = 512, H = 256, depth = 0, dev0 = 0, frames = 1, gpus = 1, threads = 0;
+    bool stats = false, bands = false, cpu = false;
     const char* out = nullptr;
     for (int i = 2; i < argc; ++i) {
         if (argv[i][0] != '-') continue;
@@ -59,6 +75,18 @@ int main(int argc, char** argv)
         }
         if (std::strcmp(argv[i], "--bands") == 0) {
             bands = true;
+            continue;
+        }
+        if (std::strcmp(argv[i], "--threads") == 0) {
+            next(threads);
+            continue;
+        }
+        if (std::strcmp(argv[i], "--backend") == 0) {
+            const char* b = i + 1 < argc ? argv[++i] : "";
+            if (std::strcmp(b, "cpu") == 0)
+                cpu = true;
+            else if (std::strcmp(b, "hip") != 0)
+                return fail("arguments", RT_E_ARG, "--backend is hip or cpu");
             continue;
         }
         switch (argv[i][1]) {
@@ -92,6 +120,25 @@ int main(int argc, char** argv)
     rt_scene_get_frame(scene, &frame);
     if (stats) frame.flags |= RT_FLAG_STATS;
 
+    if (cpu) {  // the CPU backend: one context, host threads
+        if (gpus != 1 || bands) return fail("arguments", RT_E_ARG, "-g / --bands are for the hip backend");
+        rt_ctx* c = nullptr;
+        if ((rc = rt_create_cpu(threads, &c))) return fail("rt_create_cpu", rc, "");
+        if ((rc = rt_upload_scene(c, &flat))) return fail("rt_upload_scene", rc, rt_last_error(c));
+        std::vector<uint8_t> img((size_t)W * H * 4);
+        std::printf("[ETAT]: Lancer de rayons (CPU)...\n");
+        double total = 0.0;
+        for (int k = 0; k < frames; ++k) {
+            const auto t0 = std::chrono::steady_clock::now();
+            if ((rc = rt_cpu_render(c, &frame, img.data()))) return fail("LancerRayons", rc, rt_last_error(c));
+            total += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        }
+        std::printf("[ETAT]: Termine! --> Temps total de rendu : %.6f secondes (%d frame(s), CPU)\n", total, frames);
+        if (out && write_ppm(out, W, H, img)) return fail("fopen", -1, out);
+        rt_destroy(c);
+        rt_scene_destroy(scene);
+        return 0;
+    }
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail("rt_create", RT_E_HIP, "no HIP device");
     // one context per GPU share; part r = rows of slab r, or band set r
@@ -161,15 +208,7 @@ int main(int argc, char** argv)
                     (unsigned long long)st.shadow_rays, (unsigned long long)st.shadow_tests_skipped,
                     st.stack_depth, (unsigned long long)st.triangle_tests, (unsigned long long)st.plane_tests,
                     (unsigned long long)st.quadric_tests);
-    if (out) {
-        FILE* f = std::fopen(out, "wb");
-        if (!f) return fail("fopen", -1, out);
-        std::fprintf(f, "P6\n%d %d\n255\n", W, H);
-        for (int y = H - 1; y >= 0; --y)  // PPM: top row first
-            for (int x = 0; x < W; ++x) std::fwrite(&full[((size_t)y * W + x) * 4], 1, 3, f);
-        std::fclose(f);
-        std::printf("[ETAT]: Image ecrite dans %s\n", out);
-    }
+    if (out && write_ppm(out, W, H, full)) return fail("fopen", -1, out);
     for (rt_ctx* c : ctx) rt_destroy(c);
     rt_scene_destroy(scene);
     return 0;

@@ -23,7 +23,8 @@ from typing import Optional
 import numpy as np
 
 __all__ = [
-    "RtError", "SceneFlat", "Frame", "Stats", "Scene", "Context", "CScene", "lib", "band_rows", "frame_rows",
+    "RtError", "SceneFlat", "Frame", "Stats", "Scene", "Context", "CpuContext", "CScene", "lib", "band_rows",
+    "frame_rows",
     "LIB_PATH", "TRIANGLE", "PLANE", "QUADRIC", "FLAG_STATS", "OPTIONS", "camera_path",
 ]
 
@@ -95,6 +96,9 @@ SIGNATURES = {
     "rt_scene_error": (ctypes.c_char_p, [_VP]),
     "rt_scene_destroy": (None, [_VP]),
     "rt_create": (ctypes.c_int, [ctypes.c_int32, ctypes.POINTER(_VP)]),
+    "rt_create_cpu": (ctypes.c_int, [ctypes.c_int32, ctypes.POINTER(_VP)]),
+    "rt_cpu_render": (ctypes.c_int, [_VP, ctypes.POINTER(Frame), _VP]),
+    "rt_cpu_render_float": (ctypes.c_int, [_VP, ctypes.POINTER(Frame), _VP]),
     "rt_upload_scene": (ctypes.c_int, [_VP, ctypes.POINTER(SceneFlat)]),
     "rt_render": (ctypes.c_int, [_VP, ctypes.POINTER(Frame), _VP]),
     "rt_render_float": (ctypes.c_int, [_VP, ctypes.POINTER(Frame), _VP]),
@@ -315,10 +319,58 @@ def camera_path(frame: Frame, n: int, yaw_deg: float = 0.5, step=(0.4, 0.0, -0.2
     return out
 
 
-class CScene:
-    """The reference's CScene verbs over the HIP backend (Scene.h:41-70)."""
+class CpuContext:
+    """The CPU backend (rt_create_cpu / rt_cpu_render*): the same images on
+    host threads.  Explicit only — Context never falls back to it."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, threads: int = 0):
+        L = lib()
+        self._h = _VP()
+        _check("rt_create_cpu", L.rt_create_cpu(threads, ctypes.byref(self._h)))
+
+    def _err(self) -> str:
+        return (lib().rt_last_error(self._h) or b"").decode()
+
+    def upload(self, scene: Scene):
+        _check("rt_upload_scene", lib().rt_upload_scene(self._h, ctypes.byref(scene.flat)), self._err)
+
+    def render(self, frame: Frame) -> np.ndarray:
+        out = np.zeros((frame_rows(frame), frame.width, 4), np.uint8)
+        _check("rt_cpu_render", lib().rt_cpu_render(self._h, ctypes.byref(frame), out.ctypes.data), self._err)
+        return out
+
+    def render_float(self, frame: Frame) -> np.ndarray:
+        out = np.zeros((frame_rows(frame), frame.width, 3), np.float32)
+        _check("rt_cpu_render_float", lib().rt_cpu_render_float(self._h, ctypes.byref(frame), out.ctypes.data),
+               self._err)
+        return out
+
+    def stats(self) -> Stats:
+        s = Stats()
+        _check("rt_last_stats", lib().rt_last_stats(self._h, ctypes.byref(s)))
+        return s
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().rt_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class CScene:
+    """The reference's CScene verbs (Scene.h:41-70) over the HIP backend, or —
+    backend="cpu", the reference's CVar::g_ComputerShadersON = false — the
+    CPU backend."""
+
+    def __init__(self, device: int = 0, backend: str = "hip", threads: int = 0):
+        if backend not in ("hip", "cpu"):
+            raise ValueError("backend is 'hip' or 'cpu'")
+        self._backend, self._threads = backend, threads
         self._w, self._h = 512, 256          # Var.cpp:4-5
         self._max_bounces = 20               # Scene.cpp:68
         self._min_energy = 0.01              # Scene.cpp:69
@@ -351,7 +403,7 @@ class CScene:
         if self._scene is None:
             self._scene = Scene(self._path, self._w, self._h, self._max_bounces, self._min_energy, self._scene_ior)
             if self._ctx is None:
-                self._ctx = Context(self._device)
+                self._ctx = Context(self._device) if self._backend == "hip" else CpuContext(self._threads)
             self._ctx.upload(self._scene)
         return self._scene
 
