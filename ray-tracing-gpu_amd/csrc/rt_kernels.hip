@@ -1643,7 +1643,13 @@ static bool frame_ok(const rt_frame* f)
 // on another stream.  Capturing: nothing may be written (RT_E_STATE).
 static int prepare_state(rt_ctx* c, const rt_frame* f, hipStream_t st, bool sync_path, bool capturing, bool cb_want)
 {
-    if (!sync_path) {
+    if (capturing && c->state_pending && c->state_stream != st) {
+        // a wait on an event recorded outside the capture cannot be captured
+        c->err = "hipGraph capture: the camera state was written by an async render on another stream "
+                 "(rt_sync or a synchronous render first)";
+        return RT_E_STATE;
+    }
+    if (!sync_path && !capturing) {
         if (int rc = wait_state(c, st)) return rc;
     }
     const bool need_prep = camera_needs_prepass(c, f, cb_want);

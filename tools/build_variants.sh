@@ -11,7 +11,7 @@ pids=()
 for spec in "$@"; do
   name="${spec%%=*}"; defs="${spec#*=}"
   /opt/rocm/bin/hipcc $FLAGS $defs --offload-arch=gfx950 -shared -o lib/var/librt_amd_$name.so \
-      csrc/rt_kernels.hip csrc/rt_scene.cpp -Wl,-rpath,/opt/rocm/lib &
+      csrc/rt_kernels.hip csrc/rt_scene.cpp csrc/rt_cpu.cpp -Wl,-rpath,/opt/rocm/lib &
   pids+=($!)
 done
 for p in "${pids[@]}"; do wait $p; done
