@@ -237,3 +237,33 @@ def test_sequence_graph_replay_is_self_contained():
         for i, f in enumerate(want_other):
             assert np.array_equal(tmp[i].cpu().numpy(), f), (rep, i)
         assert np.array_equal(ctx.render(other[rep]), want_other[rep])
+
+
+def test_capture_after_async_prepass_on_another_stream():
+    """A camera first prepared by an async render on stream s1 (its state
+    write pending there) cannot be captured on another stream — that would
+    need a wait on an event outside the capture — until rt_sync; then it can,
+    and the replay is exact."""
+    w, h = 320, 240
+    s = rt_amd.Scene(scene(2), w, h, 0)
+    f = _cameras(s, [(5.0, -2.0)])[0]
+    want = _cold(scene(2), w, h, [f])[0]
+    ctx = rt_amd.Context(0)
+    ctx.upload(s)
+    s1 = torch.cuda.Stream()
+    out = torch.zeros((h, w, 3), dtype=torch.float32, device="cuda")
+    ctx.render_async(f, 0, out.data_ptr(), s1.cuda_stream)  # prepass on s1
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        with pytest.raises(rt_amd.RtError) as e:
+            ctx.render_async(f, 0, out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    assert e.value.code == -4
+    ctx.sync()
+    torch.cuda.synchronize()
+    g2 = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g2):
+        ctx.render_async(f, 0, out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    out.zero_()
+    g2.replay()
+    torch.cuda.synchronize()
+    assert bits_equal(out.cpu().numpy(), want)
