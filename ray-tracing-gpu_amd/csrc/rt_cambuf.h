@@ -13,6 +13,15 @@
 namespace rt {
 
 // ---------------------------------------------------------- camera buffer
+// Does the frame's slab (or band set) cover any row of tile row ty?  Only
+// those tiles get lists: a rank rendering 1/n of the frame builds 1/n of
+// the buffer.  (Bands are multiples of 16 rows, so no tile straddles two.)
+__device__ __forceinline__ bool cb_tile_row_needed(const FrameDev& F, int ty)
+{
+    if (F.band_rows > 0) return ((ty * 8) / F.band_rows) % F.band_count == F.band_index;
+    return ty * 8 < F.row_end && ty * 8 + 8 > F.row_begin;
+}
+
 // One wave per 8x8 tile of the full frame, laid out like rt_trace_kernel
 // (256-thread blocks of 2 x 2 tiles): the tile's 64 camera rays (camera_dir
 // on the same clamped pixels as the trace kernel, so the same bits), their
@@ -29,6 +38,13 @@ __global__ __launch_bounds__(256) void rt_cb_build(const SceneDev S, const Frame
     const int tx = blockIdx.x * 2 + (wave & 1), ty = blockIdx.y * 2 + (wave >> 1);
     if (tx * 8 >= F.width || ty * 8 >= F.height) return;
     const int tile = ty * S.cb_tiles_x + tx;
+    if (!cb_tile_row_needed(F, ty)) {  // outside the frame's rows: no list
+        if (!FILL && lane == 0) {
+            flag[tile] = 1u;
+            cnt[tile] = 0u;
+        }
+        return;
+    }
     const int px = tx * 8 + (lane & 7), py = ty * 8 + (lane >> 3);
     const Vec3 D = camera_dir(F, px < F.width ? px : F.width - 1, py < F.height ? py : F.height - 1);
     const WaveCone wc = wave_cone(D, true);
@@ -177,7 +193,12 @@ __global__ __launch_bounds__(256) void rt_cb_block(const SceneDev S, const Frame
     for (int j = 0; j < NT / 4; ++j) {
         const int lt = wave * (NT / 4) + j;
         const int tx = bx0 + (lt % BLK), ty = by0 + (lt / BLK);
-        const bool present = tx < S.cb_tiles_x && ty < tiles_y;
+        const bool inside = tx < S.cb_tiles_x && ty < tiles_y;
+        const bool present = inside && cb_tile_row_needed(F, ty);
+        if (inside && !present && lane == 0 && !FILL) {  // outside the frame's rows: no list
+            flag[ty * S.cb_tiles_x + tx] = 1u;
+            cnt[ty * S.cb_tiles_x + tx] = 0u;
+        }
         WaveCone wc;
         wc.ok = false;
         if (present) {

@@ -418,7 +418,10 @@ struct rt_ctx {
     size_t scan_words = 0;
     unsigned long long* h_word = nullptr;  // pinned: totals read back by the builds
     int cb_tiles_x = 0, cb_ntiles = 0;
-    float cb_key[25] = {};      // cam_pos, orient, half_w, half_h, inv_w, inv_h, width, height (as float bits)
+    // cam_pos, orient, half_w, half_h, inv_w, inv_h, width, height, and the
+    // tile rows the lists were built for: row_begin, row_end, band_rows,
+    // band_count, band_index (ints as float bits)
+    float cb_key[30] = {};
     bool cb_valid = false;
     double cb_build_ms = 0.0;
     size_t cb_entries = 0;
@@ -1434,6 +1437,10 @@ static void cb_key_of(const rt_frame* f, float* key)
     key[22] = f->inv_h;
     std::memcpy(key + 23, &f->width, sizeof(int));
     std::memcpy(key + 24, &f->height, sizeof(int));
+    // the rows whose tiles have lists (a rank's slab or band set)
+    const int32_t rows[5] = {f->band_rows ? 0 : f->row_begin, f->band_rows ? 0 : f->row_end, f->band_rows,
+                             f->band_rows ? f->band_count : 0, f->band_rows ? f->band_index : 0};
+    std::memcpy(key + 25, rows, sizeof rows);
 }
 
 static void frame_dev(const rt_frame* f, FrameDev& F)
@@ -1623,7 +1630,7 @@ static int cb_build(rt_ctx* c, const rt_frame* f, hipStream_t st)
 static bool cb_matches(const rt_ctx* c, const rt_frame* f)
 {
     if (!c->cb_valid) return false;
-    float key[25];
+    float key[30];
     cb_key_of(f, key);
     return std::memcmp(key, c->cb_key, sizeof key) == 0;
 }

@@ -288,3 +288,38 @@ def test_wave_primitives_selftest(ctx):
     fails = ctypes.c_uint(99)
     assert f(0, 4096, ctypes.byref(fails)) == 0
     assert fails.value == 0
+
+
+@pytest.mark.parametrize("which", ["scene2", "heightfield"])
+def test_camera_buffer_covers_only_the_ranks_rows(which, heightfield_path):
+    """A slab (or band set) render builds the camera buffer for its own tile
+    rows only — 1/n of the lists for 1/n of the frame — and still renders
+    the full frame's bits for those rows."""
+    import ctypes
+
+    path = scene(2) if which == "scene2" else heightfield_path
+    s = rt_amd.Scene(path, 1920, 1080, 0)
+    c = rt_amd.Context(0)
+    c.upload(s)
+    L = rt_amd.lib()
+    L.rt_debug_cb_info.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+
+    def entries():
+        info = (ctypes.c_double * 6)()
+        assert L.rt_debug_cb_info(c._h, info, 6) == 0 and info[0] == 1.0
+        return info[1]
+
+    full = c.render_float(s.frame)
+    n_full = entries()
+    f = s.frame.copy()
+    f.row_begin, f.row_end = 136, 272  # rank 1 of 8 (slab_rows)
+    assert bits_equal(c.render_float(f), full[136:272])
+    assert 0 < entries() < n_full / 4
+    f = s.frame.copy()
+    f.band_rows, f.band_count, f.band_index = 16, 8, 3
+    part = c.render_float(f)
+    assert 0 < entries() < n_full / 4
+    for q in range(part.shape[0] // 16):
+        a = (q * 8 + 3) * 16
+        e = min(1080, a + 16)
+        assert bits_equal(part[q * 16: q * 16 + (e - a)], full[a:e])
