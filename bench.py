@@ -240,9 +240,16 @@ def progressive(ctx, frame, W, rows, n=60):
         ctx.render_sequence_async(path, ring.data_ptr(), stride, 0, 0, torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     direct = (time.perf_counter() - t0) / (3 * n)
+    import gc
+
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
-        ctx.render_sequence_async(path, ring.data_ptr(), stride, 0, 0, torch.cuda.current_stream().cuda_stream)
+    gc.collect()
+    gc.disable()  # no finalizer may synchronise a stream during the capture
+    try:
+        with torch.cuda.graph(g):
+            ctx.render_sequence_async(path, ring.data_ptr(), stride, 0, 0, torch.cuda.current_stream().cuda_stream)
+    finally:
+        gc.enable()
     g.replay()
     torch.cuda.synchronize()
     t0 = time.perf_counter()

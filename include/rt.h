@@ -215,9 +215,13 @@ enum {
                                    at least 128 cells per face edge); > 0 sets R alone */
     RT_OPT_DCOV_NEAR = 5,       /* upload: big lists' near light-buffer distance, x the
                                    light's farthest triangle; 0 = default (1.25) */
-    RT_OPT_CB_INLINE_MAX_MB = 6 /* launch: camera-buffer entries carry inline camera
+    RT_OPT_CB_INLINE_MAX_MB = 6,/* launch: camera-buffer entries carry inline camera
                                    records while they fit this many MiB (default 128;
                                    0 = never: the index walk) */
+    RT_OPT_HOST_CHUNK_MB = 7    /* launch: synchronous renders into host memory render
+                                   and copy in row chunks of this many MiB of output,
+                                   each copy overlapping the next chunk (default 8;
+                                   0 = one kernel, then one copy) */
 };
 int rt_set_option(rt_ctx*, int32_t option, double value);
 int rt_get_option(rt_ctx*, int32_t option, double* value);

@@ -446,6 +446,10 @@ struct rt_ctx {
     // per-camera state not yet host-synced (an async camera prepass).
     std::vector<hipStream_t> async_streams;
     hipEvent_t ev_fence = nullptr, ev_state = nullptr;
+    // synchronous renders into host memory: the slab in row chunks, each
+    // copied over PCIe on copy_stream while the next one renders
+    hipStream_t copy_stream = nullptr;
+    hipEvent_t ev_chunk[8] = {};
     hipStream_t state_stream = nullptr;
     bool state_pending = false;
     bool captured = false;                // a render was captured into a hipGraph
@@ -457,6 +461,7 @@ struct rt_ctx {
     double opt_lb_scale = 0.0;
     double opt_dcov_near = 0.0;
     double opt_cb_inline_mb = 128.0;
+    double opt_host_chunk_mb = 8.0;
     std::vector<double> far_ladder;       // big lists' far light buffers
     double upload_parts_ms[4] = {0, 0, 0, 0};  // copy+records, prepasses, light buffer, total
     int n_surf = 0, n_lights = 0;
@@ -504,6 +509,8 @@ RT_EXPORT int rt_create(int32_t dev, rt_ctx** out)
     HIP_TRY(c, hipEventCreate(&c->ev1));
     HIP_TRY(c, hipEventCreateWithFlags(&c->ev_fence, hipEventDisableTiming));
     HIP_TRY(c, hipEventCreateWithFlags(&c->ev_state, hipEventDisableTiming));
+    HIP_TRY(c, hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+    for (hipEvent_t& e : c->ev_chunk) HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIP_TRY(c, hipEventCreate(&c->ev_cb0));
     HIP_TRY(c, hipEventCreate(&c->ev_cb1));
     HIP_TRY(c, hipHostMalloc((void**)&c->h_word, 2 * sizeof(unsigned long long), hipHostMallocDefault));
@@ -563,6 +570,7 @@ static void note_async(rt_ctx* c, hipStream_t s)
 static int sync_all(rt_ctx* c)
 {
     HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (c->copy_stream) HIP_TRY(c, hipStreamSynchronize(c->copy_stream));
     for (hipStream_t s : c->async_streams) HIP_TRY(c, hipStreamSynchronize(s));
     c->async_streams.clear();
     c->state_pending = false;
@@ -613,6 +621,10 @@ RT_EXPORT int rt_set_option(rt_ctx* c, int32_t opt, double v)
         if (v < 0) return RT_E_ARG;
         c->opt_cb_inline_mb = v;
         return RT_OK;
+    case RT_OPT_HOST_CHUNK_MB:
+        if (v < 0) return RT_E_ARG;
+        c->opt_host_chunk_mb = v;
+        return RT_OK;
     default: return RT_E_ARG;
     }
 }
@@ -627,6 +639,7 @@ RT_EXPORT int rt_get_option(rt_ctx* c, int32_t opt, double* v)
     case RT_OPT_LB_SCALE: *v = c->opt_lb_scale; return RT_OK;
     case RT_OPT_DCOV_NEAR: *v = c->opt_dcov_near; return RT_OK;
     case RT_OPT_CB_INLINE_MAX_MB: *v = c->opt_cb_inline_mb; return RT_OK;
+    case RT_OPT_HOST_CHUNK_MB: *v = c->opt_host_chunk_mb; return RT_OK;
     default: return RT_E_ARG;
     }
 }
@@ -713,6 +726,9 @@ RT_EXPORT void rt_destroy(rt_ctx* c)
     if (c->ev1) hipEventDestroy(c->ev1);
     if (c->ev_fence) hipEventDestroy(c->ev_fence);
     if (c->ev_state) hipEventDestroy(c->ev_state);
+    for (hipEvent_t e : c->ev_chunk)
+        if (e) hipEventDestroy(e);
+    if (c->copy_stream) hipStreamDestroy(c->copy_stream);
     if (c->ev_cb0) hipEventDestroy(c->ev_cb0);
     if (c->ev_cb1) hipEventDestroy(c->ev_cb1);
     if (c->h_word) hipHostFree(c->h_word);
@@ -1687,8 +1703,13 @@ static int prepare_state(rt_ctx* c, const rt_frame* f, hipStream_t st, bool sync
 
 // sync_path: rt_render / rt_render_float on c->stream (may build the camera
 // buffer); else rt_render_async on the caller's stream (never builds it).
+// host_out (synchronous renders into host memory): the output is copied
+// there — for a big slab in up to 8 row chunks (multiples of 16 rows, one
+// per RT_OPT_HOST_CHUNK_MB of output), chunk i's copy on c->copy_stream
+// overlapping chunk i + 1's kernel (the same pixels: every pixel is independent, and the chunks keep
+// the unchunked launch's 8-row wave rows).
 static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_dev, hipStream_t st, bool timed,
-                  bool sync_path)
+                  bool sync_path, void* host_out = nullptr)
 {
     if (!c || !f) return RT_E_ARG;
     if (!c->uploaded) {
@@ -1729,11 +1750,52 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
     c->last.light_batch = lb;
     if (rows == 0) return RT_OK;
     if (f->flags & RT_FLAG_STATS) HIP_TRY(c, hipMemsetAsync(c->d_stats, 0, kStatSlots * sizeof(StatsDev), st));
-    dim3 grid((f->width + 15) / 16, (rows + 15) / 16);
     if (timed) HIP_TRY(c, hipEventRecord(c->ev0, st));
     StatsDev* stats = c->d_stats;
-    void* args[] = {&S, &F, &rgba_dev, &rgb_dev, &stats};
-    HIP_TRY(c, hipLaunchKernel((const void*)k, grid, dim3(256), args, 0, st));
+    const size_t px_bytes = rgba_dev ? 4 : 12;
+    // a chunk per RT_OPT_HOST_CHUNK_MB (8 MiB; each copy has a fixed cost of
+    // tens of us: a 1080p RGBA8 frame is one copy, 4K four chunks -10%,
+    // 7680 x 4320 eight chunks -30%, tools/host_chunks.py)
+    const size_t out_bytes = (size_t)rows * f->width * px_bytes;
+    const double chunk = c->opt_host_chunk_mb * 1048576.0;
+    const int nch = (host_out && f->band_rows == 0 && chunk > 0)
+                        ? (int)std::min(8.0, std::floor((double)out_bytes / chunk))
+                        : 1;
+    if (nch <= 1) {
+        dim3 grid((f->width + 15) / 16, (rows + 15) / 16);
+        void* args[] = {&S, &F, &rgba_dev, &rgb_dev, &stats};
+        HIP_TRY(c, hipLaunchKernel((const void*)k, grid, dim3(256), args, 0, st));
+        if (host_out)
+            HIP_TRY(c, hipMemcpyAsync(host_out, rgba_dev ? (void*)rgba_dev : (void*)rgb_dev,
+                                      (size_t)rows * f->width * px_bytes, hipMemcpyDeviceToHost, st));
+    } else {
+        // every chunk's kernel first, then the copies (a copy into pageable
+        // memory blocks the host; the kernels behind it keep running)
+        const int step = ((rows + nch - 1) / nch + 15) / 16 * 16;
+        int n = 0;
+        for (int r0 = 0; r0 < rows; r0 += step, ++n) {
+            const int r1 = std::min(rows, r0 + step);
+            FrameDev Fc = F;
+            Fc.row_begin = f->row_begin + r0;
+            Fc.row_end = f->row_begin + r1;
+            unsigned* oa = rgba_dev ? rgba_dev + (size_t)r0 * f->width : nullptr;
+            float* ob = rgb_dev ? rgb_dev + (size_t)r0 * f->width * 3 : nullptr;
+            dim3 grid((f->width + 15) / 16, (r1 - r0 + 15) / 16);
+            void* args[] = {&S, &Fc, &oa, &ob, &stats};
+            HIP_TRY(c, hipLaunchKernel((const void*)k, grid, dim3(256), args, 0, st));
+            HIP_TRY(c, hipEventRecord(c->ev_chunk[n], st));
+        }
+        if (timed) HIP_TRY(c, hipEventRecord(c->ev1, st));
+        const char* src = (const char*)(rgba_dev ? (void*)rgba_dev : (void*)rgb_dev);
+        for (int i = 0; i < n; ++i) {
+            const int r0 = i * step, r1 = std::min(rows, r0 + step);
+            const size_t off = (size_t)r0 * f->width * px_bytes;
+            HIP_TRY(c, hipStreamWaitEvent(c->copy_stream, c->ev_chunk[i], 0));
+            HIP_TRY(c, hipMemcpyAsync((char*)host_out + off, src + off, (size_t)(r1 - r0) * f->width * px_bytes,
+                                      hipMemcpyDeviceToHost, c->copy_stream));
+        }
+        timed = false;  // ev1 already recorded after the last kernel
+    }
     if (timed) HIP_TRY(c, hipEventRecord(c->ev1, st));
     if (capturing)
         c->captured = true;
@@ -1745,6 +1807,7 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
 static int finish_sync(rt_ctx* c, const rt_frame* f, hipStream_t st, bool timed)
 {
     HIP_TRY(c, hipStreamSynchronize(st));
+    HIP_TRY(c, hipStreamSynchronize(c->copy_stream));
     // c->stream waited for every async render enqueued before this call
     // (fence_async), so none is in flight any more
     c->async_streams.clear();
@@ -1819,9 +1882,8 @@ static int render_sync(rt_ctx* c, const rt_frame* f, void* out, bool as_float)
         target = c->d_scratch;
     }
     int rc = launch(c, f, as_float ? nullptr : (unsigned*)target, as_float ? (float*)target : nullptr, c->stream, true,
-                    true);
+                    true, (!dev && bytes) ? out : nullptr);
     if (rc) return rc;
-    if (!dev && bytes) HIP_TRY(c, hipMemcpyAsync(out, target, bytes, hipMemcpyDeviceToHost, c->stream));
     return finish_sync(c, f, c->stream, true);
 }
 

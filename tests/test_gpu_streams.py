@@ -11,6 +11,9 @@ every output, bit for bit, with a cold context that renders each camera
 alone (the reference's bits are pinned for those by test_gpu_parity.py)."""
 from __future__ import annotations
 
+import contextlib
+import gc
+
 import numpy as np
 import pytest
 
@@ -19,6 +22,20 @@ from conftest import bits_equal, scene
 
 pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
+
+
+@contextlib.contextmanager
+def capture(g):
+    """torch.cuda.graph without the garbage collector: a collection during
+    the capture could finalize an unrelated context, whose rt_destroy
+    synchronises streams — illegal while a stream is capturing."""
+    gc.collect()
+    gc.disable()
+    try:
+        with torch.cuda.graph(g):
+            yield
+    finally:
+        gc.enable()
 
 
 def _cameras(s, moves):
@@ -140,7 +157,7 @@ def test_graph_capture_and_replay():
     ctx.render_float(cams[0])  # prepares camera 0
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    with capture(g):
         ctx.render_async(cams[0], 0, out.data_ptr(), torch.cuda.current_stream().cuda_stream)
     for _ in range(3):
         out.zero_()
@@ -149,7 +166,7 @@ def test_graph_capture_and_replay():
         assert bits_equal(out.cpu().numpy(), want[0])
     # an unprepared camera cannot be captured
     g2 = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g2):
+    with capture(g2):
         with pytest.raises(rt_amd.RtError) as e:
             ctx.render_async(cams[1], 0, out.data_ptr(), torch.cuda.current_stream().cuda_stream)
     assert e.value.code == -4
@@ -223,7 +240,7 @@ def test_sequence_graph_replay_is_self_contained():
     tmp = torch.zeros((len(other), h, w, 4), dtype=torch.uint8, device="cuda")
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    with capture(g):
         ctx.render_sequence_async(frames, out.data_ptr(), h * w * 4, 0, 0, torch.cuda.current_stream().cuda_stream)
     for rep in range(3):
         out.zero_()
@@ -254,14 +271,14 @@ def test_capture_after_async_prepass_on_another_stream():
     out = torch.zeros((h, w, 3), dtype=torch.float32, device="cuda")
     ctx.render_async(f, 0, out.data_ptr(), s1.cuda_stream)  # prepass on s1
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    with capture(g):
         with pytest.raises(rt_amd.RtError) as e:
             ctx.render_async(f, 0, out.data_ptr(), torch.cuda.current_stream().cuda_stream)
     assert e.value.code == -4
     ctx.sync()
     torch.cuda.synchronize()
     g2 = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g2):
+    with capture(g2):
         ctx.render_async(f, 0, out.data_ptr(), torch.cuda.current_stream().cuda_stream)
     out.zero_()
     g2.replay()
