@@ -355,6 +355,9 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="N>1 collective backend: nccl (= RCCL over xGMI, the benchmark) or gloo (the "
                          "gather staged through host memory; lets several ranks share one GPU for tests)")
+    ap.add_argument("--gather-batch", type=int, default=4,
+                    help="N>1: frames per gather collective (RCCL's fixed cost per call is comparable to a 1/N "
+                         "slab of a 1080p frame; 1 = one gather per frame)")
     ap.add_argument("--frame-sha", action="store_true",
                     help="rank 0 adds the SHA-256 of the last assembled RGBA8 frame (bottom row first)")
     args = ap.parse_args()
@@ -448,7 +451,7 @@ def main():
     if band:
         frame.band_rows, frame.band_count, frame.band_index = band, world, rank
         _, rows = band_layout(H, world, band)
-    gather = RootGather(dist, H, W, "cuda", band_rows=band) if world > 1 else None
+    gather = RootGather(dist, H, W, "cuda", band_rows=band, batch=args.gather_batch) if world > 1 else None
     single = torch.zeros((rows, W, 4), dtype=torch.uint8, device="cuda")
 
     # one counted render (atomics) for the algorithmic work of this rank's slab
@@ -571,7 +574,8 @@ def main():
             "config": {"workload": f"{name} {W}x{H} max_bounces={depth}", "width": W, "height": H,
                        "max_bounces": depth, "surfaces": int(types.shape[0]),
                        "parallelism": (f"row-band16 x{world}" if band else f"row-slab x{world}") +
-                                      ((" + RCCL gather to rank 0 (double-buffered)" if args.dist_backend == "nccl"
+                                      ((f" + RCCL gather to rank 0 (double-buffered, {args.gather_batch} frame(s) "
+                                        "per collective)" if args.dist_backend == "nccl"
                                         else " + gloo gather to rank 0 through host memory") if world > 1 else ""),
                        "slab_imbalance": round(imbalance, 3) if imbalance is not None else None},
             "total_rays_per_s_M": round((tot_primary + tot_bounce + tot_shadow) * args.steps / elapsed / 1e6, 3),

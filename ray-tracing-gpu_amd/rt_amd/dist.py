@@ -6,16 +6,18 @@ into contiguous row slabs with no exchange until the very end, where the
 slabs meet in ONE gather over xGMI:
 
 * ``RootGather`` — the frame is assembled on rank 0 (the display / writer):
-  rank 0 renders its slab straight into the frame buffer and receives every
-  other slab in one ``dist.gather`` per frame (RCCL has no ncclGather;
-  torch's NCCL backend issues it as one group of point-to-point sends and
-  receives, so each peer uses its own direct xGMI link to the root).  Frames
-  are double-buffered, so the gather of frame k runs on RCCL's stream while
-  frame k+1 renders on the compute stream.
+  rank 0 renders its slab straight into the receive buffer and receives
+  every other slab in one ``dist.gather`` per batch of frames (RCCL has no
+  ncclGather; torch's NCCL backend issues it as one group of point-to-point
+  sends and receives, so each peer uses its own direct xGMI link to the
+  root).  Batches are double-buffered, so the gather of batch j runs on
+  RCCL's stream while batch j+1 renders on the compute stream.
 * ``gather_frame`` — the all-gather form (every rank gets the frame).
 
-Slabs are equal-height (the last one padded) so a frame is one contiguous
-buffer of ``world * rows`` rows in row order — no permutation pass.
+Slabs are equal-height (the last one padded) so with one frame per gather
+the receive buffer is the frame (``world * rows`` rows in row order, no
+permutation pass); a batch of K frames, or cyclic bands, costs rank 0 one
+strided device copy per batch.
 
 With the gloo backend (CPU collectives: tests, and several ranks sharing one
 GPU, which RCCL refuses) the same gather is staged through host tensors:
@@ -68,25 +70,33 @@ def gather_frame(slab, full, dist, group=None):
 
 
 class RootGather:
-    """Double-buffered gather of row slabs to rank 0.
+    """Double-buffered gather of row slabs to rank 0, `batch` frames per
+    collective.
 
     Per frame k: ``out = g.target(k)`` is where this rank renders its slab
-    (on rank 0 a view into frame buffer k % depth); ``g.submit(k)`` posts the
-    sends/receives asynchronously; ``g.frame(k)`` (rank 0) is the assembled
-    frame once ``g.wait(k)`` (or ``g.finish()``) has run.
+    (on rank 0 a view into the gather's own receive buffer);
+    ``g.submit(k)`` posts the gather once a batch of `batch` frames is
+    rendered (one collective for all of them: RCCL's fixed cost per call is
+    comparable to a 1/n slab of a 1080p frame, so batching amortises it —
+    ``batch=1`` is one gather per frame); ``g.finish()`` posts a partial
+    last batch and waits for everything; ``g.frame(k)`` (rank 0) is the
+    assembled frame k of the last ``depth * batch`` frames.
     """
 
     def __init__(self, dist, height: int, width: int, device, depth: int = 2, dtype=None, channels: int = 4,
-                 band_rows: int = 0):
+                 band_rows: int = 0, batch: int = 1):
         import torch
 
+        if batch < 1:
+            raise ValueError("batch >= 1")
         self.dist = dist
         self.world = dist.get_world_size()
         self.rank = dist.get_rank()
         self.H, self.W, self.C = height, width, channels
+        self.batch = batch
         # band_rows > 0: each rank renders cyclic row bands (rt_frame.band_rows)
-        # for load balance; rank 0 gathers the band sets into a staging buffer
-        # and un-permutes them into the frame with one strided copy.
+        # for load balance; rank 0 un-permutes the gathered band sets into
+        # frames with one strided copy per batch.
         self.band_rows = band_rows
         if band_rows:
             self.q, self.rows = band_layout(height, self.world, band_rows)
@@ -94,71 +104,94 @@ class RootGather:
             _, _, self.rows = slab_rows(height, self.world, self.rank)
         self.depth = depth
         dtype = dtype or torch.uint8
-        shape_full = (self.world * self.rows, width, channels)
-        shape_slab = (self.rows, width, channels)
+        K, R, n = batch, self.rows, self.world
         # gloo moves host tensors only: stage the device slabs through them
         self.host = str(device) != "cpu" and dist.get_backend() == "gloo"
-        if self.host:
-            self.h_slabs = [torch.zeros(shape_slab, dtype=dtype) for _ in range(depth)]
-            self.h_full = ([torch.zeros(shape_full, dtype=dtype) for _ in range(depth)] if self.rank == 0 else [])
-            self.h_views = ([[f[r * self.rows:(r + 1) * self.rows] for r in range(self.world)] for f in self.h_full]
-                            if self.rank == 0 else [])
-        self.staging = []
         if self.rank == 0:
-            self.frames = [torch.zeros(shape_full, dtype=dtype, device=device) for _ in range(depth)]
-            if band_rows:
-                self.staging = [torch.zeros(shape_full, dtype=dtype, device=device) for _ in range(depth)]
-            src = self.staging if band_rows else self.frames
-            self.slabs = [f[: self.rows] for f in src]
-            # the gather's targets: row blocks in rank order (contiguous views)
-            self.views = [[f[r * self.rows:(r + 1) * self.rows] for r in range(self.world)] for f in src]
+            # receive buffers [rank][frame in batch][row], rank 0's own part
+            # rendered in place; frames [frame in batch][frame row]
+            self.recv = [torch.zeros((n, K, R, width, channels), dtype=dtype, device=device) for _ in range(depth)]
+            # one frame of row slabs per gather: the receive buffer IS the frame
+            self.alias = K == 1 and not band_rows
+            self.frames = [r.view(K, n * R, width, channels) if self.alias else
+                           torch.zeros((K, n * R, width, channels), dtype=dtype, device=device) for r in self.recv]
+            self.slabs = [r[0] for r in self.recv]
+            self.views = [[r[i] for i in range(n)] for r in self.recv]
         else:
-            self.frames = []
-            self.slabs = [torch.zeros(shape_slab, dtype=dtype, device=device) for _ in range(depth)]
-            self.views = []
+            self.recv, self.frames, self.views = [], [], []
+            self.slabs = [torch.zeros((K, R, width, channels), dtype=dtype, device=device) for _ in range(depth)]
+        if self.host:
+            self.h_slabs = [torch.zeros((K, R, width, channels), dtype=dtype) for _ in range(depth)]
+            self.h_recv = ([torch.zeros((n, K, R, width, channels), dtype=dtype) for _ in range(depth)]
+                           if self.rank == 0 else [])
+            self.h_views = [[r[i] for i in range(n)] for r in self.h_recv]
         self.pending: List[Optional[list]] = [None] * depth
+        self.posted = -1   # last batch whose gather was posted
+        self.last = -1     # last frame rendered
+
+    def _slot(self, batch_index: int) -> int:
+        return batch_index % self.depth
 
     def target(self, k: int):
         """Buffer to render frame k's slab into (waits until it is free)."""
-        self.wait(k)
-        return self.slabs[k % self.depth]
+        if k % self.batch == 0:
+            self._wait_slot(self._slot(k // self.batch))
+        self.last = max(self.last, k)
+        return self.slabs[self._slot(k // self.batch)][k % self.batch]
 
     def submit(self, k: int):
-        """Post frame k's gather: ONE collective call per frame (RCCL runs it
-        as a group of point-to-point receives on rank 0 and one send per
-        peer, each over its own direct xGMI link), so the host cost per frame
-        does not grow with the number of ranks."""
-        if self.world == 1:
+        """Post the gather of frame k's batch once its last frame is
+        rendered: ONE collective call per batch (RCCL runs it as a group of
+        point-to-point receives on rank 0 and one send per peer, each over
+        its own direct xGMI link), so the host cost per batch does not grow
+        with the number of ranks."""
+        if self.world == 1 or k % self.batch != self.batch - 1:
             return
-        d, b = self.dist, k % self.depth
-        if self.host:
-            import torch
+        self._post(k // self.batch)
 
-            self.h_slabs[b].copy_(self.slabs[b])  # waits for the render on the current stream
+    def _post(self, bi: int):
+        d, b = self.dist, self._slot(bi)
+        if self.host:
+            self.h_slabs[b].copy_(self.slabs[b])  # waits for the renders on the current stream
             views = self.h_views[b] if self.rank == 0 else None
             self.pending[b] = [d.gather(self.h_slabs[b], gather_list=views, dst=0, async_op=True)]
+        else:
+            views = self.views[b] if self.rank == 0 else None
+            self.pending[b] = [d.gather(self.slabs[b], gather_list=views, dst=0, async_op=True)]
+        self.posted = bi
+
+    def _wait_slot(self, b: int):
+        if self.pending[b] is None:
             return
-        views = self.views[b] if self.rank == 0 else None
-        self.pending[b] = [d.gather(self.slabs[b], gather_list=views, dst=0, async_op=True)]
+        for w in self.pending[b]:
+            w.wait()
+        self.pending[b] = None
+        if self.rank != 0:
+            return
+        if self.host:
+            self.recv[b].copy_(self.h_recv[b])
+        K, n, R, W, C = self.batch, self.world, self.rows, self.W, self.C
+        if self.alias:
+            return
+        if self.band_rows:
+            # recv[rank][frame][local band][row] -> frames[frame][global band = local * n + rank][row]
+            br, q = self.band_rows, self.q
+            self.frames[b].view(K, q, n, br, W, C).copy_(
+                self.recv[b].view(n, K, q, br, W, C).permute(1, 2, 0, 3, 4, 5))
+        else:
+            self.frames[b].view(K, n, R, W, C).copy_(self.recv[b].transpose(0, 1))
 
     def wait(self, k: int):
-        b = k % self.depth
-        if self.pending[b] is not None:
-            for w in self.pending[b]:
-                w.wait()
-            self.pending[b] = None
-            if self.host and self.rank == 0:
-                (self.staging if self.band_rows else self.frames)[b].copy_(self.h_full[b])
-            if self.band_rows and self.rank == 0:
-                # staging[rank][local band][row] -> frame[global band = local * world + rank][row]
-                br, W, C = self.band_rows, self.W, self.C
-                self.frames[b].view(self.q, self.world, br, W, C).copy_(
-                    self.staging[b].view(self.world, self.q, br, W, C).transpose(0, 1))
+        """Wait for the gather of frame k's batch (posted by submit/finish)."""
+        self._wait_slot(self._slot(k // self.batch))
 
     def finish(self):
+        """Post a partial last batch, then wait for every pending gather."""
+        if self.world > 1 and self.last >= 0 and self.last // self.batch > self.posted:
+            self._post(self.last // self.batch)
         for b in range(self.depth):
-            self.wait(b)
+            self._wait_slot(b)
 
     def frame(self, k: int):
         """Rank 0: the assembled frame k (H rows, bottom-up)."""
-        return self.frames[k % self.depth][: self.H]
+        return self.frames[self._slot(k // self.batch)][k % self.batch][: self.H]

@@ -45,52 +45,58 @@ def _worker(rank, world, port, path, w, h, depth, out_q):
     dist.destroy_process_group()
 
 
-def _worker_root(rank, world, port, path, w, h, depth, out_q, band_rows=0):
-    """RootGather: 3 frames through the double-buffered gather (row slabs,
-    or cyclic bands of `band_rows` rows un-permuted on rank 0)."""
+def _worker_root(rank, world, port, path, w, h, depth, out_q, band_rows=0, batch=1, nframes=3):
+    """RootGather: `nframes` frames through the double-buffered gather,
+    `batch` frames per collective (row slabs, or cyclic bands of
+    `band_rows` rows un-permuted on rank 0).  Frame k = the scene at depth
+    k % 3 (different images per frame)."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from conftest import Oracle
     from rt_amd.dist import RootGather
 
-    g = RootGather(dist, h, w, "cpu", depth=2, band_rows=band_rows)
+    g = RootGather(dist, h, w, "cpu", depth=2, band_rows=band_rows, batch=batch)
     r0, r1, rows = slab_rows(h, world, rank)
     frames = []
-    for k in range(3):
+    for k in range(nframes):
         buf = g.target(k)
         buf.zero_()
         if band_rows:
-            # frame k = the scene at depth k; this rank's bands, packed in order
+            # this rank's bands, packed in order
             for q in range(g.q):
                 a = (q * world + rank) * band_rows
                 if a < h:
                     e = min(h, a + band_rows)
-                    img = Oracle().render(path, w, h, k, (a, e, 0, w), threads=1)
+                    img = Oracle().render(path, w, h, k % 3, (a, e, 0, w), threads=1)
                     buf[q * band_rows: q * band_rows + (e - a)] = torch.from_numpy(rgba8(img))
         elif r1 > r0:
-            # frame k = the scene at depth k (different images per frame)
-            img = Oracle().render(path, w, h, k, (r0, r1, 0, w), threads=1)
+            img = Oracle().render(path, w, h, k % 3, (r0, r1, 0, w), threads=1)
             buf[: r1 - r0] = torch.from_numpy(rgba8(img))
         g.submit(k)
-        if rank == 0 and k >= 1:
+        if rank == 0 and batch == 1 and k >= 1:  # frame by frame, as the frames arrive
             g.wait(k - 1)
             frames.append(g.frame(k - 1).numpy().copy())
     g.finish()
     if rank == 0:
-        frames.append(g.frame(2).numpy().copy())
+        if batch == 1:
+            frames.append(g.frame(nframes - 1).numpy().copy())
+        else:  # the last depth * batch frames are held after finish()
+            frames = [g.frame(k).numpy().copy() for k in range(nframes)]
         out_q.put(frames)
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,h,band_rows", [(2, 30, 0), (3, 31, 0), (2, 70, 16), (3, 71, 16), (3, 50, 32)])
-def test_root_gather_pipelined(oracle, world, h, band_rows):
+@pytest.mark.parametrize("world,h,band_rows,batch,nframes", [
+    (2, 30, 0, 1, 3), (3, 31, 0, 1, 3), (2, 70, 16, 1, 3), (3, 71, 16, 1, 3), (3, 50, 32, 1, 3),
+    (2, 30, 0, 2, 4), (3, 31, 0, 3, 5), (2, 70, 16, 2, 3), (3, 71, 16, 4, 7)])
+def test_root_gather_pipelined(oracle, world, h, band_rows, batch, nframes):
     w = 36
     path = os.path.join(SCENES, "scene7.dat")
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker_root, args=(r, world, port, path, w, h, 0, q, band_rows))
+    procs = [ctx.Process(target=_worker_root, args=(r, world, port, path, w, h, 0, q, band_rows, batch, nframes))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -98,8 +104,9 @@ def test_root_gather_pipelined(oracle, world, h, band_rows):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for k in range(3):
-        assert np.array_equal(got[k], rgba8(oracle.render(path, w, h, k))), k
+    assert len(got) == nframes
+    for k in range(nframes):
+        assert np.array_equal(got[k], rgba8(oracle.render(path, w, h, k % 3))), k
 
 
 @pytest.mark.parametrize("world,h", [(2, 30), (3, 31)])
