@@ -422,6 +422,135 @@ __device__ __forceinline__ void shadow_opaque_wave(const SceneDev& S, int l0, in
     }
 }
 
+// LDS-staged per-lane walk (RT_LB_LDS build option; A/B experiment): when
+// the wave's lanes fall in a few cells, every still-active lane of one cell is
+// at the same entry of its list (each active lane consumes one entry per
+// iteration), so the wave stages the next W entries of every cell's list in
+// its own LDS window with ONE batch of coalesced loads, and the lanes read
+// their entries from LDS — one load latency per W entries instead of a
+// dependent gather per entry.  Same tests, same order per lane: the any-hit
+// result is the global walk's.  Returns false (nothing done) for more cells
+// than it stages (RT_LB_LDS_G).
+#ifndef RT_LB_LDS
+#define RT_LB_LDS 1
+#endif
+#if RT_LB_LDS
+#ifndef RT_LB_LDS_CAP
+#define RT_LB_LDS_CAP 64
+#endif
+#ifndef RT_LB_LDS_G
+#define RT_LB_LDS_G 4
+#endif
+#ifndef RT_LB_LDS_ONE  // also the one-cell walk (window of 1 << RT_LB_LDS_SH1 entries)
+#define RT_LB_LDS_ONE 0
+#endif
+#ifndef RT_LB_LDS_SH1
+#define RT_LB_LDS_SH1 4
+#endif
+constexpr int kLbLdsCap = RT_LB_LDS_CAP;  // entries per wave window
+constexpr int kLbLdsG = RT_LB_LDS_G;      // most cells a wave stages
+__device__ __forceinline__ bool lb_walk_lds(const SceneDev& S, bool use, int cell, unsigned e, unsigned end,
+                                            const Vec3 P, const Vec3 L, float dist, bool& occ, Counters& cnt)
+{
+    __shared__ float4 lds_a[4 * kLbLdsCap], lds_b[4 * kLbLdsCap];
+    __shared__ float2 lds_c[4 * kLbLdsCap];
+    unsigned long long rem = __ballot(use);
+    unsigned gp[kLbLdsG], ge[kLbLdsG];
+    unsigned long long gm[kLbLdsG];
+    int ng = 0, grp = 0;
+#pragma unroll
+    for (int i = 0; i < kLbLdsG; ++i) {
+        gp[i] = ge[i] = 0u;
+        gm[i] = 0ull;
+        if (rem) {
+            const int lead = (int)__builtin_ctzll(rem);
+            const int c = __builtin_amdgcn_readlane(cell, lead);
+            const unsigned long long m = __ballot(use & (cell == c));
+            gp[i] = (unsigned)__builtin_amdgcn_readlane((int)e, lead);
+            ge[i] = (unsigned)__builtin_amdgcn_readlane((int)end, lead);
+            gm[i] = m;
+            if (use & (cell == c)) grp = i;
+            rem &= ~m;
+            ng = i + 1;
+        }
+    }
+    if (rem) return false;
+    // window per cell: the capacity over the cell count rounded up to a power of 2
+    const int lg = ng <= 1 ? 0 : 32 - __builtin_clz((unsigned)(ng - 1));
+    const int sh = ng <= 1 ? RT_LB_LDS_SH1 : __builtin_ctz((unsigned)kLbLdsCap) - lg;
+    const unsigned wmask = (1u << sh) - 1u;
+    const int base = (int)(threadIdx.x >> 6) * kLbLdsCap;
+    const unsigned long long ex = __ballot(true);
+    const int nact = __popcll(ex);
+    const int rk = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(ex >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)ex, 0u));
+    bool have = use & (e < end);
+    unsigned k = 0;  // entries each active lane has consumed (wave-uniform)
+    for (;;) {
+        const bool act = have & !occ;
+        const unsigned long long ba = __ballot(act);
+        if (!ba) break;
+        if ((k & wmask) == 0) {  // stage entries k .. k + W - 1 of every cell with an active lane
+            unsigned gact = 0;
+#pragma unroll
+            for (int i = 0; i < kLbLdsG; ++i) gact |= (ba & gm[i]) ? (1u << i) : 0u;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            for (int s = rk; s < (ng << sh); s += nact) {
+                const int gi = s >> sh;
+                unsigned q0 = gp[0], q1 = ge[0];
+#pragma unroll
+                for (int i = 1; i < kLbLdsG; ++i) {
+                    q0 = gi == i ? gp[i] : q0;
+                    q1 = gi == i ? ge[i] : q1;
+                }
+                const unsigned q = q0 + k + ((unsigned)s & wmask);
+                if (((gact >> gi) & 1u) && q < q1) {
+                    const float4* r = S.lb_ent + kLbEnt * (size_t)q;
+                    lds_a[base + s] = r[0];
+                    lds_b[base + s] = r[1];
+                    lds_c[base + s] = lb_tail(r);
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        RT_EV(cnt, 3);
+        const int slot = base + (grp << sh) + (int)(k & wmask);
+        bool go = false;
+        float4 c0 = make_float4(0.f, 0.f, 0.f, 0.f), c1 = c0;
+        float2 c2 = make_float2(0.f, 0.f);
+        if (act) {
+            c0 = lds_a[slot];
+            if (!(c0.w < dist)) {
+                have = false;  // this and every later entry lie beyond P (dmin)
+            } else {
+                go = true;
+                c1 = lds_b[slot];
+                c2 = lds_c[slot];
+            }
+        }
+        ++k;
+        have = have & (e + k < end);
+        if (__any(go)) {
+            ++cnt.tri;
+            RT_EV(cnt, 4);
+            RT_EVN(cnt, 7, (unsigned)__popcll(__ballot(go)));
+            if (go) {
+                const Vec3 e1 = make3(c1.x, c1.y, c1.z), e2 = make3(c1.w, c2.x, c2.y);
+                const TriU u = tri_u(make3(c0.x, c0.y, c0.z), e1, e2, P, L);
+                if (__any(u.ok)) {
+                    float t;
+                    const bool ok = tri_vt(u, e1, e2, L, t);
+                    occ |= ok & (t > kEps) & (t < dist);
+                }
+            }
+        }
+    }
+    return true;
+}
+#endif
+
 // One buffer slot's walk for the lanes in `cand` (slot = a light, or
 // n_lights + the light for its far buffer): the lanes whose dist the slot
 // covers (dist <= its dcov) look their cell up, walk its list, then the
@@ -456,7 +585,12 @@ __device__ __forceinline__ bool lb_slot(const SceneDev& S, int slot, const Vec3 
         if (one_cell) RT_EV(cnt, 0);
         else RT_EV(cnt, 1);
     }
-    if (one_cell) {
+#if RT_LB_LDS && RT_LB_LDS_ONE
+    constexpr bool lds_one = (RT_LB_LDS & (PIPE ? 1 : 2)) != 0;
+#else
+    constexpr bool lds_one = false;
+#endif
+    if (one_cell && !lds_one) {
         const unsigned* o = S.lb_off + obase + cf;
         const unsigned q0 = o[0], q1 = o[1];
 #ifdef RT_ABLATE_LBCELL  // timing-only build: no cell walk
@@ -487,6 +621,10 @@ __device__ __forceinline__ bool lb_slot(const SceneDev& S, int slot, const Vec3 
         e = o[0];
         end = o[1];
     }
+#if RT_LB_LDS
+    if ((RT_LB_LDS & (PIPE ? 1 : 2)) && (!one_cell || lds_one) && bu && lb_walk_lds(S, use, cell, e, end, P, L, dist, occ, cnt))
+        end = e;  // walked: skip the global walk below
+#endif
     // The next entry's loads are issued before the current entry's exact
     // test (software pipelining of the per-lane gathers).
     float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0;
