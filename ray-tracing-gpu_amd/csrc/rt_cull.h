@@ -236,6 +236,38 @@ __device__ __forceinline__ Vec3 camera_dir(const FrameDev& F, int pxc, int pyc)
     return len > kEps ? dm * recip_w(len) : make3(0.f, 0.f, 0.f);
 }
 
+// Per-wave LDS windows (4 waves per workgroup): the light-buffer walk's
+// staged entries (rt_shade.h lb_walk_lds: kLbLdsCap entries of lds_a, lds_b,
+// lds_c per wave) and the camera-list walk's staged records (lds_a, lds_b:
+// kLbLdsCap / 2 records of 64 B per wave).  The two walks never overlap in a
+// wave.
+#ifndef RT_LB_LDS_CAP
+#define RT_LB_LDS_CAP 64
+#endif
+constexpr int kLbLdsCap = RT_LB_LDS_CAP;  // entries per wave window
+__shared__ float4 lds_a[4 * kLbLdsCap], lds_b[4 * kLbLdsCap];
+__shared__ float2 lds_c[4 * kLbLdsCap];
+
+__device__ __forceinline__ void wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Camera-list walk from LDS (RT_CB_LDS build option; bit 0 the big-list
+// kernel, bit 1 the small-list one): the wave stages the next W records of
+// its list with one load per lane (for lists of indices, the index then its
+// record: two latencies per window instead of per entry) and walks them from
+// LDS — same entries, same order, same exit.
+#ifndef RT_CB_LDS
+#define RT_CB_LDS 1
+#endif
+#ifndef RT_CB_LDS_W
+#define RT_CB_LDS_W 32
+#endif
+static_assert(2 * RT_CB_LDS_W <= RT_LB_LDS_CAP, "camera window exceeds the wave's LDS");
+
 // Closest hit for camera rays from the tile's camera-buffer list (the wave
 // is the tile: full, rows aligned).  Planes and quadrics first (their hits
 // tighten the exit); then the list in cluster order, leaving once every
@@ -265,6 +297,55 @@ __device__ __forceinline__ int closest_hit_camera_list(const SceneDev& S, int ti
         take_min(ok, t, __float_as_int(c.z), bt, bi);
     }
     const unsigned e1 = S.cb_off[tile + 1];
+#if RT_CB_LDS
+    if constexpr ((RT_CB_LDS & (INLINE ? 1 : 2)) != 0) {
+        constexpr unsigned W = RT_CB_LDS_W;
+        const int lane = (int)(threadIdx.x & 63);
+        const int base = (int)(threadIdx.x >> 6) * kLbLdsCap;
+        const bool inl = INLINE && S.cb_rec;
+        for (unsigned w0 = S.cb_off[tile]; w0 < e1; w0 += W) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            if ((unsigned)lane < W && w0 + lane < e1) {
+                float4 a, b, c, d;
+                if (inl) {
+                    const float4* r = S.cb_rec + 4 * (size_t)(w0 + lane);
+                    a = r[0];
+                    b = r[1];
+                    c = r[2];
+                    d = r[3];
+                } else {
+                    const int2 en = S.cb_ent[w0 + lane];
+                    const float4* r = S.tricam + 4 * (size_t)en.x;
+                    a = r[0];
+                    b = r[1];
+                    c = r[2];
+                    d = r[3];
+                    d.z = __int_as_float(en.y);
+                }
+                lds_a[base + 2 * lane] = a;
+                lds_a[base + 2 * lane + 1] = b;
+                lds_b[base + 2 * lane] = c;
+                lds_b[base + 2 * lane + 1] = d;
+            }
+            wave_lds_sync();
+            const unsigned n = e1 - w0 < W ? e1 - w0 : W;
+            bool stop = false;
+            for (unsigned j = 0; j < n; ++j) {
+                const float4 d = lds_b[base + 2 * j + 1];
+                if (!__any((bi < 0) | !(bt < d.z))) {
+                    stop = true;
+                    break;
+                }
+                RT_EV(cnt, 2);
+                camera_tri(lds_a[base + 2 * j], lds_a[base + 2 * j + 1], lds_b[base + 2 * j], d, D, bt, bi, cnt);
+            }
+            if (stop) break;
+        }
+        best_t = bt;
+        return bi;
+    }
+#endif
     if (INLINE && S.cb_rec) {  // records inline: one scalar load round trip per entry
         for (unsigned e = S.cb_off[tile]; e < e1; ++e) {
             const float4* r = S.cb_rec + 4 * (size_t)e;

@@ -435,9 +435,6 @@ __device__ __forceinline__ void shadow_opaque_wave(const SceneDev& S, int l0, in
 #define RT_LB_LDS 1
 #endif
 #if RT_LB_LDS
-#ifndef RT_LB_LDS_CAP
-#define RT_LB_LDS_CAP 64
-#endif
 #ifndef RT_LB_LDS_G
 #define RT_LB_LDS_G 4
 #endif
@@ -447,13 +444,16 @@ __device__ __forceinline__ void shadow_opaque_wave(const SceneDev& S, int l0, in
 #ifndef RT_LB_LDS_SH1
 #define RT_LB_LDS_SH1 4
 #endif
-constexpr int kLbLdsCap = RT_LB_LDS_CAP;  // entries per wave window
+#ifndef RT_LB_LDS_PF  // prefetch the next window into registers
+#define RT_LB_LDS_PF 0
+#endif
+#ifndef RT_LB_LDS_UBR  // v and t only where some lane's u is in [0, 1]
+#define RT_LB_LDS_UBR 1
+#endif
 constexpr int kLbLdsG = RT_LB_LDS_G;      // most cells a wave stages
 __device__ __forceinline__ bool lb_walk_lds(const SceneDev& S, bool use, int cell, unsigned e, unsigned end,
                                             const Vec3 P, const Vec3 L, float dist, bool& occ, Counters& cnt)
 {
-    __shared__ float4 lds_a[4 * kLbLdsCap], lds_b[4 * kLbLdsCap];
-    __shared__ float2 lds_c[4 * kLbLdsCap];
     unsigned long long rem = __ballot(use);
     unsigned gp[kLbLdsG], ge[kLbLdsG];
     unsigned long long gm[kLbLdsG];
@@ -475,6 +475,9 @@ __device__ __forceinline__ bool lb_walk_lds(const SceneDev& S, bool use, int cel
         }
     }
     if (rem) return false;
+#ifdef RT_ABLATE_LBMULTI  // timing-only build: no multi-cell walk
+    return true;
+#endif
     // window per cell: the capacity over the cell count rounded up to a power of 2
     const int lg = ng <= 1 ? 0 : 32 - __builtin_clz((unsigned)(ng - 1));
     const int sh = ng <= 1 ? RT_LB_LDS_SH1 : __builtin_ctz((unsigned)kLbLdsCap) - lg;
@@ -485,6 +488,15 @@ __device__ __forceinline__ bool lb_walk_lds(const SceneDev& S, bool use, int cel
     const int rk = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(ex >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)ex, 0u));
     bool have = use & (e < end);
     unsigned k = 0;  // entries each active lane has consumed (wave-uniform)
+    const int nslots = ng << sh;
+#if RT_LB_LDS_PF
+    // every slot of a window has its own lane: the next window's entries are
+    // loaded into registers while this one is walked
+    const bool pf = nslots <= nact;
+    float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa;
+    float2 pc = make_float2(0.f, 0.f);
+    bool pv = false;
+#endif
     for (;;) {
         const bool act = have & !occ;
         const unsigned long long ba = __ballot(act);
@@ -495,7 +507,16 @@ __device__ __forceinline__ bool lb_walk_lds(const SceneDev& S, bool use, int cel
             for (int i = 0; i < kLbLdsG; ++i) gact |= (ba & gm[i]) ? (1u << i) : 0u;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
-            for (int s = rk; s < (ng << sh); s += nact) {
+#if RT_LB_LDS_PF
+            if (pf && k > 0) {
+                if (pv) {
+                    lds_a[base + rk] = pa;
+                    lds_b[base + rk] = pb;
+                    lds_c[base + rk] = pc;
+                }
+            } else
+#endif
+            for (int s = rk; s < nslots; s += nact) {
                 const int gi = s >> sh;
                 unsigned q0 = gp[0], q1 = ge[0];
 #pragma unroll
@@ -511,6 +532,28 @@ __device__ __forceinline__ bool lb_walk_lds(const SceneDev& S, bool use, int cel
                     lds_c[base + s] = lb_tail(r);
                 }
             }
+#if RT_LB_LDS_PF
+            if (pf) {  // issue the next window's loads (waited for at the next boundary)
+                pv = false;
+                if (rk < nslots) {
+                    const int gi = rk >> sh;
+                    unsigned q0 = gp[0], q1 = ge[0];
+#pragma unroll
+                    for (int i = 1; i < kLbLdsG; ++i) {
+                        q0 = gi == i ? gp[i] : q0;
+                        q1 = gi == i ? ge[i] : q1;
+                    }
+                    const unsigned q = q0 + k + (wmask + 1u) + ((unsigned)rk & wmask);
+                    if (((gact >> gi) & 1u) && q < q1) {
+                        const float4* r = S.lb_ent + kLbEnt * (size_t)q;
+                        pa = r[0];
+                        pb = r[1];
+                        pc = lb_tail(r);
+                        pv = true;
+                    }
+                }
+            }
+#endif
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -539,7 +582,10 @@ __device__ __forceinline__ bool lb_walk_lds(const SceneDev& S, bool use, int cel
             if (go) {
                 const Vec3 e1 = make3(c1.x, c1.y, c1.z), e2 = make3(c1.w, c2.x, c2.y);
                 const TriU u = tri_u(make3(c0.x, c0.y, c0.z), e1, e2, P, L);
-                if (__any(u.ok)) {
+#if RT_LB_LDS_UBR
+                if (__any(u.ok))
+#endif
+                {
                     float t;
                     const bool ok = tri_vt(u, e1, e2, L, t);
                     occ |= ok & (t > kEps) & (t < dist);

@@ -16,11 +16,16 @@ from collections import defaultdict
 def main(d="gpurun_out/pmc", kernel="rt_trace_kernel"):
     out = {}
     for f in sorted(glob.glob(f"{d}/*counter_collection.csv")):
+        rows = [r for r in csv.DictReader(open(f)) if kernel in r["Kernel_Name"]]
+        # the timed launches only: the non-counting instantiation (COUNT =
+        # false) over the whole frame — not the counted launch, nor the row
+        # chunks of synchronous renders into host memory (RT_OPT_HOST_CHUNK_MB)
+        timed = [r for r in rows if "false>" in r["Kernel_Name"]] or rows
+        grid = max((int(r["Grid_Size"]) for r in timed), default=0)
         per = defaultdict(list)
-        for r in csv.DictReader(open(f)):
-            if kernel not in r["Kernel_Name"]:
-                continue
-            per[r["Counter_Name"]].append(float(r["Counter_Value"]))
+        for r in timed:
+            if int(r["Grid_Size"]) == grid:
+                per[r["Counter_Name"]].append(float(r["Counter_Value"]))
         for k, v in per.items():
             # skip the first (stats-enabled, cold) dispatch
             vals = v[1:] if len(v) > 1 else v
