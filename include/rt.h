@@ -216,8 +216,9 @@ enum {
     RT_OPT_DCOV_NEAR = 5,       /* upload: big lists' near light-buffer distance, x the
                                    light's farthest triangle; 0 = default (1.25) */
     RT_OPT_CB_INLINE_MAX_MB = 6,/* launch: camera-buffer entries carry inline camera
-                                   records while they fit this many MiB (default 128;
-                                   0 = never: the index walk) */
+                                   records while they fit this many MiB (default 0 =
+                                   never: the index walk, whose records are staged in
+                                   LDS per window; 128 was the round-1 default) */
     RT_OPT_HOST_CHUNK_MB = 7    /* launch: synchronous renders into host memory render
                                    and copy in row chunks of this many MiB of output,
                                    each copy overlapping the next chunk (default 8;

@@ -460,7 +460,7 @@ struct rt_ctx {
     bool opt_union = true;
     double opt_lb_scale = 0.0;
     double opt_dcov_near = 0.0;
-    double opt_cb_inline_mb = 128.0;
+    double opt_cb_inline_mb = 0.0;
     double opt_host_chunk_mb = 8.0;
     std::vector<double> far_ladder;       // big lists' far light buffers
     double upload_parts_ms[4] = {0, 0, 0, 0};  // copy+records, prepasses, light buffer, total

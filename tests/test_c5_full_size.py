@@ -97,8 +97,8 @@ def test_c5_full_frame_windows_bands_and_slabs(c5_golden, heightfield_path):
 @pytest.mark.gpu
 @pytest.mark.parametrize("inline_mb", [0, 128])
 def test_camera_buffer_index_and_inline_walks(golden_images, heightfield_path, inline_mb):
-    """RT_OPT_CB_INLINE_MAX_MB 0 forces the walk by index (C5's) on C3's
-    frame, 128 keeps the inline records: both give the reference's bits."""
+    """RT_OPT_CB_INLINE_MAX_MB 0 (the default) walks C3's camera buffer by
+    index, 128 puts inline records in it: both give the reference's bits."""
     s = rt_amd.Scene(heightfield_path, 1920, 1080, 1)
     ctx = rt_amd.Context(0, cb_inline_max_mb=inline_mb)
     ctx.upload(s)

@@ -184,7 +184,7 @@ def test_graph_capture_and_replay():
 def test_options_round_trip_and_validation():
     ctx = rt_amd.Context(0)
     for name, v in (("light_buffer", 2), ("camera_buffer", 0), ("union_pretest", 0), ("lb_scale", 3.5),
-                    ("dcov_near", 1.5), ("cb_inline_max_mb", 0)):
+                    ("dcov_near", 1.5), ("cb_inline_max_mb", 64)):
         ctx.set_option(name, v)
         assert ctx.get_option(name) == v
     for name, v in (("light_buffer", 3), ("lb_scale", -1), ("dcov_near", 0.5), ("cb_inline_max_mb", -2)):
