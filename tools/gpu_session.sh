@@ -25,13 +25,13 @@ for s in $STEPS; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 400 python bench.py ;;
     bench_all)
-      for c in c1 c2 c3 c4 c4s7 c4s9 c5; do run bench_$c 400 python bench.py --config $c --steps 10 --cpu-seconds 5; done ;;
+      for c in c1 c2 c3 c4 c4s7 c4s9 c5; do run bench_$c 400 python bench.py --config $c --cpu-seconds 5; done ;;
     bench_big)
       for c in ${CONFIGS:-c3 c5}; do run bench_$c 400 python bench.py --config $c --steps 10 --no-cpu-baseline; done ;;
     bench_one) run bench_${CONFIG:-c2} 400 python bench.py --config ${CONFIG:-c2} --steps 20 --no-cpu-baseline ;;
     listpmc) run list_counters 120 rocprofv3 -L ;;
     pmc)
-      B="python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-host-boundary --config ${CONFIG:-c2}"
+      B="python bench.py --steps 5 --warmup 1 --settle-ms 0 --no-cpu-baseline --no-host-boundary --config ${CONFIG:-c2}"
       run pmc_fetch_${CONFIG:-c2} 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_${CONFIG:-c2} -o fetch -- $B
       run pmc_write_${CONFIG:-c2} 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_${CONFIG:-c2} -o write -- $B
       run pmc_sq_${CONFIG:-c2} 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmc_${CONFIG:-c2} -o sq -- $B
