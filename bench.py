@@ -295,12 +295,16 @@ def frame_costs(scene, frame, W, cold):
     if L.rt_render(ctx._h, ctypes.byref(frame), pinned.data_ptr()) != 0:
         return {"error": ctx._err()}
     t2 = time.perf_counter()
-    up = _debug(L, "rt_debug_upload_info", ctx, 4)
+    up = _debug(L, "rt_debug_upload_info", ctx, 9)
     cb = _debug(L, "rt_debug_cb_info", ctx, 6)
     res = {"first_frame_ms": round((t2 - t0) * 1e3, 3), "upload_ms": round((t1 - t0) * 1e3, 3),
            "first_render_ms": round((t2 - t1) * 1e3, 3),
            "upload_parts_ms": {"records_and_copies": round(up[0], 3), "prepasses": round(up[1], 3),
-                               "light_buffer": round(up[2], 3)} if up else None,
+                               "light_buffer": round(up[2], 3),
+                               "light_buffer_phases": {"cones_to_host": round(up[4], 3), "host_prep": round(up[5], 3),
+                                                       "supercell_counts": round(up[6], 3),
+                                                       "supercell_lists_cell_counts": round(up[7], 3),
+                                                       "entries": round(up[8], 3)}} if up else None,
            "camera_buffer_build_ms": round(cb[2], 3) if cb else None, "cold": cold}
     nfr = 20 if W * rows <= 4_000_000 else 8
     frames = []

@@ -464,6 +464,7 @@ struct rt_ctx {
     double opt_host_chunk_mb = 8.0;
     std::vector<double> far_ladder;       // big lists' far light buffers
     double upload_parts_ms[4] = {0, 0, 0, 0};  // copy+records, prepasses, light buffer, total
+    double lb_parts_ms[5] = {0, 0, 0, 0, 0};    // lb_build phases (rt_debug_upload_info out[4..8])
     int n_surf = 0, n_lights = 0;
     int n_tri = 0, n_plane = 0, n_quad = 0;
     int n_tri_opaque = 0, n_plane_opaque = 0, n_quad_opaque = 0, n_translucent = 0;
@@ -828,6 +829,12 @@ static int lb_build(rt_ctx* c, int ntr, int n_opaque, const std::vector<const fl
     hipStream_t st = c->stream;
     const int nl = (int)cones.size();
     const auto t0 = std::chrono::steady_clock::now();
+    auto tp = t0;
+    auto mark = [&](int i) {
+        const auto now = std::chrono::steady_clock::now();
+        c->lb_parts_ms[i] = std::chrono::duration<double, std::milli>(now - tp).count();
+        tp = now;
+    };
     // cells of ~1/4 the median cone radius: best of 1-8 on C3 and C5; and
     // no coarser than 128 cells per face edge (small scenes: C2 -3.3%, C4
     // -2.5% against their 16-48, flat from 192 to 512).  An explicit
@@ -868,6 +875,7 @@ static int lb_build(rt_ctx* c, int ntr, int n_opaque, const std::vector<const fl
             LB_TRY(hipMemcpyAsync(h.data() + (size_t)j * ntr * 2, cones[j], (size_t)ntr * 2 * sizeof(float4),
                                   hipMemcpyDeviceToHost, st));
         LB_TRY(hipStreamSynchronize(st));
+        mark(0);
         // per slot on its own host thread (independent): cell resolution from
         // the median cone angle, the triangles in dmin order, the dcap list
         std::vector<std::vector<int>> perms((size_t)nl), dperms((size_t)nl);
@@ -919,6 +927,7 @@ static int lb_build(rt_ctx* c, int ntr, int n_opaque, const std::vector<const fl
             b.ob = ob;
             ob += b.ncell + 1;
         }
+        mark(1);
         // 2. device arrays; supercell lists (counts, scan, fill)
         const size_t np = perm_all.size() + dperm_all.size();
         LB_TRY(hipMalloc(&d_perm, std::max<size_t>(np, 1) * sizeof(int)));
@@ -949,6 +958,7 @@ static int lb_build(rt_ctx* c, int ntr, int n_opaque, const std::vector<const fl
         LB_TRY(hipMemcpyAsync(c->h_word, tot, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
         LB_TRY(hipStreamSynchronize(st));
         const unsigned long long nsl = *c->h_word;
+        mark(2);
         if (nsl > 0xFFFFFFF0ull) {
             c->err = "light buffer too large";
             goto done;
@@ -971,6 +981,7 @@ static int lb_build(rt_ctx* c, int ntr, int n_opaque, const std::vector<const fl
         LB_TRY(hipMemcpyAsync(c->h_word, tot, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
         LB_TRY(hipStreamSynchronize(st));
         const unsigned long long total = *c->h_word;
+        mark(3);
         if (total >= 0xFFFFFFF0ull / 4) {  // entry indices are 32-bit
             c->err = "light buffer too large";
             goto done;
@@ -1001,6 +1012,7 @@ static int lb_build(rt_ctx* c, int ntr, int n_opaque, const std::vector<const fl
         }
         LB_TRY(hipMemcpyAsync(c->d_lb_meta, meta.data(), meta.size() * sizeof(float4), hipMemcpyHostToDevice, st));
         LB_TRY(hipStreamSynchronize(st));  // meta (host) outlives the copy; the temporaries are freed below
+        mark(4);
         c->lb_ready = true;
         c->lb_entries = total;
     }
@@ -2116,6 +2128,9 @@ RT_EXPORT int rt_debug_upload_info(rt_ctx* c, double* out, int n)
 {
     if (!c || !out || n < 4) return RT_E_ARG;
     for (int i = 0; i < 4; ++i) out[i] = c->upload_parts_ms[i];
+    // light-buffer build phases: cone records to the host, host preparation,
+    // supercell counts + scan, supercell lists + cell counts + scan, entries
+    for (int i = 0; i < 5 && 4 + i < n; ++i) out[4 + i] = c->lb_parts_ms[i];
     return RT_OK;
 }
 
