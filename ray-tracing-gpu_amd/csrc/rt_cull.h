@@ -236,17 +236,29 @@ __device__ __forceinline__ Vec3 camera_dir(const FrameDev& F, int pxc, int pyc)
     return len > kEps ? dm * recip_w(len) : make3(0.f, 0.f, 0.f);
 }
 
-// Per-wave LDS windows (4 waves per workgroup): the light-buffer walk's
-// staged entries (rt_shade.h lb_walk_lds: kLbLdsCap entries of lds_a, lds_b,
-// lds_c per wave) and the camera-list walk's staged records (lds_a, lds_b:
+// Per-wave LDS windows (dynamic LDS, one per wave): the light-buffer walk's
+// staged entries (rt_shade.h lb_walk_lds: kLbLdsCap entries of a, b,
+// c per wave) and the camera-list walk's staged records (a, b:
 // kLbLdsCap / 2 records of 64 B per wave).  The two walks never overlap in a
 // wave.
 #ifndef RT_LB_LDS_CAP
 #define RT_LB_LDS_CAP 64
 #endif
 constexpr int kLbLdsCap = RT_LB_LDS_CAP;  // entries per wave window
-__shared__ float4 lds_a[4 * kLbLdsCap], lds_b[4 * kLbLdsCap];
-__shared__ float2 lds_c[4 * kLbLdsCap];
+// The wave's window in the launch's dynamic LDS (kLdsWaveBytes per wave of
+// the workgroup, trace_dims on the host): a[cap], b[cap] float4, c[cap] float2.
+constexpr size_t kLdsWaveBytes = (size_t)kLbLdsCap * 40;
+struct LdsWin {
+    float4* a;
+    float4* b;
+    float2* c;
+};
+__device__ __forceinline__ LdsWin lds_window()
+{
+    extern __shared__ float4 rt_lds_dyn[];
+    float4* a = rt_lds_dyn + (threadIdx.x >> 6) * (kLbLdsCap * 5 / 2);
+    return LdsWin{a, a + kLbLdsCap, reinterpret_cast<float2*>(a + 2 * kLbLdsCap)};
+}
 
 __device__ __forceinline__ void wave_lds_sync()
 {
@@ -301,7 +313,7 @@ __device__ __forceinline__ int closest_hit_camera_list(const SceneDev& S, int ti
     if constexpr ((RT_CB_LDS & (INLINE ? 1 : 2)) != 0) {
         constexpr unsigned W = RT_CB_LDS_W;
         const int lane = (int)(threadIdx.x & 63);
-        const int base = (int)(threadIdx.x >> 6) * kLbLdsCap;
+        const LdsWin win = lds_window();
         const bool inl = INLINE && S.cb_rec;
         for (unsigned w0 = S.cb_off[tile]; w0 < e1; w0 += W) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -323,22 +335,22 @@ __device__ __forceinline__ int closest_hit_camera_list(const SceneDev& S, int ti
                     d = r[3];
                     d.z = __int_as_float(en.y);
                 }
-                lds_a[base + 2 * lane] = a;
-                lds_a[base + 2 * lane + 1] = b;
-                lds_b[base + 2 * lane] = c;
-                lds_b[base + 2 * lane + 1] = d;
+                win.a[2 * lane] = a;
+                win.a[2 * lane + 1] = b;
+                win.b[2 * lane] = c;
+                win.b[2 * lane + 1] = d;
             }
             wave_lds_sync();
             const unsigned n = e1 - w0 < W ? e1 - w0 : W;
             bool stop = false;
             for (unsigned j = 0; j < n; ++j) {
-                const float4 d = lds_b[base + 2 * j + 1];
+                const float4 d = win.b[2 * j + 1];
                 if (!__any((bi < 0) | !(bt < d.z))) {
                     stop = true;
                     break;
                 }
                 RT_EV(cnt, 2);
-                camera_tri(lds_a[base + 2 * j], lds_a[base + 2 * j + 1], lds_b[base + 2 * j], d, D, bt, bi, cnt);
+                camera_tri(win.a[2 * j], win.a[2 * j + 1], win.b[2 * j], d, D, bt, bi, cnt);
             }
             if (stop) break;
         }

@@ -199,6 +199,9 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
 #ifndef RT_WAVES_PER_EU
 #define RT_WAVES_PER_EU 7
 #endif
+#ifndef RT_WG1
+#define RT_WG1 3
+#endif
 #ifndef RT_WAVES_PER_EU_BIG
 #define RT_WAVES_PER_EU_BIG 8
 #endif
@@ -212,8 +215,14 @@ template <int MAXD, int LB, int WAVE, bool COUNT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(waves_per_eu(MAXD, WAVE)))) void rt_trace_kernel(const SceneDev S, const FrameDev F, unsigned* __restrict__ rgba,
                                                        float* __restrict__ rgbf, StatsDev* __restrict__ stats)
 {
+    // One wave per workgroup (RT_WG1 3, the default): one 8 x 8 tile each, so
+    // a CU takes a new tile as soon as any wave slot frees instead of four at
+    // once (A/B against 2 x 2 tiles per workgroup: C3 -3.1%, C5 -4.5%, C4
+    // -3.7%, scene7 -3.4%, scene9 -1.4%, C2 -0.8%).  1: only the small-list
+    // camera-buffer kernel, 2: every kernel but the big-list ones, 0: none.
+    constexpr bool kWg1 = RT_WG1 == 1 ? WAVE == 13 : (RT_WG1 == 2 ? !(WAVE & 2) : RT_WG1 == 3);
     const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
+    const int wave = kWg1 ? 0 : (int)(threadIdx.x >> 6);
     // XCD-aware block order: the dispatcher deals workgroups round-robin over
     // the 8 XCDs (each with its own L2), so workgroup w runs on XCD w % 8 as
     // that XCD's (w / 8)-th; give every XCD one contiguous run of blocks in
@@ -235,8 +244,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(waves_per_e
             by = (int)(lw / gridDim.x);
         }
     }
-    const int px = bx * 16 + (wave & 1) * 8 + (lane & 7);
-    const int ly0 = by * 16 + (wave >> 1) * 8;  // the wave's first output row
+    const int tile_x = kWg1 ? bx : bx * 2 + (wave & 1);  // 8-pixel column of the wave's tile
+    const int px = tile_x * 8 + (lane & 7);
+    const int ly0 = kWg1 ? by * 8 : by * 16 + (wave >> 1) * 8;  // the wave's first output row
     const int ly = ly0 + (lane >> 3);
     // frame row of output row r: the slab, or band (r / band_rows) of this
     // rank's cyclic set (a wave's 8 rows never straddle a band: 16 | band_rows)
@@ -266,7 +276,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(waves_per_e
         // full frame (the buffer's lists hold for its lanes' clamped pixels)
         int tile = -1;
         if ((WAVE & 8) && S.cb_tiles_x > 0 && (py0 & 7) == 0) {
-            tile = (py0 >> 3) * S.cb_tiles_x + bx * 2 + (wave & 1);
+            tile = (py0 >> 3) * S.cb_tiles_x + tile_x;
             if (S.cb_flag[tile]) tile = -1;
         }
         c = radiance<MAXD, LB, WAVE>(S, F, O, D, cnt, valid, tile);
@@ -289,7 +299,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(waves_per_e
             atomicAdd(&rt_prof_ev[i], (unsigned long long)cnt.ev[i]);
             tot += cnt.pt[i];
         }
-        const int tile = (int)((blockIdx.y * 2 + (wave >> 1)) * (gridDim.x * 2) + blockIdx.x * 2 + (wave & 1));
+        const int tile = kWg1 ? (int)(blockIdx.y * gridDim.x + blockIdx.x)
+                              : (int)((blockIdx.y * 2 + (wave >> 1)) * (gridDim.x * 2) + blockIdx.x * 2 + (wave & 1));
         if (rt_prof_tiles && tile < rt_prof_ntiles) {
             unsigned* o = rt_prof_tiles + 16 * (size_t)tile;
             o[0] = (unsigned)tot;
@@ -1448,6 +1459,29 @@ static kernel_fn pick_kernel(int depth, int n_tri, int n_lights, bool lbuf, bool
     return nullptr;
 }
 
+// Launch shape of a trace kernel over `rows` output rows: 16 x 16-pixel
+// workgroups of 4 waves, or (RT_WG1) one 8 x 8 tile per workgroup.
+static void trace_dims(kernel_fn k, int width, int rows, dim3& grid, dim3& block, unsigned& lds)
+{
+    const bool big = k == (kernel_fn)&rt_trace_kernel<0, 1, 14, false> || k == (kernel_fn)&rt_trace_kernel<0, 1, 14, true> ||
+                     k == (kernel_fn)&rt_trace_kernel<0, 1, 6, false> || k == (kernel_fn)&rt_trace_kernel<0, 1, 6, true> ||
+                     k == (kernel_fn)&rt_trace_kernel<0, RT_WAVE_LB, 10, false> ||
+                     k == (kernel_fn)&rt_trace_kernel<0, RT_WAVE_LB, 10, true> ||
+                     k == (kernel_fn)&rt_trace_kernel<0, RT_WAVE_LB, 2, false> ||
+                     k == (kernel_fn)&rt_trace_kernel<0, RT_WAVE_LB, 2, true>;
+    const bool small13 = k == (kernel_fn)&rt_trace_kernel<0, 1, 13, false> ||
+                         k == (kernel_fn)&rt_trace_kernel<0, 1, 13, true>;
+    // the big-list kernels' LDS windows (RT_LB_LDS, RT_CB_LDS): one per wave
+    if ((RT_WG1 == 1 && small13) || (RT_WG1 == 2 && !big) || RT_WG1 == 3) {
+        grid = dim3((width + 7) / 8, (rows + 7) / 8);
+        block = dim3(64);
+    } else {
+        grid = dim3((width + 15) / 16, (rows + 15) / 16);
+        block = dim3(256);
+    }
+    lds = big ? (unsigned)(block.x / 64 * kLdsWaveBytes) : 0u;
+}
+
 // Output rows of a launch: the slab, or this rank's band set.
 static int frame_rows(const rt_frame* f)
 {
@@ -1774,9 +1808,11 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
                         ? (int)std::min(8.0, std::floor((double)out_bytes / chunk))
                         : 1;
     if (nch <= 1) {
-        dim3 grid((f->width + 15) / 16, (rows + 15) / 16);
+        dim3 grid, block;
+        unsigned lds = 0;
+        trace_dims(k, f->width, rows, grid, block, lds);
         void* args[] = {&S, &F, &rgba_dev, &rgb_dev, &stats};
-        HIP_TRY(c, hipLaunchKernel((const void*)k, grid, dim3(256), args, 0, st));
+        HIP_TRY(c, hipLaunchKernel((const void*)k, grid, block, args, lds, st));
         if (host_out)
             HIP_TRY(c, hipMemcpyAsync(host_out, rgba_dev ? (void*)rgba_dev : (void*)rgb_dev,
                                       (size_t)rows * f->width * px_bytes, hipMemcpyDeviceToHost, st));
@@ -1792,9 +1828,11 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
             Fc.row_end = f->row_begin + r1;
             unsigned* oa = rgba_dev ? rgba_dev + (size_t)r0 * f->width : nullptr;
             float* ob = rgb_dev ? rgb_dev + (size_t)r0 * f->width * 3 : nullptr;
-            dim3 grid((f->width + 15) / 16, (r1 - r0 + 15) / 16);
+            dim3 grid, block;
+            unsigned lds = 0;
+            trace_dims(k, f->width, r1 - r0, grid, block, lds);
             void* args[] = {&S, &Fc, &oa, &ob, &stats};
-            HIP_TRY(c, hipLaunchKernel((const void*)k, grid, dim3(256), args, 0, st));
+            HIP_TRY(c, hipLaunchKernel((const void*)k, grid, block, args, lds, st));
             HIP_TRY(c, hipEventRecord(c->ev_chunk[n], st));
         }
         if (timed) HIP_TRY(c, hipEventRecord(c->ev1, st));
@@ -1961,8 +1999,10 @@ RT_EXPORT int rt_render_sequence_async(rt_ctx* c, const rt_frame* frames, int32_
         float* rgb = rgb_dev ? (float*)((char*)rgb_dev + (size_t)i * rgb_stride) : nullptr;
         StatsDev* stats = c->d_stats;
         void* args[] = {&S, &F, &rgba, &rgb, &stats};
-        dim3 grid((f->width + 15) / 16, (rows + 15) / 16);
-        HIP_TRY(c, hipLaunchKernel((const void*)k, grid, dim3(256), args, 0, st));
+        dim3 grid, block;
+        unsigned lds = 0;
+        trace_dims(k, f->width, rows, grid, block, lds);
+        HIP_TRY(c, hipLaunchKernel((const void*)k, grid, block, args, lds, st));
     }
     if (capturing)
         c->captured = true;

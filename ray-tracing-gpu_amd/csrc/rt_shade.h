@@ -482,7 +482,7 @@ __device__ __forceinline__ bool lb_walk_lds(const SceneDev& S, bool use, int cel
     const int lg = ng <= 1 ? 0 : 32 - __builtin_clz((unsigned)(ng - 1));
     const int sh = ng <= 1 ? RT_LB_LDS_SH1 : __builtin_ctz((unsigned)kLbLdsCap) - lg;
     const unsigned wmask = (1u << sh) - 1u;
-    const int base = (int)(threadIdx.x >> 6) * kLbLdsCap;
+    const LdsWin win = lds_window();
     const unsigned long long ex = __ballot(true);
     const int nact = __popcll(ex);
     const int rk = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(ex >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)ex, 0u));
@@ -510,9 +510,9 @@ __device__ __forceinline__ bool lb_walk_lds(const SceneDev& S, bool use, int cel
 #if RT_LB_LDS_PF
             if (pf && k > 0) {
                 if (pv) {
-                    lds_a[base + rk] = pa;
-                    lds_b[base + rk] = pb;
-                    lds_c[base + rk] = pc;
+                    win.a[rk] = pa;
+                    win.b[rk] = pb;
+                    win.c[rk] = pc;
                 }
             } else
 #endif
@@ -527,9 +527,9 @@ __device__ __forceinline__ bool lb_walk_lds(const SceneDev& S, bool use, int cel
                 const unsigned q = q0 + k + ((unsigned)s & wmask);
                 if (((gact >> gi) & 1u) && q < q1) {
                     const float4* r = S.lb_ent + kLbEnt * (size_t)q;
-                    lds_a[base + s] = r[0];
-                    lds_b[base + s] = r[1];
-                    lds_c[base + s] = lb_tail(r);
+                    win.a[s] = r[0];
+                    win.b[s] = r[1];
+                    win.c[s] = lb_tail(r);
                 }
             }
 #if RT_LB_LDS_PF
@@ -559,18 +559,18 @@ __device__ __forceinline__ bool lb_walk_lds(const SceneDev& S, bool use, int cel
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
         RT_EV(cnt, 3);
-        const int slot = base + (grp << sh) + (int)(k & wmask);
+        const int slot = (grp << sh) + (int)(k & wmask);
         bool go = false;
         float4 c0 = make_float4(0.f, 0.f, 0.f, 0.f), c1 = c0;
         float2 c2 = make_float2(0.f, 0.f);
         if (act) {
-            c0 = lds_a[slot];
+            c0 = win.a[slot];
             if (!(c0.w < dist)) {
                 have = false;  // this and every later entry lie beyond P (dmin)
             } else {
                 go = true;
-                c1 = lds_b[slot];
-                c2 = lds_c[slot];
+                c1 = win.b[slot];
+                c2 = win.c[slot];
             }
         }
         ++k;
