@@ -8,12 +8,13 @@ allowance: ocml powf vs glibc powf on Phong highlights)."""
 from __future__ import annotations
 
 import hashlib
+import os
 
 import numpy as np
 import pytest
 
 import rt_amd
-from conftest import bits_equal, rgba8, scene, ulp_diff
+from conftest import REPO, bits_equal, rgba8, scene, ulp_diff
 
 pytestmark = pytest.mark.gpu
 
@@ -84,16 +85,29 @@ def test_big_frame_windows(ctx, golden_images, name, i, w, h, depth):
         check(full[r0:r1, c0:c1], golden_images[k], i)
 
 
-def test_heightfield_windows(ctx, golden_images, heightfield_path):
+@pytest.fixture(scope="module")
+def c3_column():
+    """_ref windows down the whole C3 frame (tests/golden/make_c3_column_golden.py)."""
+    return np.load(os.path.join(REPO, "tests", "golden", "c3_column.npz"))
+
+
+def _hf_windows(golden_images, c3_column):
+    out = [(k, golden_images[k]) for k in golden_images.files if k.startswith("hf_1080p_d1_win_")]
+    out += [(k, c3_column[k]) for k in c3_column.files]
+    assert len(out) > 40
+    return out
+
+
+def test_heightfield_windows(ctx, golden_images, c3_column, heightfield_path):
     full = render(ctx, heightfield_path, 1920, 1080, 1)
-    for k in [k for k in golden_images.files if k.startswith("hf_1080p_d1_win_")]:
+    for k, want in _hf_windows(golden_images, c3_column):
         r0, r1, c0, c1 = map(int, k.rsplit("_win_", 1)[1].split("_"))
-        check(full[r0:r1, c0:c1], golden_images[k], 0)
+        check(full[r0:r1, c0:c1], want, 0)
 
 
 @pytest.mark.parametrize("near,far", [(1.5, [64.0]), (1.5, [1.6]), (1.05, [1.1, 1.3, 2.0, 4.0]),
                                       (1.02, [1.05, 1.1, 1.2, 1.4, 1.8, 2.5, 4.0, 8.0]), (1.25, [])])
-def test_heightfield_far_buffer(golden_images, heightfield_path, near, far):
+def test_heightfield_far_buffer(golden_images, c3_column, heightfield_path, near, far):
     """Big lists: lanes beyond the light buffer's distance walk the light's
     far buffers level by level, lanes beyond the last the per-lane loop over
     every triangle.  The distances shrunk (RT_OPT_DCOV_NEAR, rt_set_far_ladder,
@@ -101,11 +115,9 @@ def test_heightfield_far_buffer(golden_images, heightfield_path, near, far):
     reference's bits."""
     c = rt_amd.Context(0, dcov_near=near, far_ladder=far)
     full = render(c, heightfield_path, 1920, 1080, 1)
-    keys = [k for k in golden_images.files if k.startswith("hf_1080p_d1_win_")]
-    assert keys
-    for k in keys:
+    for k, want in _hf_windows(golden_images, c3_column):
         r0, r1, c0, c1 = map(int, k.rsplit("_win_", 1)[1].split("_"))
-        check(full[r0:r1, c0:c1], golden_images[k], 0)
+        check(full[r0:r1, c0:c1], want, 0)
 
 
 def test_scene2_1080p_digest_and_counts(ctx, digests):

@@ -5,6 +5,7 @@ here is bit-exact: float32 images, prepared geometry and per-primitive hits."""
 from __future__ import annotations
 
 import hashlib
+import os
 
 import numpy as np
 import pytest
@@ -79,6 +80,17 @@ def test_oracle_heightfield_windows(oracle, golden_images, heightfield_path):
     for k in keys:
         r0, r1, c0, c1 = map(int, k.rsplit("_win_", 1)[1].split("_"))
         assert bits_equal(oracle.render(heightfield_path, 1920, 1080, 1, (r0, r1, c0, c1)), golden_images[k]), k
+
+
+def test_oracle_heightfield_column_windows(oracle, heightfield_path):
+    """The restatement against _ref down the C3 frame (make_c3_column_golden.py):
+    mesh, shadowed ground, far plane — a third of the windows, for time."""
+    with np.load(os.path.join(os.path.dirname(__file__), "golden", "c3_column.npz")) as z:
+        keys = sorted(z.files)[::3]
+        assert len(keys) >= 15
+        for k in keys:
+            r0, r1, c0, c1 = map(int, k.rsplit("_win_", 1)[1].split("_"))
+            assert bits_equal(oracle.render(heightfield_path, 1920, 1080, 1, (r0, r1, c0, c1), threads=8), z[k]), k
 
 
 def test_oracle_scene2_1080p_digest(oracle, digests):
