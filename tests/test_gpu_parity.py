@@ -105,6 +105,33 @@ def test_heightfield_windows(ctx, golden_images, c3_column, heightfield_path):
         check(full[r0:r1, c0:c1], want, 0)
 
 
+def test_heightfield_without_plane_silhouette(ctx, tmp_path):
+    """The mesh against the sky (no ground plane): waves on its silhouette
+    shade only some lanes, so the big-list kernel's LDS-staged light-buffer
+    walk runs on partial waves there.  120 _ref windows
+    (tests/golden/make_hf_sky_golden.py), 7 of them across the silhouette."""
+    from rt_amd import synth
+
+    lines = synth.heightfield_dat().split("\n")
+    i = lines.index("Plane: plane_1")
+    j = i + 1
+    while j < len(lines) and lines[j].startswith(" "):
+        j += 1
+    path = tmp_path / "hf_sky.dat"
+    path.write_text("\n".join(lines[:i] + lines[j:]))
+    full = render(ctx, str(path), 1920, 1080, 1)
+    bg = np.array([0.0, 0.0, 150 / 255.0], dtype=np.float32)
+    mixed = 0
+    with np.load(os.path.join(REPO, "tests", "golden", "hf_sky.npz")) as z:
+        for k in z.files:
+            r0, r1, c0, c1 = map(int, k.rsplit("_win_", 1)[1].split("_"))
+            want = z[k]
+            check(full[r0:r1, c0:c1], want, 0)
+            sky = int((np.abs(want.reshape(-1, 3) - bg).sum(1) < 1e-6).sum())
+            mixed += 0 < sky < want.shape[0] * want.shape[1]
+    assert mixed >= 5
+
+
 @pytest.mark.parametrize("near,far", [(1.5, [64.0]), (1.5, [1.6]), (1.05, [1.1, 1.3, 2.0, 4.0]),
                                       (1.02, [1.05, 1.1, 1.2, 1.4, 1.8, 2.5, 4.0, 8.0]), (1.25, [])])
 def test_heightfield_far_buffer(golden_images, c3_column, heightfield_path, near, far):
