@@ -170,16 +170,21 @@ int rt_render_float(rt_ctx*, const rt_frame*, float* rgb_out);
 int rt_render_async(rt_ctx*, const rt_frame*, uint8_t* rgba8_dev, float* rgb_dev, void* hip_stream);
 /* ABI 4: a camera path rendered on the device — the headless analogue of
  * the reference's GLUT display loop (Main.cpp:229-250).
- * frames[0..n) (any cameras and sizes) are enqueued on `hip_stream` one after
- * the other, frame i's RGBA8 into rgba8_dev + i * rgba8_stride bytes and/or
- * its float RGB into (char*)rgb_dev + i * rgb_stride.  Each frame prepares
- * its own camera into the context's two sequence slots (alternating; apart
- * from the state the other render calls use), so the call needs no host
- * sync and no allocation, and a sequence captured into a hipGraph replays
- * exactly whatever was rendered on the context between capture and replay.
- * Sequences of one context must not overlap (one stream, or ordered by the
- * caller).  Shadow rays use the light buffer; camera rays the per-wave
- * culling (no camera buffer).  RT_FLAG_STATS is not accepted here. */
+ * frames[0..n) (any cameras and sizes) are rendered after the work already
+ * on `hip_stream`, and the work enqueued on it afterwards runs after all of
+ * them; frame i's RGBA8 goes to rgba8_dev + i * rgba8_stride bytes and/or
+ * its float RGB to (char*)rgb_dev + i * rgb_stride.  Frame i prepares its
+ * own camera into sequence slot i % 4 (apart from the state the other
+ * render calls use) and runs on the context's internal stream i % 4, forked
+ * from and joined back into `hip_stream` by events, so up to four
+ * consecutive frames are in flight at once; the call needs no host sync and
+ * no allocation after the first, and a sequence captured into a hipGraph
+ * (the internal streams join the capture) replays exactly whatever was
+ * rendered on the context between capture and replay.  A sequence waits for
+ * the context's async work on other streams (the slots are shared); a
+ * captured one is ordered by its graph's position only.  Shadow rays use the
+ * light buffer; camera rays the per-wave culling (no camera buffer).
+ * RT_FLAG_STATS is not accepted here. */
 int rt_render_sequence_async(rt_ctx*, const rt_frame* frames, int32_t n, uint8_t* rgba8_dev, size_t rgba8_stride,
                              float* rgb_dev, size_t rgb_stride, void* hip_stream);
 /* ABI 4: make the per-camera state (camera records, and the camera buffer

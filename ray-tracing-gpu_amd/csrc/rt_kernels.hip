@@ -382,6 +382,15 @@ __global__ void rt_selftest_kernel(unsigned seed, unsigned* __restrict__ fails)
 // ===================================================================== host
 using namespace rt;
 
+// Frames of rt_render_sequence_async in flight at once (one stream and one
+// camera slot each): a frame's camera prepasses and trace kernel overlap the
+// previous frames' (measured: 1 vs 4 streams, tools/overlap_probe.py; 2
+// streams gain nothing on MI355X, 3-4 do).
+#ifndef RT_SEQ_STREAMS
+#define RT_SEQ_STREAMS 4
+#endif
+constexpr int kSeqSlots = RT_SEQ_STREAMS;
+
 struct rt_ctx {
     int device = 0;
     // CPU backend (rt_create_cpu): no HIP object is ever made for it
@@ -407,11 +416,15 @@ struct rt_ctx {
     float4* d_clu_light = nullptr;
     int n_clu = 0;
     float4* d_uni = nullptr;  // union records (small lists): camera, then one per light
-    // Camera state of rt_render_sequence_async: two slots of the per-camera
-    // records, apart from the state above, alternating frame by frame.
+    // Camera state of rt_render_sequence_async: kSeqSlots slots of the
+    // per-camera records, apart from the state above; frame i of a sequence
+    // uses slot i % kSeqSlots on internal stream i % kSeqSlots, so up to
+    // kSeqSlots consecutive frames (different cameras) are in flight at once.
     struct CamSlot {
         float4 *tricam = nullptr, *cone_cam = nullptr, *clu_cam = nullptr, *uni = nullptr;
-    } seq[2];
+    } seq[kSeqSlots];
+    hipStream_t seq_streams[kSeqSlots] = {};
+    hipEvent_t seq_fork = nullptr, seq_join[kSeqSlots] = {};
     // camera buffer (rt_cb_build): per-tile lists for the camera of cb_key
     unsigned* d_cb_off = nullptr;
     unsigned* d_cb_flag = nullptr;
@@ -741,6 +754,11 @@ RT_EXPORT void rt_destroy(rt_ctx* c)
     for (hipEvent_t e : c->ev_chunk)
         if (e) hipEventDestroy(e);
     if (c->copy_stream) hipStreamDestroy(c->copy_stream);
+    for (int j = 0; j < kSeqSlots; ++j) {
+        if (c->seq_streams[j]) hipStreamDestroy(c->seq_streams[j]);
+        if (c->seq_join[j]) hipEventDestroy(c->seq_join[j]);
+    }
+    if (c->seq_fork) hipEventDestroy(c->seq_fork);
     if (c->ev_cb0) hipEventDestroy(c->ev_cb0);
     if (c->ev_cb1) hipEventDestroy(c->ev_cb1);
     if (c->h_word) hipHostFree(c->h_word);
@@ -1978,13 +1996,32 @@ RT_EXPORT int rt_render_sequence_async(rt_ctx* c, const rt_frame* frames, int32_
     }
     const int mode = c->opt_light_buffer;
     const bool lbuf = c->lb_ready && (mode == 1 || (mode == 2 && c->n_tri > kClusterMinTriangles));
+    // The camera slots are shared by every sequence call: one on another
+    // stream still in flight must finish first (a captured sequence's
+    // ordering against work outside the graph is the caller's, as for any
+    // captured launch).
+    if (!capturing && n > 0) {
+        if (int rc = fence_async(c, st)) return rc;
+    }
+    // Fork: the internal streams start after everything already on st.
+    const int S = std::min(n, kSeqSlots);
+    if (S > 1) {
+        for (int j = 0; j < S; ++j) {
+            if (!c->seq_streams[j]) HIP_TRY(c, hipStreamCreateWithFlags(&c->seq_streams[j], hipStreamNonBlocking));
+            if (!c->seq_join[j]) HIP_TRY(c, hipEventCreateWithFlags(&c->seq_join[j], hipEventDisableTiming));
+        }
+        if (!c->seq_fork) HIP_TRY(c, hipEventCreateWithFlags(&c->seq_fork, hipEventDisableTiming));
+        HIP_TRY(c, hipEventRecord(c->seq_fork, st));
+        for (int j = 0; j < S; ++j) HIP_TRY(c, hipStreamWaitEvent(c->seq_streams[j], c->seq_fork, 0));
+    }
     for (int i = 0; i < n; ++i) {
         const rt_frame* f = frames + i;
-        const rt_ctx::CamSlot& q = c->seq[i & 1];
+        const rt_ctx::CamSlot& q = c->seq[i % kSeqSlots];
+        hipStream_t fs = S > 1 ? c->seq_streams[i % S] : st;
         const int rows = frame_rows(f);
         if (rows == 0) continue;
         if (c->n_tri > 0) {
-            if (int rc = camera_records(c, f->cam_pos, st, false, q.tricam, q.cone_cam, q.uni, q.clu_cam)) return rc;
+            if (int rc = camera_records(c, f->cam_pos, fs, false, q.tricam, q.cone_cam, q.uni, q.clu_cam)) return rc;
         }
         int cap = 0, lb = 1;
         kernel_fn k = pick_kernel<false>(reachable_depth(c, f), c->n_tri, c->n_lights, lbuf, false, cap, lb);
@@ -2002,7 +2039,14 @@ RT_EXPORT int rt_render_sequence_async(rt_ctx* c, const rt_frame* frames, int32_
         dim3 grid, block;
         unsigned lds = 0;
         trace_dims(k, f->width, rows, grid, block, lds);
-        HIP_TRY(c, hipLaunchKernel((const void*)k, grid, block, args, lds, st));
+        HIP_TRY(c, hipLaunchKernel((const void*)k, grid, block, args, lds, fs));
+    }
+    // Join: st continues after every frame.
+    if (S > 1) {
+        for (int j = 0; j < S; ++j) {
+            HIP_TRY(c, hipEventRecord(c->seq_join[j], c->seq_streams[j]));
+            HIP_TRY(c, hipStreamWaitEvent(st, c->seq_join[j], 0));
+        }
     }
     if (capturing)
         c->captured = true;

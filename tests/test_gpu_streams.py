@@ -223,6 +223,38 @@ def test_sequence_matches_cold_renders(which, w, h, depth, heightfield_path):
     assert bits_equal(ctx.render_float(frames[-1]), want[-1])
 
 
+def test_sequences_on_two_streams_share_the_slots_safely():
+    """Sequences of 7 frames (more than the 4 camera slots and internal
+    streams a sequence keeps in flight) on two caller streams, back to back
+    with no host sync: the second waits for the first's slots; every frame
+    equals a fresh context's render."""
+    w, h = 256, 192
+    s = rt_amd.Scene(scene(2), w, h, 0)
+    a = rt_amd.camera_path(s.frame, 7, yaw_deg=2.0, step=(1.5, 0.0, -2.0))
+    b = rt_amd.camera_path(s.frame, 7, yaw_deg=-2.5, step=(-3.0, 0.5, 1.0))
+    cold = rt_amd.Context(0)
+    cold.upload(s)
+    want_a = [cold.render(f) for f in a]
+    want_b = [cold.render(f) for f in b]
+    ctx = rt_amd.Context(0)
+    ctx.upload(s)
+    oa = torch.zeros((7, h, w, 4), dtype=torch.uint8, device="cuda")
+    ob = torch.zeros((7, h, w, 4), dtype=torch.uint8, device="cuda")
+    oc = torch.zeros((7, h, w, 4), dtype=torch.uint8, device="cuda")
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    for rep in range(3):
+        ctx.render_sequence_async(a, oa.data_ptr(), h * w * 4, 0, 0, s1.cuda_stream)
+        ctx.render_sequence_async(b, ob.data_ptr(), h * w * 4, 0, 0, s2.cuda_stream)
+        ctx.render_sequence_async(a[::-1], oc.data_ptr(), h * w * 4, 0, 0, s1.cuda_stream)
+        torch.cuda.synchronize()
+        for i in range(7):
+            assert np.array_equal(oa[i].cpu().numpy(), want_a[i]), (rep, "a", i)
+            assert np.array_equal(ob[i].cpu().numpy(), want_b[i]), (rep, "b", i)
+            assert np.array_equal(oc[i].cpu().numpy(), want_a[6 - i]), (rep, "c", i)
+        oa.zero_(), ob.zero_(), oc.zero_()
+
+
 def test_sequence_graph_replay_is_self_contained():
     """A camera path captured into a hipGraph replays the reference's frames
     even after other cameras and sequences were rendered on the context."""
