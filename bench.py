@@ -557,10 +557,11 @@ def main():
         achieved = flops / (kernel_ms * 1e-3) / 1e12
         # Hardware counters of the same kernel on the same config, from the
         # rocprofv3 --pmc passes committed under profiles/ (tools/pmc_summary.py):
-        # HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE) and VALU
+        # L2-to-fabric bytes per launch (read requests by size + WRITE_SIZE,
+        # calibrated in tools/calib; FETCH_SIZE x2 kept beside it) and VALU
         # wave-instructions per launch; VALU busy = those x 2 cycles (wave64
         # on a SIMD32) over 1,024 SIMDs x this run's kernel time at 2.4 GHz.
-        traffic, valu_busy, pmc_src = None, None, None
+        traffic, valu_busy, pmc_src, rec = None, None, None, None
         tfile = os.path.join(REPO, "profiles", "pmc.json")
         if os.path.exists(tfile):
             with open(tfile) as f:
@@ -603,6 +604,9 @@ def main():
             "light_buffer": lbinfo,
             "camera_buffer": cbinfo,
             "hbm": {"algorithmic_bytes": int(alg_bytes), "measured_bytes": traffic,
+                    "measured_fetch_x2_bytes": (rec or {}).get("fetch_x2_bytes_per_launch") if traffic else None,
+                    "measured_note": "L2-to-fabric bytes per launch (Infinity Cache hits included): 128/64/32-B "
+                                     "read requests + WRITE_SIZE, calibrated on known-byte kernels (tools/calib)",
                     "measured_gbps": round(traffic / (kernel_ms * 1e-3) / 1e9, 1) if traffic else None,
                     "frac_of_8TBps": round(traffic / (kernel_ms * 1e-3) / 8e12, 4) if traffic else None,
                     "valu_busy": valu_busy, "source": pmc_src},

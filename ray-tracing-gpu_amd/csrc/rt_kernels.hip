@@ -193,9 +193,12 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
 
 // Occupancy floor (waves per SIMD) for the depth-0 kernels: 7 (<= 72
 // VGPRs, no spills) — C2 -4% against the unconstrained 5 waves, 6 waves
-// +1-3% and 8 waves +40% (spills) at C2/C4 — except the big-list kernels
-// with clusters, camera and light buffer (WAVE 14: C3, C5), which run best
-// at 8: -3% / -4% against 7 (tools/ab_variants.py, MI355X).
+// +1-3% and 8 waves +40% (spills) at C2/C4.  The big-list kernels (WAVE 14:
+// C3, C5) ran at 8 in round 1 (-3/-4% against 7) while spilling 9-10 VGPRs
+// (44 B/lane of scratch: 1.4 GB of writes per C5 frame, tools/calib); with
+// the LDS walks and an unpipelined global walk they fit 72 VGPRs with no
+// scratch at 7 waves, as fast as 8 waves with spills (C3 -0.4%, C5 +0.5%)
+// and 0.57 GB fewer bytes written per C5 frame.
 #ifndef RT_WAVES_PER_EU
 #define RT_WAVES_PER_EU 7
 #endif
@@ -203,7 +206,7 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
 #define RT_WG1 3
 #endif
 #ifndef RT_WAVES_PER_EU_BIG
-#define RT_WAVES_PER_EU_BIG 8
+#define RT_WAVES_PER_EU_BIG 7
 #endif
 constexpr int waves_per_eu(int maxd, int wave)
 {

@@ -672,7 +672,12 @@ __device__ __forceinline__ bool lb_slot(const SceneDev& S, int slot, const Vec3 
         end = e;  // walked: skip the global walk below
 #endif
     // The next entry's loads are issued before the current entry's exact
-    // test (software pipelining of the per-lane gathers).
+    // test (software pipelining of the per-lane gathers; PG — only waves
+    // over more than the staged cells walk here in the big-list kernel).
+#ifndef RT_LB_PIPE_GLOBAL
+#define RT_LB_PIPE_GLOBAL 0
+#endif
+    constexpr bool PG = PIPE && RT_LB_PIPE_GLOBAL;
     float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0;
     float2 r2 = make_float2(0.f, 0.f);
 #ifdef RT_ABLATE_LBCELL  // timing-only build: no cell walk
@@ -680,7 +685,7 @@ __device__ __forceinline__ bool lb_slot(const SceneDev& S, int slot, const Vec3 
 #else
     bool have = e < end;
 #endif
-    if (PIPE && have) {
+    if (PG && have) {
         const float4* r = S.lb_ent + kLbEnt * (size_t)e;
         r0 = r[0];
         r1 = r[1];
@@ -691,7 +696,7 @@ __device__ __forceinline__ bool lb_slot(const SceneDev& S, int slot, const Vec3 
         if (!__any(act)) break;
         RT_EV(cnt, 3);
         bool go = false;
-        if (!PIPE && act) {
+        if (!PG && act) {
             const float4* r = S.lb_ent + kLbEnt * (size_t)e;
             r0 = r[0];
             r1 = r[1];
@@ -706,7 +711,7 @@ __device__ __forceinline__ bool lb_slot(const SceneDev& S, int slot, const Vec3 
                 go = true;
                 ++e;
                 have = e < end;
-                if (PIPE && have) {
+                if (PG && have) {
                     const float4* r = S.lb_ent + kLbEnt * (size_t)e;
                     r0 = r[0];
                     r1 = r[1];

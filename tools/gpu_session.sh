@@ -34,6 +34,7 @@ for s in $STEPS; do
       B="python bench.py --steps 5 --warmup 1 --settle-ms 0 --no-cpu-baseline --no-host-boundary --config ${CONFIG:-c2}"
       run pmc_fetch_${CONFIG:-c2} 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_${CONFIG:-c2} -o fetch -- $B
       run pmc_write_${CONFIG:-c2} 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_${CONFIG:-c2} -o write -- $B
+      run pmc_rdreq_${CONFIG:-c2} 300 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_32B_sum --output-format csv -d gpurun_out/pmc_${CONFIG:-c2} -o rdreq -- $B
       run pmc_sq_${CONFIG:-c2} 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmc_${CONFIG:-c2} -o sq -- $B
       run pmc_sq2_${CONFIG:-c2} 300 rocprofv3 --pmc SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM SQ_INSTS_LDS SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_SALU SQ_THREAD_CYCLES_VALU SQ_INSTS_BRANCH --output-format csv -d gpurun_out/pmc_${CONFIG:-c2} -o sq2 -- $B
       python tools/pmc_summary.py gpurun_out/pmc_${CONFIG:-c2} > gpurun_out/pmc_${CONFIG:-c2}/summary.json
