@@ -217,7 +217,8 @@ enum {
     RT_OPT_CAMERA_BUFFER = 2,   /* launch: per-camera tile lists, 1 (default) / 0 */
     RT_OPT_UNION_PRETEST = 3,   /* launch: small lists' union cone pre-test, 1 (default) / 0 */
     RT_OPT_LB_SCALE = 4,        /* upload: light-buffer cells per cone radius; 0 = auto (4,
-                                   at least 128 cells per face edge); > 0 sets R alone */
+                                   at least 128 cells per face edge; 6 above 1,024
+                                   triangles); > 0 sets R alone */
     RT_OPT_DCOV_NEAR = 5,       /* upload: big lists' near light-buffer distance, x the
                                    light's farthest triangle; 0 = default (1.25) */
     RT_OPT_CB_INLINE_MAX_MB = 6,/* launch: camera-buffer entries carry inline camera

@@ -871,8 +871,12 @@ static int lb_build(rt_ctx* c, int ntr, int n_opaque, const std::vector<const fl
     // no coarser than 128 cells per face edge (small scenes: C2 -3.3%, C4
     // -2.5% against their 16-48, flat from 192 to 512).  An explicit
     // RT_OPT_LB_SCALE (A/B, the stress tests' coarse cells) sets R alone.
+    // Big lists (the ladder): 1/6 of the median cone radius since the LDS
+    // walks (round 2: C3 -4.5%, C5 -1.4% against 1/4, whose lists were
+    // twice as long; 22 M -> 47 M entries and +24 ms of build at upload; 5
+    // and 8 measured worse); small lists keep 4 (flat at C1/C2/C4).
     const bool scale_set = c->opt_lb_scale > 0.0;
-    const double scale = scale_set ? c->opt_lb_scale : 4.0;
+    const double scale = scale_set ? c->opt_lb_scale : (ntr > kClusterMinTriangles ? 6.0 : 4.0);
     const int r_min = scale_set ? kLbGroup : RT_LB_RMIN;
     // Slot j's pieces in the concatenated device arrays: its triangles in
     // dmin order (perm) and its dcap list (dperm); its supercell counts /
