@@ -884,17 +884,25 @@ static int lb_build(rt_ctx* c, int ntr, int n_opaque, const std::vector<const fl
     // from ob: the slot's lb_off) — each slot's last word stays 0 as a
     // count, so ONE exclusive scan over a whole array gives every slot its
     // absolute offsets, the last word its end.
+    // Big slots (more than kLbHyperMin triangles) first filter their
+    // triangles per block of kLbHyper x kLbHyper supercells (hob: that
+    // level's counts / offsets, like sob).
     struct Slot {
         int R = 16;
-        size_t perm0 = 0, nperm = 0, dperm0 = 0, ndperm = 0, sob = 0, ob = 0;
-        unsigned nsup = 0, ncell = 0;
+        size_t perm0 = 0, nperm = 0, dperm0 = 0, ndperm = 0, sob = 0, ob = 0, hob = 0;
+        unsigned nsup = 0, ncell = 0, nhyp = 0;
+        int Gp = 0;
     };
+    constexpr int kLbHyper = 4;
+    constexpr size_t kLbHyperMin = 4096;
     std::vector<Slot> B((size_t)nl);
     std::vector<int> perm_all, dperm_all;
-    size_t sob = 0, ob = 0;
+    size_t sob = 0, ob = 0, hob = 0;
     int* d_perm = nullptr;
     unsigned* d_soff = nullptr;
     int* d_slists = nullptr;
+    unsigned* d_hoff = nullptr;
+    int* d_hlists = nullptr;
     int rc = RT_OK;
     auto fail = [&](hipError_t e, const char* what) {
         if (rc == RT_OK) rc = hip_fail(c, e, what);
@@ -962,6 +970,12 @@ static int lb_build(rt_ctx* c, int ntr, int n_opaque, const std::vector<const fl
             sob += b.nsup + 1;
             b.ob = ob;
             ob += b.ncell + 1;
+            if (b.nperm > kLbHyperMin) {
+                b.Gp = (int)((G + kLbHyper - 1) / kLbHyper);
+                b.nhyp = 6u * (unsigned)(b.Gp * b.Gp);
+                b.hob = hob;
+                hob += b.nhyp + 1;
+            }
         }
         mark(1);
         // 2. device arrays; supercell lists (counts, scan, fill)
@@ -975,7 +989,7 @@ static int lb_build(rt_ctx* c, int ntr, int n_opaque, const std::vector<const fl
         LB_TRY(hipMalloc(&d_soff, sob * sizeof(unsigned) + sizeof(unsigned)));
         LB_TRY(hipMalloc(&c->d_lb_off, ob * sizeof(unsigned) + sizeof(unsigned)));
         {
-            const int src = ensure_scan(c, scan_scratch(std::max(sob, ob)));
+            const int src = ensure_scan(c, scan_scratch(std::max(std::max(sob, ob), hob)));
             if (src) {
                 rc = src;
                 goto done;
@@ -983,13 +997,45 @@ static int lb_build(rt_ctx* c, int ntr, int n_opaque, const std::vector<const fl
         }
         LB_TRY(hipMemsetAsync(d_soff, 0, sob * sizeof(unsigned), st));
         LB_TRY(hipMemsetAsync(c->d_lb_off, 0, ob * sizeof(unsigned), st));
+        unsigned long long* tot = nullptr;
+        // 2a. the hyper level of the big slots (counts, scan, fill)
+        if (hob > 0) {
+            LB_TRY(hipMalloc(&d_hoff, hob * sizeof(unsigned) + sizeof(unsigned)));
+            LB_TRY(hipMemsetAsync(d_hoff, 0, hob * sizeof(unsigned), st));
+            for (int j = 0; j < nl; ++j) {
+                const Slot& b = B[j];
+                if (!b.nhyp) continue;
+                hipLaunchKernelGGL(rt_lb_super, dim3(b.nhyp), dim3(256), 0, st, cones[j], ntr, d_perm + b.perm0,
+                                   (int)b.nperm, b.R, (float)dcov[j], nullptr, d_hoff + b.hob, nullptr,
+                                   kLbGroup * kLbHyper, b.Gp, 2e-3, nullptr, nullptr, 1, 1);
+                LB_TRY(hipGetLastError());
+            }
+            LB_TRY(scan_u32(d_hoff, (unsigned)hob, d_hoff, (unsigned long long*)c->d_scan, st, &tot));
+            LB_TRY(hipMemcpyAsync(c->h_word, tot, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+            LB_TRY(hipStreamSynchronize(st));
+            const unsigned long long nhl = *c->h_word;
+            if (nhl > 0xFFFFFFF0ull) {
+                c->err = "light buffer too large";
+                goto done;
+            }
+            LB_TRY(hipMalloc(&d_hlists, std::max<size_t>(nhl, 1) * sizeof(int)));
+            for (int j = 0; j < nl; ++j) {
+                const Slot& b = B[j];
+                if (!b.nhyp) continue;
+                hipLaunchKernelGGL(rt_lb_super, dim3(b.nhyp), dim3(256), 0, st, cones[j], ntr, d_perm + b.perm0,
+                                   (int)b.nperm, b.R, (float)dcov[j], d_hoff + b.hob, nullptr, d_hlists,
+                                   kLbGroup * kLbHyper, b.Gp, 2e-3, nullptr, nullptr, 1, 1);
+                LB_TRY(hipGetLastError());
+            }
+        }
+        // 2b. supercells: counts, scan, fill
         for (int j = 0; j < nl; ++j) {
             const Slot& b = B[j];
             hipLaunchKernelGGL(rt_lb_super, dim3(b.nsup), dim3(256), 0, st, cones[j], ntr, d_perm + b.perm0,
-                               (int)b.nperm, b.R, (float)dcov[j], nullptr, d_soff + b.sob, nullptr);
+                               (int)b.nperm, b.R, (float)dcov[j], nullptr, d_soff + b.sob, nullptr, kLbGroup,
+                               b.R / kLbGroup, 1e-3, b.nhyp ? d_hoff + b.hob : nullptr, d_hlists, kLbHyper, b.Gp);
             LB_TRY(hipGetLastError());
         }
-        unsigned long long* tot = nullptr;
         LB_TRY(scan_u32(d_soff, (unsigned)sob, d_soff, (unsigned long long*)c->d_scan, st, &tot));
         LB_TRY(hipMemcpyAsync(c->h_word, tot, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
         LB_TRY(hipStreamSynchronize(st));
@@ -1003,7 +1049,8 @@ static int lb_build(rt_ctx* c, int ntr, int n_opaque, const std::vector<const fl
         for (int j = 0; j < nl; ++j) {
             const Slot& b = B[j];
             hipLaunchKernelGGL(rt_lb_super, dim3(b.nsup), dim3(256), 0, st, cones[j], ntr, d_perm + b.perm0,
-                               (int)b.nperm, b.R, (float)dcov[j], d_soff + b.sob, nullptr, d_slists);
+                               (int)b.nperm, b.R, (float)dcov[j], d_soff + b.sob, nullptr, d_slists, kLbGroup,
+                               b.R / kLbGroup, 1e-3, b.nhyp ? d_hoff + b.hob : nullptr, d_hlists, kLbHyper, b.Gp);
             LB_TRY(hipGetLastError());
         }
         // 3. cell lists (counts, scan into lb_off, fill) and the dcap lists
@@ -1057,6 +1104,8 @@ done:
     if (rc != RT_OK || !c->lb_ready) (void)hipStreamSynchronize(st);
     hipFree(d_slists);
     hipFree(d_soff);
+    hipFree(d_hlists);
+    hipFree(d_hoff);
     hipFree(d_perm);
     c->lb_build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     if (rc == RT_OK && !c->lb_ready) {  // too large: run without it

@@ -121,29 +121,44 @@ __device__ __forceinline__ bool lb_keep(const WaveCone& wc, const float4 c0, con
     return cone_overlap(wc, c0, c1.w, ang) && edges_open(wc, e, ang);
 }
 
-// Build pass 1: per supercell (16 x 16 cells, cone widened by 1e-3 rad so
-// that rejecting a triangle for it implies rejecting it for each of its
-// cells), the triangles of `perm` (nearest-first) it keeps, in order
-// (block-ordered compaction).  lists == nullptr: counts only.
+// Build pass 1, per level of blocks of gs x gs cells (Gl blocks per face
+// edge; the last row/column clipped to R): the triangles a block keeps, in
+// input order (block-ordered compaction).  The block's cone is widened by
+// `widen` (1e-3 rad for supercells of 16 x 16 cells) so that rejecting a
+// triangle for it implies rejecting it for each cell it covers.  Input: the
+// slot's triangles `perm` (nearest-first), or — with a parent level
+// (poffs != nullptr; parents of pf x pf blocks, Gp per face edge, cones
+// widened more) — the parent block's list, which already lacks what the
+// parent's cone rejects (a proof for every direction inside it).  Big
+// lists run a level of 4 x 4 supercells first (round 2: the supercell
+// passes were O(supercells x triangles), 60 ms of a C3 upload).
+// lists == nullptr: counts only.
 __global__ __launch_bounds__(256) void rt_lb_super(const float4* __restrict__ cone, int n, const int* __restrict__ perm,
                                                    int np, int R, float dcov, const unsigned* __restrict__ offs,
-                                                   unsigned* __restrict__ counts, int* __restrict__ lists)
+                                                   unsigned* __restrict__ counts, int* __restrict__ lists, int gs,
+                                                   int Gl, double widen, const unsigned* __restrict__ poffs,
+                                                   const int* __restrict__ plists, int pf, int Gp)
 {
-    const int G = R / kLbGroup;
     const int s = blockIdx.x;
-    const int face = s / (G * G), rem = s % (G * G), sj = rem / G, si = rem % G;
-    const WaveCone wc = lb_cone(face, si * kLbGroup, si * kLbGroup + kLbGroup, sj * kLbGroup, sj * kLbGroup + kLbGroup,
-                                R, 1e-3);
+    const int face = s / (Gl * Gl), rem = s % (Gl * Gl), sj = rem / Gl, si = rem % Gl;
+    const WaveCone wc = lb_cone(face, si * gs, min(R, si * gs + gs), sj * gs, min(R, sj * gs + gs), R, widen);
+    const int* in = perm;
+    int nin = np;
+    if (poffs) {
+        const int p = (face * Gp + sj / pf) * Gp + si / pf;
+        in = plists + poffs[p];
+        nin = (int)(poffs[p + 1] - poffs[p]);
+    }
     __shared__ unsigned wtot[4];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     unsigned total = 0;
     const unsigned base = lists ? offs[s] : 0u;
-    for (int q0 = 0; q0 < np; q0 += 256) {
+    for (int q0 = 0; q0 < nin; q0 += 256) {
         const int q = q0 + (int)threadIdx.x;
         int k = -1;
         bool keep = false;
-        if (q < np) {
-            k = perm[q];
+        if (q < nin) {
+            k = in[q];
             keep = lb_keep(wc, cone[2 * k], cone[2 * k + 1], cone + 2 * (size_t)n + 3 * (size_t)k, dcov);
         }
         const unsigned long long b = __ballot(keep);
