@@ -1553,7 +1553,10 @@ static void trace_dims(kernel_fn k, int width, int rows, dim3& grid, dim3& block
         grid = dim3((width + 15) / 16, (rows + 15) / 16);
         block = dim3(256);
     }
-    lds = big ? (unsigned)(block.x / 64 * kLdsWaveBytes) : 0u;
+    // (the small-list kernels use them only in the A/B builds RT_LB_LDS /
+    // RT_CB_LDS bit 1)
+    const bool windows = big || ((RT_LB_LDS | RT_CB_LDS) & 2);
+    lds = windows ? (unsigned)(block.x / 64 * kLdsWaveBytes) : 0u;
 }
 
 // Output rows of a launch: the slab, or this rank's band set.
