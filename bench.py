@@ -365,6 +365,9 @@ def main():
     ap.add_argument("--gather-batch", type=int, default=4,
                     help="N>1: frames per gather collective (RCCL's fixed cost per call is comparable to a 1/N "
                          "slab of a 1080p frame; 1 = one gather per frame)")
+    ap.add_argument("--gather-channels", type=int, default=3, choices=[3, 4],
+                    help="N>1: bytes per pixel the gather carries (3: RGB, rank 0 restores the RGBA8 frame's "
+                         "constant alpha; 4: the RGBA8 pixels as rendered)")
     ap.add_argument("--frame-sha", action="store_true",
                     help="rank 0 adds the SHA-256 of the last assembled RGBA8 frame (bottom row first)")
     args = ap.parse_args()
@@ -458,7 +461,8 @@ def main():
     if band:
         frame.band_rows, frame.band_count, frame.band_index = band, world, rank
         _, rows = band_layout(H, world, band)
-    gather = RootGather(dist, H, W, "cuda", band_rows=band, batch=args.gather_batch) if world > 1 else None
+    gather = (RootGather(dist, H, W, "cuda", band_rows=band, batch=args.gather_batch,
+                         send_channels=args.gather_channels) if world > 1 else None)
     single = torch.zeros((rows, W, 4), dtype=torch.uint8, device="cuda")
 
     # one counted render (atomics) for the algorithmic work of this rank's slab
@@ -591,7 +595,7 @@ def main():
                        "max_bounces": depth, "surfaces": int(types.shape[0]),
                        "parallelism": (f"row-band16 x{world}" if band else f"row-slab x{world}") +
                                       ((f" + RCCL gather to rank 0 (double-buffered, {args.gather_batch} frame(s) "
-                                        "per collective)" if args.dist_backend == "nccl"
+                                        f"per collective, {args.gather_channels} B/px)" if args.dist_backend == "nccl"
                                         else " + gloo gather to rank 0 through host memory") if world > 1 else ""),
                        "slab_imbalance": round(imbalance, 3) if imbalance is not None else None},
             "total_rays_per_s_M": round((tot_primary + tot_bounce + tot_shadow) * args.steps / elapsed / 1e6, 3),

@@ -74,7 +74,8 @@ class RootGather:
     collective.
 
     Per frame k: ``out = g.target(k)`` is where this rank renders its slab
-    (on rank 0 a view into the gather's own receive buffer);
+    (on rank 0 a view into the gather's own receive buffer; with
+    ``send_channels=3`` a staging batch packed to RGB before the gather);
     ``g.submit(k)`` posts the gather once a batch of `batch` frames is
     rendered (one collective for all of them: RCCL's fixed cost per call is
     comparable to a 1/n slab of a 1080p frame, so batching amortises it —
@@ -84,7 +85,7 @@ class RootGather:
     """
 
     def __init__(self, dist, height: int, width: int, device, depth: int = 2, dtype=None, channels: int = 4,
-                 band_rows: int = 0, batch: int = 1):
+                 band_rows: int = 0, batch: int = 1, send_channels: int = 0, fill: int = 255):
         import torch
 
         if batch < 1:
@@ -94,6 +95,17 @@ class RootGather:
         self.rank = dist.get_rank()
         self.H, self.W, self.C = height, width, channels
         self.batch = batch
+        # send_channels < channels: only the first send_channels of every
+        # pixel travel (the RGBA8 frame's alpha is 0xFF for every pixel, so
+        # RGB carries it all — 3/4 of the bytes over the links); each rank
+        # renders into a staging batch and packs it with one strided copy
+        # per batch, rank 0 unpacks into frames whose other channels hold
+        # `fill`.
+        Ct = send_channels or channels
+        if not 0 < Ct <= channels:
+            raise ValueError("0 < send_channels <= channels")
+        self.Ct = Ct
+        self.packed = Ct < channels
         # band_rows > 0: each rank renders cyclic row bands (rt_frame.band_rows)
         # for load balance; rank 0 un-permutes the gathered band sets into
         # frames with one strided copy per batch.
@@ -109,20 +121,24 @@ class RootGather:
         self.host = str(device) != "cpu" and dist.get_backend() == "gloo"
         if self.rank == 0:
             # receive buffers [rank][frame in batch][row], rank 0's own part
-            # rendered in place; frames [frame in batch][frame row]
-            self.recv = [torch.zeros((n, K, R, width, channels), dtype=dtype, device=device) for _ in range(depth)]
+            # rendered (or packed) in place; frames [frame in batch][frame row]
+            self.recv = [torch.zeros((n, K, R, width, Ct), dtype=dtype, device=device) for _ in range(depth)]
             # one frame of row slabs per gather: the receive buffer IS the frame
-            self.alias = K == 1 and not band_rows
+            self.alias = K == 1 and not band_rows and not self.packed
             self.frames = [r.view(K, n * R, width, channels) if self.alias else
-                           torch.zeros((K, n * R, width, channels), dtype=dtype, device=device) for r in self.recv]
+                           torch.full((K, n * R, width, channels), fill, dtype=dtype, device=device)
+                           for r in self.recv]
             self.slabs = [r[0] for r in self.recv]
             self.views = [[r[i] for i in range(n)] for r in self.recv]
         else:
             self.recv, self.frames, self.views = [], [], []
-            self.slabs = [torch.zeros((K, R, width, channels), dtype=dtype, device=device) for _ in range(depth)]
+            self.slabs = [torch.zeros((K, R, width, Ct), dtype=dtype, device=device) for _ in range(depth)]
+        # render targets: the slabs themselves, or full-pixel staging batches
+        self.stage = ([torch.zeros((K, R, width, channels), dtype=dtype, device=device) for _ in range(depth)]
+                      if self.packed else self.slabs)
         if self.host:
-            self.h_slabs = [torch.zeros((K, R, width, channels), dtype=dtype) for _ in range(depth)]
-            self.h_recv = ([torch.zeros((n, K, R, width, channels), dtype=dtype) for _ in range(depth)]
+            self.h_slabs = [torch.zeros((K, R, width, Ct), dtype=dtype) for _ in range(depth)]
+            self.h_recv = ([torch.zeros((n, K, R, width, Ct), dtype=dtype) for _ in range(depth)]
                            if self.rank == 0 else [])
             self.h_views = [[r[i] for i in range(n)] for r in self.h_recv]
         self.pending: List[Optional[list]] = [None] * depth
@@ -137,7 +153,7 @@ class RootGather:
         if k % self.batch == 0:
             self._wait_slot(self._slot(k // self.batch))
         self.last = max(self.last, k)
-        return self.slabs[self._slot(k // self.batch)][k % self.batch]
+        return self.stage[self._slot(k // self.batch)][k % self.batch]
 
     def submit(self, k: int):
         """Post the gather of frame k's batch once its last frame is
@@ -151,6 +167,8 @@ class RootGather:
 
     def _post(self, bi: int):
         d, b = self.dist, self._slot(bi)
+        if self.packed:  # the batch's first Ct channels, one strided copy
+            self.slabs[b].copy_(self.stage[b][..., : self.Ct])
         if self.host:
             self.h_slabs[b].copy_(self.slabs[b])  # waits for the renders on the current stream
             views = self.h_views[b] if self.rank == 0 else None
@@ -170,16 +188,16 @@ class RootGather:
             return
         if self.host:
             self.recv[b].copy_(self.h_recv[b])
-        K, n, R, W, C = self.batch, self.world, self.rows, self.W, self.C
+        K, n, R, W, C, Ct = self.batch, self.world, self.rows, self.W, self.C, self.Ct
         if self.alias:
             return
         if self.band_rows:
             # recv[rank][frame][local band][row] -> frames[frame][global band = local * n + rank][row]
             br, q = self.band_rows, self.q
-            self.frames[b].view(K, q, n, br, W, C).copy_(
-                self.recv[b].view(n, K, q, br, W, C).permute(1, 2, 0, 3, 4, 5))
+            self.frames[b].view(K, q, n, br, W, C)[..., :Ct].copy_(
+                self.recv[b].view(n, K, q, br, W, Ct).permute(1, 2, 0, 3, 4, 5))
         else:
-            self.frames[b].view(K, n, R, W, C).copy_(self.recv[b].transpose(0, 1))
+            self.frames[b].view(K, n, R, W, C)[..., :Ct].copy_(self.recv[b].transpose(0, 1))
 
     def wait(self, k: int):
         """Wait for the gather of frame k's batch (posted by submit/finish)."""

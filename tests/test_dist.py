@@ -45,17 +45,18 @@ def _worker(rank, world, port, path, w, h, depth, out_q):
     dist.destroy_process_group()
 
 
-def _worker_root(rank, world, port, path, w, h, depth, out_q, band_rows=0, batch=1, nframes=3):
+def _worker_root(rank, world, port, path, w, h, depth, out_q, band_rows=0, batch=1, nframes=3, send_channels=0):
     """RootGather: `nframes` frames through the double-buffered gather,
     `batch` frames per collective (row slabs, or cyclic bands of
-    `band_rows` rows un-permuted on rank 0).  Frame k = the scene at depth
+    `band_rows` rows un-permuted on rank 0; send_channels 3: RGB on the
+    wire, rank 0 restoring the constant alpha).  Frame k = the scene at depth
     k % 3 (different images per frame)."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from conftest import Oracle
     from rt_amd.dist import RootGather
 
-    g = RootGather(dist, h, w, "cpu", depth=2, band_rows=band_rows, batch=batch)
+    g = RootGather(dist, h, w, "cpu", depth=2, band_rows=band_rows, batch=batch, send_channels=send_channels)
     r0, r1, rows = slab_rows(h, world, rank)
     frames = []
     for k in range(nframes):
@@ -87,16 +88,18 @@ def _worker_root(rank, world, port, path, w, h, depth, out_q, band_rows=0, batch
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,h,band_rows,batch,nframes", [
-    (2, 30, 0, 1, 3), (3, 31, 0, 1, 3), (2, 70, 16, 1, 3), (3, 71, 16, 1, 3), (3, 50, 32, 1, 3),
-    (2, 30, 0, 2, 4), (3, 31, 0, 3, 5), (2, 70, 16, 2, 3), (3, 71, 16, 4, 7)])
-def test_root_gather_pipelined(oracle, world, h, band_rows, batch, nframes):
+@pytest.mark.parametrize("world,h,band_rows,batch,nframes,send_channels", [
+    (2, 30, 0, 1, 3, 0), (3, 31, 0, 1, 3, 0), (2, 70, 16, 1, 3, 0), (3, 71, 16, 1, 3, 0), (3, 50, 32, 1, 3, 0),
+    (2, 30, 0, 2, 4, 0), (3, 31, 0, 3, 5, 0), (2, 70, 16, 2, 3, 0), (3, 71, 16, 4, 7, 0),
+    (2, 30, 0, 1, 3, 3), (3, 31, 0, 3, 5, 3), (3, 71, 16, 4, 7, 3)])
+def test_root_gather_pipelined(oracle, world, h, band_rows, batch, nframes, send_channels):
     w = 36
     path = os.path.join(SCENES, "scene7.dat")
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker_root, args=(r, world, port, path, w, h, 0, q, band_rows, batch, nframes))
+    procs = [ctx.Process(target=_worker_root,
+                         args=(r, world, port, path, w, h, 0, q, band_rows, batch, nframes, send_channels))
              for r in range(world)]
     for p in procs:
         p.start()

@@ -28,14 +28,14 @@ def _port():
         return s.getsockname()[1]
 
 
-def _bench(n, config, partition="auto", gather_batch=4):
+def _bench(n, config, partition="auto", gather_batch=4, gather_channels=3):
     args = ["bench.py", "--gpus", str(n), "--steps", "3", "--warmup", "1", "--config", config, "--frame-sha",
             "--no-cpu-baseline", "--no-host-boundary"]
     if n > 1:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(n),
                "--master-addr", "127.0.0.1", "--master-port", str(_port())] + args + [
                    "--dist-backend", "gloo", "--partition", partition,
-                   "--gather-batch", str(gather_batch)]
+                   "--gather-batch", str(gather_batch), "--gather-channels", str(gather_channels)]
     else:
         cmd = [sys.executable] + args
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2")
@@ -52,11 +52,13 @@ def one_rank():
 
 
 # 4 frames per run (1 warmup + 3 timed): gather batches of 4 (one collective),
-# 1 (one per frame) and 3 (a full batch, then a partial one posted by finish)
-@pytest.mark.parametrize("n,partition,gather_batch", [(2, "slabs", 4), (2, "bands", 4), (3, "auto", 4),
-                                                      (3, "slabs", 1), (2, "bands", 3), (3, "slabs", 3)])
-def test_scene2_ranks_match_reference_digest(one_rank, digests, n, partition, gather_batch):
-    out = _bench(n, "c2", partition, gather_batch)
+# 1 (one per frame) and 3 (a full batch, then a partial one posted by finish);
+# RGB on the wire (the default) and the RGBA8 pixels as rendered
+@pytest.mark.parametrize("n,partition,gather_batch,gather_channels", [
+    (2, "slabs", 4, 3), (2, "bands", 4, 3), (3, "auto", 4, 3), (3, "slabs", 1, 3), (2, "bands", 3, 3),
+    (3, "slabs", 3, 4), (2, "slabs", 1, 4)])
+def test_scene2_ranks_match_reference_digest(one_rank, digests, n, partition, gather_batch, gather_channels):
+    out = _bench(n, "c2", partition, gather_batch, gather_channels)
     assert out["n_gpus"] == n
     assert out["frame_rgba8_sha256"] == one_rank["c2"]["frame_rgba8_sha256"]
     # scene2 has no reflective/refractive surface: depth 3 renders the depth-0 image
