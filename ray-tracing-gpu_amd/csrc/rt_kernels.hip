@@ -846,14 +846,15 @@ static void cluster_order(std::vector<float>& tri, int n_opaque)
 // 2.3x / 8.8x slower).  Small lists (<= 1,024 triangles, no clusters, one
 // level): F = RT_DCOV_FACTOR_SMALL — far ground-plane points then stay
 // in the buffer (A/B against 4: 16 / 32 / 64 / 256 = C2 -8 / -10 / -11 /
-// +1%, C4 -8 / -8 / -6 / +5%; C1 and the bounce scenes flat).
+// +1%, C4 -8 / -8 / -6 / +5%; C1 and the bounce scenes flat; re-tuned at the
+// end of round 2: 24 against 32 C2 -2.5%, C4 -2.4%, 20 and 28 worse).
 // RT_OPT_DCOV_NEAR and rt_set_far_ladder override the big-list ladder at
 // upload (tests, A/B).
 #ifndef RT_DCOV_FACTOR
 #define RT_DCOV_FACTOR 1.25
 #endif
 #ifndef RT_DCOV_FACTOR_SMALL
-#define RT_DCOV_FACTOR_SMALL 32.0
+#define RT_DCOV_FACTOR_SMALL 24.0
 #endif
 // Slots: one buffer per entry of `cones` (a light's cone records, built for
 // the distance dcov[j]): the lights, then (big lists) their far buffers.
