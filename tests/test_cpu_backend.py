@@ -142,3 +142,18 @@ def test_cli_cpu_backend_matches_reference_digest(tmp_path, digests):
     assert hashlib.sha256(tex.tobytes()).hexdigest() == digests["scene2_1920x1080_d0_rgba8_sha256"]
     bad = subprocess.run([exe, scene(2), "--backend", "vulkan"], capture_output=True, text=True, timeout=60)
     assert bad.returncode == 1 and "[ERREUR]" in bad.stderr
+
+
+@pytest.mark.parametrize("seed", range(120))
+def test_fuzz_scenes_match_oracle(cpu, oracle, tmp_path, seed):
+    """The seeded random scenes of tests/fuzz_scenes.py (pinned against
+    oracle/_ref by test_oracle_fuzz.py), all 120 at the same sizes and
+    depths, Phong and the 1,100-1,600-triangle scenes included: the CPU backend equals the oracle bit for bit."""
+    from fuzz_scenes import fuzz_dat
+
+    big = seed % 10 == 7
+    path = tmp_path / f"fuzz{seed}.dat"
+    path.write_text(fuzz_dat(seed, seed % 3 == 2, big))
+    depth = 0 if big and seed % 20 == 7 else seed % 6
+    w, h = (64, 48) if big else (48, 36)
+    assert bits_equal(render(cpu, str(path), w, h, depth), oracle.render(str(path), w, h, depth))
