@@ -295,15 +295,19 @@ __global__ __launch_bounds__(RT_TRACE_LB) __attribute__((amdgpu_waves_per_eu(wav
                 rgbf[3 * o + 1] = c.g;
                 rgbf[3 * o + 2] = c.b;
             }
-            // Nontemporal (streaming) stores: the frame's lines leave each
-            // XCD's L2 during the kernel instead of in the release at its
-            // end (A/B, same images: C2 -1 to -2%, C4 -2%, C5 -0.5%, C1 +1%).
+            // Nontemporal (streaming) stores in the small-list kernels: the
+            // frame's lines leave each XCD's L2 during the kernel instead of
+            // in the release at its end (A/B, same images: C2 -1 to -2%, C4
+            // -2%, C1 +1%).  Not in the big-list kernels: at C5 they write
+            // each 128-B line out twice (WRITE_SIZE 134 -> 268 MB per frame:
+            // 32-B tile rows evicted before the neighbouring tiles fill the
+            // line) for -0.5%.
 #ifndef RT_NT_STORE
 #define RT_NT_STORE 1
 #endif
             if (rgba) {
                 const unsigned px8 = unorm8(c.r) | (unorm8(c.g) << 8) | (unorm8(c.b) << 16) | 0xFF000000u;
-                if constexpr (RT_NT_STORE) __builtin_nontemporal_store(px8, rgba + o);
+                if constexpr (RT_NT_STORE && !(WAVE & 2)) __builtin_nontemporal_store(px8, rgba + o);
                 else rgba[o] = px8;
             }
         }
