@@ -368,6 +368,9 @@ def main():
     ap.add_argument("--gather-channels", type=int, default=3, choices=[3, 4],
                     help="N>1: bytes per pixel the gather carries (3: RGB, rank 0 restores the RGBA8 frame's "
                          "constant alpha; 4: the RGBA8 pixels as rendered)")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="create the process group and run the gather path even with WORLD_SIZE=1 (exercises "
+                         "RCCL's init, all-reduce and gather on a 1-GPU box)")
     ap.add_argument("--frame-sha", action="store_true",
                     help="rank 0 adds the SHA-256 of the last assembled RGBA8 frame (bottom row first)")
     args = ap.parse_args()
@@ -382,7 +385,8 @@ def main():
     device = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(device)
     dist = None
-    if world > 1:
+    use_dist = world > 1 or args.force_dist
+    if use_dist:
         import torch.distributed as dist
 
         if args.dist_backend == "nccl":
@@ -435,7 +439,7 @@ def main():
     # when the slabs' render times differ by more than 10% (measured here on
     # every rank before the run; the decision is the same on all ranks).
     partition, imbalance = "slabs", None
-    if world > 1 and args.partition != "slabs":
+    if use_dist and args.partition != "slabs":
         tmp = torch.zeros((max(rows, 1), W, 4), dtype=torch.uint8, device="cuda")
         # the timed loop's kernel: one synchronous render first builds this
         # camera's camera buffer, which the async renders below then use
@@ -462,7 +466,7 @@ def main():
         frame.band_rows, frame.band_count, frame.band_index = band, world, rank
         _, rows = band_layout(H, world, band)
     gather = (RootGather(dist, H, W, "cuda", band_rows=band, batch=args.gather_batch,
-                         send_channels=args.gather_channels) if world > 1 else None)
+                         send_channels=args.gather_channels) if use_dist else None)
     single = torch.zeros((rows, W, 4), dtype=torch.uint8, device="cuda")
 
     # one counted render (atomics) for the algorithmic work of this rank's slab
@@ -515,10 +519,10 @@ def main():
     # launch duration (back-to-back, no event packets between launches, which
     # would add their own dispatch latency).  At N>1 the compute stream also
     # waits for gather buffers, so each launch gets its own event pair.
-    per_launch = world > 1
+    per_launch = use_dist
     events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in range(args.steps if per_launch else 1)]
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -531,7 +535,7 @@ def main():
     if gather:
         gather.finish()
     torch.cuda.synchronize()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     frame_sha = None
@@ -544,7 +548,17 @@ def main():
         kernel_ms = sum(a.elapsed_time(b) for a, b in events) / args.steps
     else:
         kernel_ms = events[0][0].elapsed_time(events[0][1]) / args.steps
-    if world > 1:
+    # per-frame kernel times (median beside the mean): after
+    # the timed region, K more frames with an event pair around each launch
+    frame_ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                for _ in range(args.steps)]
+    for a, b in frame_ev:
+        a.record()
+        ctx.render_async(frame, single.data_ptr(), 0, stream)
+        b.record()
+    torch.cuda.synchronize()
+    per_frame = sorted(a.elapsed_time(b) for a, b in frame_ev)
+    if use_dist:
         cdev = "cuda" if args.dist_backend == "nccl" else "cpu"
         t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -596,11 +610,17 @@ def main():
                        "parallelism": (f"row-band16 x{world}" if band else f"row-slab x{world}") +
                                       ((f" + RCCL gather to rank 0 (double-buffered, {args.gather_batch} frame(s) "
                                         f"per collective, {args.gather_channels} B/px)" if args.dist_backend == "nccl"
-                                        else " + gloo gather to rank 0 through host memory") if world > 1 else ""),
+                                        else " + gloo gather to rank 0 through host memory") if use_dist else ""),
                        "slab_imbalance": round(imbalance, 3) if imbalance is not None else None},
             "total_rays_per_s_M": round((tot_primary + tot_bounce + tot_shadow) * args.steps / elapsed / 1e6, 3),
             "rays_per_frame": {"primary": int(tot_primary), "bounce": int(tot_bounce), "shadow": int(tot_shadow)},
             "kernel_ms": round(kernel_ms, 4),
+            "frame_ms": {"median": round(per_frame[len(per_frame) // 2], 4),
+                         "mean": round(sum(per_frame) / len(per_frame), 4),
+                         "p10": round(per_frame[len(per_frame) // 10], 4),
+                         "p90": round(per_frame[(9 * len(per_frame)) // 10], 4), "frames": len(per_frame),
+                         "note": "this rank's render of K more frames after the timed region, one HIP event pair "
+                                 "around each launch (includes each launch's dispatch gap)"},
             "settle": {"frames": settle_frames, "ms": round(args.settle_ms, 1),
                        "note": "untimed renders before the warmup steps (sustained clock); then warmup, then the "
                                "timed steps"},
@@ -631,6 +651,13 @@ def main():
             fc = frame_costs(scene, frame, W, cold)
             out["first_frame_ms"] = fc.get("first_frame_ms")
             out["moving_camera_ms_per_frame"] = fc.get("moving_camera_ms_per_frame")
+            mc = fc.get("moving_camera") or {}
+            if mc.get("async_device_ms_per_frame"):
+                # the camera moved every frame, device-resident output: the
+                # per-frame cost of any use that moves the camera (value
+                # re-renders one camera whose per-camera state is built once)
+                out["moving_camera_async_ms"] = mc["async_device_ms_per_frame"]
+                out["moving_camera_async_mray_s"] = round(W * H / mc["async_device_ms_per_frame"] / 1e3, 3)
             out["frame_costs"] = fc
         if world == 1 and not args.no_cpu_baseline:
             cb = cpu_baseline(path, W, H, depth, args.cpu_seconds)
@@ -640,7 +667,7 @@ def main():
             ca["gpu_over_cpu"] = round(value / ca["value"], 1) if ca["value"] else None
             out["cpu_baseline_allcores"] = ca
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 

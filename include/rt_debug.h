@@ -1,0 +1,52 @@
+/*
+ * rt_debug.h — diagnostic exports of librt_amd.so (not part of the drop-in
+ * boundary, include/rt.h).
+ *
+ * The reference has no counterpart: these read back what the acceleration
+ * structures cost (bench.py reports them beside the headline number) and
+ * self-test the wave primitives the culling relies on.  They never change an
+ * image and no product path depends on them; the ABI version of rt.h does not
+ * cover them.  Every function returns 0 or a negative RT_E_* code (rt.h).
+ */
+#ifndef RT_AMD_RT_DEBUG_H
+#define RT_AMD_RT_DEBUG_H
+
+#include "rt.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Light buffer of the uploaded scene: out[0] built (0/1), out[1] entries,
+ * out[2] build ms; then per light j (while 3 + 3j + 2 < n): cells per face
+ * edge, uncullable-pair list length, coverage distance dcov. */
+int rt_debug_lb_info(rt_ctx*, double* out, int n);
+
+/* Camera buffer of the last build: out[0] current (0/1), out[1] entries,
+ * out[2] device ms of the build's kernels, out[3] tiles, out[4] inline
+ * records (0/1), out[5] host wall ms of the build's enqueue; out[6..8]
+ * build counters (n > 8; see DESIGN.md §3 "Camera buffer"). */
+int rt_debug_cb_info(rt_ctx*, double* out, int n);
+
+/* The last rt_upload_scene's host wall time by part (ms): out[0] records +
+ * device copies, out[1] cone / cluster prepasses, out[2] light buffer,
+ * out[3] total, out[4..8] the light-buffer build's phases. */
+int rt_debug_upload_info(rt_ctx*, double* out, int n);
+
+/* Run the wave-primitive self-test (wave min / max / sum, wave cones) over
+ * `blocks` workgroups on `device`; *failures = lanes that disagreed. */
+int rt_debug_selftest(int device, int blocks, unsigned* failures);
+
+#ifdef RT_PROF
+/* Only in a library built with -DRT_PROF (tools/prof_sections.py,
+ * tools/prof_tiles.py): per-section shader-clock totals and event counts
+ * of the last renders (read and clear), and a per-tile record buffer. */
+int rt_debug_prof(unsigned long long* out8);
+int rt_debug_prof_events(unsigned long long* out8);
+int rt_debug_prof_tiles(unsigned* dev, int ntiles);
+#endif
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RT_AMD_RT_DEBUG_H */

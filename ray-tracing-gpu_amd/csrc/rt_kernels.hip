@@ -9,8 +9,9 @@
 // Quadrique.cpp:160).  It is NOT a translation of shaders/rayTracing.glsl.
 //
 // Execution model:
-//  * one wave64 = one 8x8 pixel tile, lane l -> (l&7, l>>3); a 256-thread
-//    workgroup covers 16x16 pixels (4 tiles);
+//  * one wave64 = one 8x8 pixel tile, lane l -> (l&7, l>>3); one wave per
+//    workgroup by default (RT_WG1 3; 0 restores 256-thread workgroups of
+//    2x2 tiles);
 //  * the surface list is walked in FILE ORDER by every lane of the wave in
 //    lockstep, so the surface index, its type switch and its 64-byte record are
 //    wave-uniform: records arrive through the scalar data cache (s_load) into
@@ -38,6 +39,7 @@
 #include <vector>
 
 #include "../../include/rt.h"
+#include "../../include/rt_debug.h"
 #include "rt_cpu.hpp"
 #include "rt_scan.h"
 #include "rt_shade.h"
@@ -666,6 +668,8 @@ RT_EXPORT int rt_set_option(rt_ctx* c, int32_t opt, double v)
         return RT_OK;
     case RT_OPT_CB_INLINE_MAX_MB:
         if (v < 0) return RT_E_ARG;
+        // the layout is chosen at a camera-buffer build: rebuild at the next render
+        if (v != c->opt_cb_inline_mb) c->cb_valid = false;
         c->opt_cb_inline_mb = v;
         return RT_OK;
     case RT_OPT_HOST_CHUNK_MB:
@@ -2083,20 +2087,20 @@ RT_EXPORT int rt_render_sequence_async(rt_ctx* c, const rt_frame* frames, int32_
         if (int rc = fence_async(c, st)) return rc;
     }
     // Fork: the internal streams start after everything already on st.
-    const int S = std::min(n, kSeqSlots);
-    if (S > 1) {
-        for (int j = 0; j < S; ++j) {
+    const int nstreams = std::min(n, kSeqSlots);
+    if (nstreams > 1) {
+        for (int j = 0; j < nstreams; ++j) {
             if (!c->seq_streams[j]) HIP_TRY(c, hipStreamCreateWithFlags(&c->seq_streams[j], hipStreamNonBlocking));
             if (!c->seq_join[j]) HIP_TRY(c, hipEventCreateWithFlags(&c->seq_join[j], hipEventDisableTiming));
         }
         if (!c->seq_fork) HIP_TRY(c, hipEventCreateWithFlags(&c->seq_fork, hipEventDisableTiming));
         HIP_TRY(c, hipEventRecord(c->seq_fork, st));
-        for (int j = 0; j < S; ++j) HIP_TRY(c, hipStreamWaitEvent(c->seq_streams[j], c->seq_fork, 0));
+        for (int j = 0; j < nstreams; ++j) HIP_TRY(c, hipStreamWaitEvent(c->seq_streams[j], c->seq_fork, 0));
     }
     for (int i = 0; i < n; ++i) {
         const rt_frame* f = frames + i;
         const rt_ctx::CamSlot& q = c->seq[i % kSeqSlots];
-        hipStream_t fs = S > 1 ? c->seq_streams[i % S] : st;
+        hipStream_t fs = nstreams > 1 ? c->seq_streams[i % nstreams] : st;
         const int rows = frame_rows(f);
         if (rows == 0) continue;
         if (c->n_tri > 0) {
@@ -2121,8 +2125,8 @@ RT_EXPORT int rt_render_sequence_async(rt_ctx* c, const rt_frame* frames, int32_
         HIP_TRY(c, hipLaunchKernel((const void*)k, grid, block, args, lds, fs));
     }
     // Join: st continues after every frame.
-    if (S > 1) {
-        for (int j = 0; j < S; ++j) {
+    if (nstreams > 1) {
+        for (int j = 0; j < nstreams; ++j) {
             HIP_TRY(c, hipEventRecord(c->seq_join[j], c->seq_streams[j]));
             HIP_TRY(c, hipStreamWaitEvent(st, c->seq_join[j], 0));
         }
@@ -2199,7 +2203,7 @@ RT_EXPORT int rt_last_stats(rt_ctx* c, rt_stats* out)
 }
 
 #ifdef RT_PROF
-// Diagnostic builds only (not in include/rt.h): read and clear the per-section
+// Diagnostic builds only (include/rt_debug.h, RT_PROF): read and clear the per-section
 // shader-clock totals (summed over waves).
 extern "C" __attribute__((visibility("default"))) int rt_debug_prof(unsigned long long* out8)
 {
@@ -2228,7 +2232,7 @@ extern "C" __attribute__((visibility("default"))) int rt_debug_prof_events(unsig
 }
 #endif
 
-// Diagnostic (not in include/rt.h): light-buffer summary of the uploaded
+// Diagnostic (include/rt_debug.h): light-buffer summary of the uploaded
 // scene: out[0] = built (0/1), out[1] = entries, out[2] = build ms,
 // then per light (up to (n - 3) / 3): R, dcap-list length, dcov.
 RT_EXPORT int rt_debug_lb_info(rt_ctx* c, double* out, int n)
@@ -2252,7 +2256,7 @@ RT_EXPORT int rt_debug_lb_info(rt_ctx* c, double* out, int n)
     return RT_OK;
 }
 
-// Diagnostic (not in include/rt.h): camera-buffer summary: out[0] = current
+// Diagnostic (include/rt_debug.h): camera-buffer summary: out[0] = current
 // (0/1), out[1] = entries, out[2] = last build ms (device time of its
 // kernels, from its first to its last, plus nothing of the host), out[3] =
 // tiles, out[4] = inline records (0/1), out[5] = the build's host wall time
@@ -2284,7 +2288,7 @@ RT_EXPORT int rt_debug_cb_info(rt_ctx* c, double* out, int n)
     return RT_OK;
 }
 
-// Diagnostic (not in include/rt.h): the last rt_upload_scene's host wall
+// Diagnostic (include/rt_debug.h): the last rt_upload_scene's host wall
 // time by part (ms): out[0] records + device copies, out[1] cone / cluster
 // prepasses, out[2] light buffer (incl. its far ladder), out[3] total.
 RT_EXPORT int rt_debug_upload_info(rt_ctx* c, double* out, int n)
@@ -2297,7 +2301,7 @@ RT_EXPORT int rt_debug_upload_info(rt_ctx* c, double* out, int n)
     return RT_OK;
 }
 
-// Diagnostic (not in include/rt.h): run rt_selftest_kernel over `blocks`
+// Diagnostic (include/rt_debug.h): run rt_selftest_kernel over `blocks`
 // workgroups; *failures = lanes whose wave reduction or wave cone was wrong.
 RT_EXPORT int rt_debug_selftest(int device, int blocks, unsigned* failures)
 {

@@ -62,7 +62,7 @@ int main(int argc, char** argv)
         return 1;
     }
     int W = 512, H = 256, depth = 0, dev0 = 0, frames = 1, gpus = 1, threads = 0;
-    bool stats = false, bands = false, cpu = false;
+    bool stats = false, bands = false, cpu = false, dev_given = false, g_given = false;
     const char* out = nullptr;
     for (int i = 2; i < argc; ++i) {
         if (argv[i][0] != '-') continue;
@@ -71,6 +71,7 @@ int main(int argc, char** argv)
         };
         if (std::strcmp(argv[i], "--device") == 0) {
             next(dev0);
+            dev_given = true;
             continue;
         }
         if (std::strcmp(argv[i], "--bands") == 0) {
@@ -93,7 +94,10 @@ int main(int argc, char** argv)
         case 'x': next(W); break;
         case 'y': next(H); break;
         case 'd': next(depth); break;
-        case 'g': next(gpus); break;
+        case 'g':
+            next(gpus);
+            g_given = true;
+            break;
         case 'n': next(frames); break;
         case 's': stats = true; break;
         case 'o':
@@ -102,6 +106,9 @@ int main(int argc, char** argv)
         }
     }
     if (W <= 0 || H <= 0 || gpus <= 0 || frames <= 0) return fail("arguments", RT_E_ARG, "-x/-y/-g/-n must be > 0");
+    // -g was the HIP device index before ABI 3; it is now the GPU count
+    if (g_given && !dev_given)
+        std::fprintf(stderr, "[NOTE]: -g %d = number of GPUs (from device 0); the device index is --device\n", gpus);
     if (((W - 1) & W) || ((H - 1) & H))
         std::fprintf(stderr, "[ATTENTION]: Resolution %dx%d n'est pas une puissance de deux "
                              "(accepted: the render core has no such restriction)\n", W, H);

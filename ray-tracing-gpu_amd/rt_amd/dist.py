@@ -160,8 +160,10 @@ class RootGather:
         rendered: ONE collective call per batch (RCCL runs it as a group of
         point-to-point receives on rank 0 and one send per peer, each over
         its own direct xGMI link), so the host cost per batch does not grow
-        with the number of ranks."""
-        if self.world == 1 or k % self.batch != self.batch - 1:
+        with the number of ranks.  With one rank the same collective runs (a
+        local copy inside the backend), so packing, bands and the batch
+        unpack are the same code at every world size."""
+        if k % self.batch != self.batch - 1:
             return
         self._post(k // self.batch)
 
@@ -205,7 +207,7 @@ class RootGather:
 
     def finish(self):
         """Post a partial last batch, then wait for every pending gather."""
-        if self.world > 1 and self.last >= 0 and self.last // self.batch > self.posted:
+        if self.last >= 0 and self.last // self.batch > self.posted:
             self._post(self.last // self.batch)
         for b in range(self.depth):
             self._wait_slot(b)

@@ -114,6 +114,16 @@ def digests():
 
 
 @pytest.fixture(scope="session")
+def config_golden():
+    """BASELINE.json configs at full size from oracle/_ref (make_config_golden.py):
+    C1's whole float32 frame and C4-scene2's digests."""
+    with open(os.path.join(GOLDEN, "configs.json")) as f:
+        d = json.load(f)
+    d["c1_frame"] = np.load(os.path.join(GOLDEN, "c1.npz"))["scene1_512x512_d1"]
+    return d
+
+
+@pytest.fixture(scope="session")
 def heightfield_path(tmp_path_factory):
     from rt_amd import synth
 

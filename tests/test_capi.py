@@ -35,6 +35,20 @@ def test_header_symbols_exported():
         assert re.search(rf"\bT {n}\b", out), n
 
 
+def test_every_export_is_declared():
+    """No undocumented exports: every rt_* symbol of the library is declared in
+    include/rt.h (the boundary) or include/rt_debug.h (diagnostics), and
+    rt_debug.h's symbols outside its RT_PROF block are exported."""
+    dbg = open(os.path.join(REPO, "include", "rt_debug.h")).read()
+    dbg = re.sub(r"/\*.*?\*/", "", dbg, flags=re.S)
+    dbg_all = set(re.findall(r"\b(rt_[a-z_0-9]+)\s*\(", dbg))
+    dbg_plain = set(re.findall(r"\b(rt_[a-z_0-9]+)\s*\(", re.sub(r"#ifdef RT_PROF.*?#endif", "", dbg, flags=re.S)))
+    out = subprocess.run(["nm", "-D", "--defined-only", rt_amd.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r"\bT (rt_[a-z_0-9]+)\b", out))
+    assert exported <= set(declared_functions()) | dbg_all, exported - set(declared_functions()) - dbg_all
+    assert dbg_plain <= exported, dbg_plain - exported
+
+
 def test_abi_version():
     assert rt_amd.lib().rt_abi_version() == 4
 

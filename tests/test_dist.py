@@ -91,7 +91,9 @@ def _worker_root(rank, world, port, path, w, h, depth, out_q, band_rows=0, batch
 @pytest.mark.parametrize("world,h,band_rows,batch,nframes,send_channels", [
     (2, 30, 0, 1, 3, 0), (3, 31, 0, 1, 3, 0), (2, 70, 16, 1, 3, 0), (3, 71, 16, 1, 3, 0), (3, 50, 32, 1, 3, 0),
     (2, 30, 0, 2, 4, 0), (3, 31, 0, 3, 5, 0), (2, 70, 16, 2, 3, 0), (3, 71, 16, 4, 7, 0),
-    (2, 30, 0, 1, 3, 3), (3, 31, 0, 3, 5, 3), (3, 71, 16, 4, 7, 3)])
+    (2, 30, 0, 1, 3, 3), (3, 31, 0, 3, 5, 3), (3, 71, 16, 4, 7, 3),
+    # one rank: the same collective path (frames must not stay the fill)
+    (1, 30, 0, 1, 3, 0), (1, 31, 0, 4, 6, 3), (1, 70, 16, 2, 3, 3), (1, 50, 16, 3, 5, 4)])
 def test_root_gather_pipelined(oracle, world, h, band_rows, batch, nframes, send_channels):
     w = 36
     path = os.path.join(SCENES, "scene7.dat")

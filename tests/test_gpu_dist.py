@@ -75,3 +75,88 @@ def test_heightfield_ranks_match_one_rank(one_rank, n):
     out = _bench(n, "c3", "auto")
     assert out["frame_rgba8_sha256"] == one_rank["c3"]["frame_rgba8_sha256"]
     assert out["config"]["slab_imbalance"] is not None
+
+
+# ---- RCCL itself on the 1-GPU box: an "nccl" process
+# group of one rank runs the code the driver's 8-GPU run depends on — the
+# process-group init with device_id, the CUDA-tensor all-reduce, and
+# RootGather's dist.gather of device tensors with async_op on RCCL's stream.
+def _rccl_worker(port, cfgs, q):
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+    try:
+        assert dist.get_backend() == "nccl"
+        t = torch.tensor([2.5], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        assert float(t.item()) == 2.5
+        import rt_amd
+        from rt_amd.dist import RootGather, band_layout
+
+        s = rt_amd.Scene(os.path.join(REPO, "tests", "golden", "scenes", "scene7.dat"), 96, 70, 3)
+        ctx = rt_amd.Context(0)
+        ctx.upload(s)
+        stream = torch.cuda.current_stream().cuda_stream
+        fails = []
+        for band, batch, ch, nframes in cfgs:
+            g = RootGather(dist, 70, 96, "cuda", band_rows=band, batch=batch, send_channels=ch)
+            want = []
+            for k in range(nframes):
+                f = s.frame.copy()
+                f.cam_pos[0] += 0.5 * k  # a different image per frame
+                if band:
+                    f.band_rows, f.band_count, f.band_index = band, 1, 0
+                out = g.target(k)
+                ctx.render_async(f, out.data_ptr(), 0, stream)
+                g.submit(k)
+                full = s.frame.copy()
+                full.cam_pos[0] += 0.5 * k
+                want.append(ctx.render(full))
+            g.finish()
+            for k in range(max(0, nframes - 2 * batch), nframes):
+                got = g.frame(k).cpu().numpy()
+                if not np.array_equal(got, want[k]):
+                    fails.append((band, batch, ch, k))
+        ctx.close()
+        q.put(("ok", fails))
+    except Exception as e:  # report, then tear down
+        q.put(("error", repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_one_rank_root_gather():
+    import torch.multiprocessing as mp
+
+    cfgs = [(0, 1, 0, 3), (0, 4, 0, 6), (0, 1, 3, 3), (0, 4, 3, 7), (16, 1, 3, 3), (16, 4, 4, 6), (16, 3, 3, 5)]
+    ctxm = mp.get_context("spawn")
+    q = ctxm.Queue()
+    p = ctxm.Process(target=_rccl_worker, args=(_port(), cfgs, q))
+    p.start()
+    status, res = q.get(timeout=180)
+    p.join(timeout=60)
+    assert status == "ok", res
+    assert res == [], res
+    assert p.exitcode == 0
+
+
+def test_bench_nccl_one_rank_runs_the_rccl_path(one_rank):
+    """bench.py under torch.distributed.run with one rank and --force-dist:
+    init_process_group("nccl", device_id=...), the CUDA-tensor all-reduces and
+    the RootGather path, with the frame byte-identical to the plain run."""
+    args = ["bench.py", "--gpus", "1", "--steps", "3", "--warmup", "1", "--config", "c2", "--frame-sha",
+            "--no-cpu-baseline", "--no-host-boundary", "--force-dist", "--dist-backend", "nccl"]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port())] + args
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2")
+    r = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith('{"metric"')]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert "RCCL gather" in out["config"]["parallelism"]
+    assert out["frame_rgba8_sha256"] == one_rank["c2"]["frame_rgba8_sha256"]
