@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 4
+#define RT_ABI_VERSION 5
 
 enum {
     RT_OK = 0,
@@ -146,10 +146,12 @@ int rt_render(rt_ctx*, const rt_frame*, uint8_t* rgba8_out);
 int rt_render_float(rt_ctx*, const rt_frame*, float* rgb_out);
 /* Asynchronous, device pointers only, enqueued on `hip_stream` (a hipStream_t;
  * NULL = the HIP null stream, as in every HIP API).  Either output may be
- * NULL.  No host sync, no allocation.  It uses the camera buffer only when it
- * is current for the frame's camera (never builds it): one synchronous render
- * after a camera change makes the following async renders take the fast
- * path.  Same image either way.
+ * NULL.  No host sync.  ABI 5: a new camera's per-camera state — the camera
+ * buffer included — is built on `hip_stream` too, so a moving camera keeps
+ * the fast path; allocation happens only when that state grows (its
+ * capacity follows earlier builds' totals, read back without waiting; a tile
+ * whose list does not fit this time renders by the per-wave path — the same
+ * image either way).
  *
  * Ordering (ABI 4).  The context keeps per-camera state on the device (camera
  * records, cone records, the camera buffer).  Every write of that state is
@@ -177,14 +179,16 @@ int rt_render_async(rt_ctx*, const rt_frame*, uint8_t* rgba8_dev, float* rgb_dev
  * own camera into sequence slot i % 4 (apart from the state the other
  * render calls use) and runs on the context's internal stream i % 4, forked
  * from and joined back into `hip_stream` by events, so up to four
- * consecutive frames are in flight at once; the call needs no host sync and
- * no allocation after the first, and a sequence captured into a hipGraph
+ * consecutive frames are in flight at once; the call needs no host sync (and
+ * allocates only when a slot's state grows), and a sequence captured into a hipGraph
  * (the internal streams join the capture) replays exactly whatever was
  * rendered on the context between capture and replay.  A sequence waits for
  * the context's async work on other streams (the slots are shared); a
  * captured one is ordered by its graph's position only.  Shadow rays use the
- * light buffer; camera rays the per-wave culling (no camera buffer).
- * RT_FLAG_STATS is not accepted here. */
+ * light buffer; camera rays the slot's own camera buffer (ABI 5: built on
+ * the frame's stream; inside a capture only into a slot an earlier call
+ * sized, else the per-wave culling — the same image).  RT_FLAG_STATS is not
+ * accepted here. */
 int rt_render_sequence_async(rt_ctx*, const rt_frame* frames, int32_t n, uint8_t* rgba8_dev, size_t rgba8_stride,
                              float* rgb_dev, size_t rgb_stride, void* hip_stream);
 /* ABI 4: make the per-camera state (camera records, and the camera buffer
@@ -225,10 +229,14 @@ enum {
                                    records while they fit this many MiB (default 0 =
                                    never: the index walk, whose records are staged in
                                    LDS per window; 128 was the round-1 default) */
-    RT_OPT_HOST_CHUNK_MB = 7    /* launch: synchronous renders into host memory render
+    RT_OPT_HOST_CHUNK_MB = 7,   /* launch: synchronous renders into host memory render
                                    and copy in row chunks of this many MiB of output,
                                    each copy overlapping the next chunk (default 8;
                                    0 = one kernel, then one copy) */
+    RT_OPT_CB_CAPACITY = 8      /* launch (ABI 5): camera-buffer entries allocated;
+                                   0 (default) = sized from earlier builds' totals.  A
+                                   tile whose list does not fit renders by the per-wave
+                                   path (tests: a small value exercises that path) */
 };
 int rt_set_option(rt_ctx*, int32_t option, double value);
 int rt_get_option(rt_ctx*, int32_t option, double* value);

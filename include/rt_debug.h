@@ -24,9 +24,16 @@ int rt_debug_lb_info(rt_ctx*, double* out, int n);
 
 /* Camera buffer of the last build: out[0] current (0/1), out[1] entries,
  * out[2] device ms of the build's kernels, out[3] tiles, out[4] inline
- * records (0/1), out[5] host wall ms of the build's enqueue; out[6..8]
- * build counters (n > 8; see DESIGN.md §3 "Camera buffer"). */
+ * records (0/1), out[5] host wall ms of the build's enqueue; out[6..10]
+ * binning counters: triangles binned by the whole grid, (triangle, tile)
+ * pairs tested, lists longer than 256, the longest, the entry capacity. */
 int rt_debug_cb_info(rt_ctx*, double* out, int n);
+
+/* The current camera buffer checked against brute force (every tile with
+ * a list against every triangle; synchronous): out[0] tiles whose list is
+ * not exactly the triangles passing the camera wave test (or mis-keyed),
+ * out[1] passing pairs, out[2] tiles with a list. */
+int rt_debug_cb_verify(rt_ctx*, unsigned long long* out3);
 
 /* The last rt_upload_scene's host wall time by part (ms): out[0] records +
  * device copies, out[1] cone / cluster prepasses, out[2] light buffer,

@@ -3,6 +3,26 @@
 // Part of the device code of rt_kernels.hip (one translation unit: the
 // kernels are templates instantiated by its host half); built with the
 // same exactness flags (no FMA contraction, IEEE div/sqrt).
+//
+// What a list holds (unchanged since round 1): tile t of the full frame
+// keeps triangle k iff the camera wave test of the per-wave path —
+// cone_overlap(wc_t, c0_k, sinT_k) and the three edge planes, wc_t the
+// wave cone of the tile's 64 camera rays (wave_cone on the clamped pixels,
+// the trace kernel's own bits) — passes: the triangles the per-wave path
+// would test exactly, so walking the list instead is exact.
+//
+// How it is built (round 3: binning by triangle, no host sync).  The test is
+// evaluated only for (triangle, tile) pairs whose tile lies in the
+// triangle's screen box — a box that provably contains every tile where the
+// test can pass (cb_box below) — instead of every tile walking every
+// cluster.  Per camera: rt_cb_tiles (the tile cones), rt_cb_bin<false> /
+// rt_cb_bin_big<false> (counts per tile), a device scan (offsets),
+// rt_cb_bin<true> / rt_cb_bin_big<true> (the entries, each at an atomic slot
+// of its tile), rt_cb_keys_wave (order and early-exit keys).  The entry
+// array has a fixed capacity chosen by the host from earlier builds; a tile
+// whose list would end past it is flagged and takes the per-wave path (the
+// same image), and the host grows the array once it reads the total back —
+// so moving cameras rebuild on the stream, with no host round trip.
 #ifndef RT_AMD_RT_CAMBUF_H
 #define RT_AMD_RT_CAMBUF_H
 
@@ -22,356 +42,265 @@ __device__ __forceinline__ bool cb_tile_row_needed(const FrameDev& F, int ty)
     return ty * 8 < F.row_end && ty * 8 + 8 > F.row_begin;
 }
 
-// One wave per 8x8 tile of the full frame, laid out like rt_trace_kernel
-// (256-thread blocks of 2 x 2 tiles): the tile's 64 camera rays (camera_dir
-// on the same clamped pixels as the trace kernel, so the same bits), their
-// wave cone, and the camera wave test of every cluster / member
-// (cone_overlap, and the edge planes) — the culling closest_hit_camera_wave
-// runs per frame, done once per camera.  COUNT: cnt[tile] = survivors;
-// else the survivors {triangle, dmin} in cluster order from off[tile].
-template <bool FILL>
-__global__ __launch_bounds__(256) void rt_cb_build(const SceneDev S, const FrameDev F, const unsigned* __restrict__ off,
-                                                   unsigned* __restrict__ cnt, unsigned* __restrict__ flag,
-                                                   int2* __restrict__ ent)
+// Per-build device state (one per camera buffer: the context's, and one per
+// sequence slot).  stat words: [0] triangles deferred to rt_cb_bin_big,
+// [1] (triangle, tile) pairs tested, [2] (unused), [3] lists longer than
+// RT_CB_SORT (their tiles in lng[]), [4] the longest of them.
+struct CbDev {
+    float4* __restrict__ tcone;   // 2 per tile: [w cosW] [sinW chord 0 0]
+    unsigned* __restrict__ off;   // nt + 1: counts, scanned in place into offsets
+    unsigned* __restrict__ cur;   // nt: fill cursors
+    unsigned* __restrict__ flag;  // nt: 1 = no list (per-wave path)
+    int2* __restrict__ ent;       // cap entries {triangle, dmin bits}
+    int* __restrict__ big;        // n_tri: triangles deferred to the grid-wide pass
+    int* __restrict__ lng;        // nt: tiles whose lists rt_cb_keys_long sorts
+    unsigned* __restrict__ stat;  // 8 words (above)
+    unsigned cap;                 // entries allocated
+    int tiles_x, tiles_y;
+    float wbound;                 // every listed tile's cone half-angle <= wbound (rad)
+    float cos_wbound;             // >= cos(wbound): a tile with cosW below it gets no list
+};
+
+// The tile cones (one wave per tile of the full frame, 4 per workgroup):
+// the trace kernel's own wave cone of the tile's 64 clamped pixels.  A tile
+// outside the frame's rows, with a degenerate cone, or wider than the bound
+// the boxes assume (cosW < cos_wbound; never seen: the bound is analytic)
+// gets no list.  Also zeroes the counts and cursors.
+__global__ __launch_bounds__(256) void rt_cb_tiles(const FrameDev F, CbDev B)
 {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int tx = blockIdx.x * 2 + (wave & 1), ty = blockIdx.y * 2 + (wave >> 1);
-    if (tx * 8 >= F.width || ty * 8 >= F.height) return;
-    const int tile = ty * S.cb_tiles_x + tx;
-    if (!cb_tile_row_needed(F, ty)) {  // outside the frame's rows: no list
-        if (!FILL && lane == 0) {
-            flag[tile] = 1u;
-            cnt[tile] = 0u;
-        }
-        return;
+    const int lane = (int)(threadIdx.x & 63);
+    const int t = (int)(blockIdx.x * 4 + (threadIdx.x >> 6));
+    const int nt = B.tiles_x * B.tiles_y;
+    if (t >= nt) return;  // wave-uniform
+    const int tx = t % B.tiles_x, ty = t / B.tiles_x;
+    const bool present = cb_tile_row_needed(F, ty);
+    WaveCone wc;
+    wc.ok = false;
+    if (present) {
+        const int px = tx * 8 + (lane & 7), py = ty * 8 + (lane >> 3);
+        const Vec3 D = camera_dir(F, px < F.width ? px : F.width - 1, py < F.height ? py : F.height - 1);
+        wc = wave_cone(D, true);
     }
-    const int px = tx * 8 + (lane & 7), py = ty * 8 + (lane >> 3);
-    const Vec3 D = camera_dir(F, px < F.width ? px : F.width - 1, py < F.height ? py : F.height - 1);
-    const WaveCone wc = wave_cone(D, true);
-    if (!wc.ok) {  // no list: the trace kernel's per-wave path
-        if (!FILL && lane == 0) {
-            flag[tile] = 1u;
-            cnt[tile] = 0u;
-        }
-        return;
-    }
-    unsigned n = 0, base = FILL ? off[tile] : 0u;
-    const unsigned long long below = (1ull << lane) - 1ull;
-    auto batch = [&](int k0) {
-        const int k = k0 + lane;
-        bool reach = false;
-        float dmin = 0.0f;
-        if (k < S.n_tri) {
-            const float4 c0 = S.cone_cam[2 * k], c1 = S.cone_cam[2 * k + 1];
-            dmin = c1.x;
-            reach = cone_overlap(wc, c0, c1.w, 0.0f) && edges_open(wc, S.cone_cam + 2 * (size_t)S.n_tri + 3 * k, 0.0f);
-        }
-        const unsigned long long m = __ballot(reach);
-        if (FILL && reach) ent[base + n + (unsigned)__popcll(m & below)] = make_int2(k, __float_as_int(dmin));
-        n += (unsigned)__popcll(m);
-    };
-    if (S.n_clu > 0) {
-        for (int c0i = 0; c0i < S.n_clu; c0i += 64) {
-            const int cl = c0i + lane;
-            float4 q0 = make_float4(0.f, 0.f, 0.f, 1.f), q1 = make_float4(INFINITY, 0.f, 0.f, 0.f);
-            if (cl < S.n_clu) {
-                q0 = S.clu_cam[2 * cl];
-                q1 = S.clu_cam[2 * cl + 1];
-            }
-            const int id = __float_as_int(q1.y);
-            unsigned long long cm = __ballot(cone_overlap(wc, q0, q1.w, 0.0f, 4e-6f));
-            while (cm) {
-                const int b = (int)__builtin_ctzll(cm);
-                cm &= cm - 1;
-                batch(64 * __builtin_amdgcn_readlane(id, b));
-            }
-        }
-    } else {
-        for (int k0 = 0; k0 < S.n_tri; k0 += 64) batch(k0);
-    }
-    if (!FILL && lane == 0) {
-        cnt[tile] = n;
-        flag[tile] = 0u;
+    const bool use = present && wc.ok && wc.cosW >= B.cos_wbound;
+    if (lane == 0) {
+        B.tcone[2 * t] = make_float4(wc.w.x, wc.w.y, wc.w.z, wc.cosW);
+        B.tcone[2 * t + 1] = make_float4(wc.sinW, wc.chord, 0.f, 0.f);
+        B.flag[t] = use ? 0u : 1u;
+        B.off[t] = 0u;
+        B.cur[t] = 0u;
     }
 }
 
-// ------------------------------------------------ block pre-cull (big lists)
-// rt_cb_build walks every cluster for every tile: at C5 (518k tiles, 782
-// clusters) that is most of the camera buffer's cost, and the same cluster
-// and member records are read by every tile.  rt_cb_block does it once per
-// block of 8 x 8 tiles: one workgroup computes the 64 tile cones (the
-// tiles' own wave_cone, bit for bit), a block cone that contains them all,
-// culls clusters and members against the block cone into a list staged in
-// LDS (member ids and cone records, cluster order), and then tests each tile
-// against that list with the tile kernel's own predicate.
+// The screen box of triangle k: tiles [tx0, tx0 + nx) x [ty0, ty0 + ny)
+// containing every tile whose camera wave test with k can pass.
 //
-// Why the block list is a superset of every tile's (so each tile's list is
-// exactly rt_cb_build's, same entries, same order): a tile keeps member k
-// when (float) w_t.a >= c_t cT - s_t sT - 2e-6 (cone_overlap) and its edge
-// planes are open.  With W_t = acos(c_t), s_t <= sin W_t + 1.1e-6 and the
-// record's sT >= sin T, that implies cos(theta_t) >= cos(W_t + T) - m, m =
-// 5e-6 (rounding included), theta_t = angle(w_t, a); so theta_t exceeds
-// W_t + T by at most delta = 2 asin(sqrt(m / 2)).  The block axis w_b is
-// alpha_t from w_t, and W_b >= W_t + alpha_t for every tile, so theta_b <=
-// theta_t + alpha_t and cos(theta_b) >= cos(W_b + T) - m - delta sin(alpha)
-// (W_b + T < 150 degrees: cT > 0, W_b < 60).  The block test uses c_b <=
-// cos W_b, s_b >= sin W_b and the margin M_b = m + delta sin(alpha_max) plus
-// its own rounding.  Edge planes: w_b.n >= w_t.n - |w_b - w_t|, so
-// E_b = max_t(chord(alpha_t) + chord_t) + rounding bounds every tile's
-// w_t.n + chord_t.  The cluster test with margin M_b + 2e-6 is implied by
-// its members' block tests (rt_cluster_prepass, cosW >= 1/2).  A block with
-// a degenerate tile cone, W_b >= 60 degrees or more than kCbBlockCap
-// survivors runs rt_cb_build's per-tile walk for its tiles instead.
-constexpr int kCbBlockCap = 320;  // staged members per block (LDS)
-
-__device__ __forceinline__ double wave_sum_d(double v)
+// Why.  With c0 = [a, cosT] (cosT > 0), the test passing means (float
+// rounding included: dot, |w|, |a|, cosW/sinW/sinT margins, the 2e-6
+// margin) cos angle(w, a) >= cos(W + T) - 4.4e-6, W = acos(cosW) <= wbound,
+// T = acos(cosT), hence angle(w, a) <= T + wbound + 2.97e-3 (the worst case,
+// at W + T = 0, is sqrt(2 * 4.4e-6)).  w is the direction of the tile's
+// reference lane 36 = pixel (8tx + 4, 8ty + 4) clamped to the frame:
+// normalize(d0 M), d0 = (X, Y, -1), X = (2 px inv_w - 1) half_w, likewise Y;
+// M's rows r0 r1 r2 orthonormal to 1e-5 (checked by the host, which gives up
+// the buffer otherwise) put w in camera coordinates as normalize(d0) within
+// 2e-5.  So the reference pixel's d0 lies in the cone of half-angle
+// Th = T + wbound + 6.2e-3 around a_c = (a.r0, a.r1, a.r2): the rays
+// through the sphere of radius sin Th around the unit a_c.  Its extent in
+// X = x / (-z) is that of the disk (a_c.x, a_c.z; sin Th) seen from the
+// origin in the xz plane: the two tangents, when the disk misses the
+// origin and both lie in front (z < 0; then so does the whole wedge, which
+// is narrower than pi) — else every column.  Likewise Y.  Pixels from X by
+// the inverse of the affine map, 2 pixels of slack each side; the tiles
+// whose pixel ranges meet that span.  cosT <= 0 (an "always test" record)
+// or Th >= 80 degrees: every tile.
+struct CbBox {
+    int tx0, ty0, nx, ny;
+};
+__device__ __forceinline__ bool cb_span(double cx, double cz, double rho, double& lo, double& hi)
 {
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
+    const double d2 = cx * cx + cz * cz;
+    if (!(d2 > rho * rho * (1.0 + 1e-9) + 1e-18)) return false;
+    const double t = sqrt(d2 - rho * rho);
+    const double ux1 = cx * t - cz * rho, uz1 = cx * rho + cz * t;
+    const double ux2 = cx * t + cz * rho, uz2 = -cx * rho + cz * t;
+    const double n1 = sqrt(ux1 * ux1 + uz1 * uz1), n2 = sqrt(ux2 * ux2 + uz2 * uz2);
+    if (!(uz1 < -1e-9 * n1) || !(uz2 < -1e-9 * n2)) return false;
+    const double s1 = ux1 / -uz1, s2 = ux2 / -uz2;
+    lo = fmin(s1, s2);
+    hi = fmax(s1, s2);
+    return isfinite(lo) && isfinite(hi);
 }
-__device__ __forceinline__ double wave_max_d(double v)
+// tile range [t0, t1] of a pixel span from slope span [lo, hi] (X or Y).
+__device__ __forceinline__ void cb_tiles_of(bool bounded, double lo, double hi, float half, float inv, int npx,
+                                            int ntiles, int& t0, int& t1)
 {
-    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
-    return v;
+    t0 = 0;
+    t1 = ntiles - 1;
+    if (!bounded) return;
+    const double s = 1.0 / (2.0 * (double)inv);
+    double p0 = floor((lo / (double)half + 1.0) * s) - 2.0, p1 = ceil((hi / (double)half + 1.0) * s) + 2.0;
+    p0 = fmax(p0, 0.0);
+    p1 = fmin(p1, (double)(npx - 1));
+    if (p1 < p0) {
+        t0 = 1;
+        t1 = 0;
+        return;
+    }
+    t0 = (int)(p0 / 8.0);
+    t1 = min(ntiles - 1, (int)(p1 / 8.0));
+}
+__device__ __forceinline__ CbBox cb_box(const float4 c0, const FrameDev& F, const CbDev& B)
+{
+    CbBox b{0, 0, B.tiles_x, B.tiles_y};
+    if (!(c0.w > 0.0f)) return b;  // always tested: every tile
+    const double Th = acos(fmin(1.0, (double)c0.w)) + (double)B.wbound + 6.2e-3;
+    if (!(Th < 1.396)) return b;
+    const double an = sqrt((double)c0.x * c0.x + (double)c0.y * c0.y + (double)c0.z * c0.z);
+    if (!(an > 0.5) || !isfinite(an)) return b;
+    const double ax = c0.x / an, ay = c0.y / an, az = c0.z / an;
+    const double cx = ax * F.orient[0] + ay * F.orient[1] + az * F.orient[2];
+    const double cy = ax * F.orient[4] + ay * F.orient[5] + az * F.orient[6];
+    const double cz = ax * F.orient[8] + ay * F.orient[9] + az * F.orient[10];
+    const double rho = sin(Th);
+    double xlo = 0, xhi = 0, ylo = 0, yhi = 0;
+    const bool bx = cb_span(cx, cz, rho, xlo, xhi);
+    const bool by = cb_span(cy, cz, rho, ylo, yhi);
+    int x0, x1, y0, y1;
+    cb_tiles_of(bx, xlo, xhi, F.half_w, F.inv_w, F.width, B.tiles_x, x0, x1);
+    cb_tiles_of(by, ylo, yhi, F.half_h, F.inv_h, F.height, B.tiles_y, y0, y1);
+    if (x1 < x0 || y1 < y0) return CbBox{0, 0, 0, 0};
+    return CbBox{x0, y0, x1 - x0 + 1, y1 - y0 + 1};
 }
 
-// rt_cb_build's per-tile walk over every cluster (global records).
+// The camera wave test of triangle k's records for tile t (rt_cb_tiles' cone).
+__device__ __forceinline__ bool cb_pair_test(const CbDev& B, int t, const float4 c0, float sinT, const float4* e)
+{
+    const float4 a = B.tcone[2 * t], b = B.tcone[2 * t + 1];
+    WaveCone wc;
+    wc.w = make3(a.x, a.y, a.z);
+    wc.cosW = a.w;
+    wc.sinW = b.x;
+    wc.chord = b.y;
+    wc.ok = true;
+    return cone_overlap(wc, c0, sinT, 0.0f) && edges_open(wc, e, 0.0f);
+}
+// One passing pair: count it (FILL false), or write its entry at its tile's
+// next slot — unless the tile's list would end past the capacity: then the
+// tile is flagged (no list: the per-wave path) and nothing is written.
 template <bool FILL>
-__device__ __forceinline__ unsigned cb_tile_walk(const SceneDev& S, const WaveCone& wc, unsigned base,
-                                                 int2* __restrict__ ent)
+__device__ __forceinline__ void cb_emit(const CbDev& B, int t, int k, float dmin)
 {
-    const int lane = threadIdx.x & 63;
+    if (!FILL) {
+        atomicAdd(&B.off[t], 1u);
+        return;
+    }
+    const unsigned e1 = B.off[t + 1];
+    if (e1 > B.cap) {
+        B.flag[t] = 1u;
+        return;
+    }
+    const unsigned slot = B.off[t] + atomicAdd(&B.cur[t], 1u);
+    B.ent[slot] = make_int2(k, __float_as_int(dmin));
+}
+
+// Boxes up to this many tiles are binned by their own wave (rt_cb_bin);
+// larger ones (an always-tested record, a triangle near the camera) by the
+// whole grid (rt_cb_bin_big), so no wave walks a long box alone.
+constexpr int kCbWaveTiles = 2048;
+
+// One wave per 64 consecutive triangles (4 waves per workgroup): each lane
+// boxes its triangle; the wave then walks the concatenation of the 64 boxes
+// one pair per lane per step (the owner of pair p by a binary search over
+// the boxes' prefix sums in LDS), so a step tests 64 pairs whatever the box
+// sizes.  FILL false: count per tile and defer the big boxes; true: write.
+template <bool FILL>
+__global__ __launch_bounds__(256) void rt_cb_bin(const SceneDev S, const FrameDev F, CbDev B)
+{
+    __shared__ float4 rec[4][64][5];
+    __shared__ int box[4][64][3];  // tx0, ty0, nx
+    __shared__ unsigned incl[4][64];
+    const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6);
+    const int k = (int)((blockIdx.x * 4 + wv) * 64) + lane;
     unsigned n = 0;
-    const unsigned long long below = (1ull << lane) - 1ull;
-    auto batch = [&](int k0) {
-        const int k = k0 + lane;
-        bool reach = false;
-        float dmin = 0.0f;
-        if (k < S.n_tri) {
-            const float4 c0 = S.cone_cam[2 * k], c1 = S.cone_cam[2 * k + 1];
-            dmin = c1.x;
-            reach = cone_overlap(wc, c0, c1.w, 0.0f) && edges_open(wc, S.cone_cam + 2 * (size_t)S.n_tri + 3 * k, 0.0f);
+    if (k < S.n_tri) {
+        const float4 c0 = S.cone_cam[2 * k];
+        const CbBox b = cb_box(c0, F, B);
+        n = (unsigned)(b.nx * b.ny);
+        if (n > (unsigned)kCbWaveTiles) {
+            if (!FILL) B.big[atomicAdd(&B.stat[0], 1u)] = k;
+            n = 0;
         }
-        const unsigned long long m = __ballot(reach);
-        if (FILL && reach) ent[base + n + (unsigned)__popcll(m & below)] = make_int2(k, __float_as_int(dmin));
-        n += (unsigned)__popcll(m);
-    };
-    for (int c0i = 0; c0i < S.n_clu; c0i += 64) {
-        const int cl = c0i + lane;
-        float4 q0 = make_float4(0.f, 0.f, 0.f, 1.f), q1 = make_float4(INFINITY, 0.f, 0.f, 0.f);
-        if (cl < S.n_clu) {
-            q0 = S.clu_cam[2 * cl];
-            q1 = S.clu_cam[2 * cl + 1];
-        }
-        const int id = __float_as_int(q1.y);
-        unsigned long long cm = __ballot(cone_overlap(wc, q0, q1.w, 0.0f, 4e-6f));
-        while (cm) {
-            const int b = (int)__builtin_ctzll(cm);
-            cm &= cm - 1;
-            batch(64 * __builtin_amdgcn_readlane(id, b));
+        if (n) {
+            rec[wv][lane][0] = c0;
+            rec[wv][lane][1] = S.cone_cam[2 * k + 1];
+            const float4* e = S.cone_cam + 2 * (size_t)S.n_tri + 3 * (size_t)k;
+            rec[wv][lane][2] = e[0];
+            rec[wv][lane][3] = e[1];
+            rec[wv][lane][4] = e[2];
+            box[wv][lane][0] = b.tx0;
+            box[wv][lane][1] = b.ty0;
+            box[wv][lane][2] = b.nx;
         }
     }
-    return n;
+    // inclusive prefix of the box sizes over the wave
+    unsigned v = n;
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned u = __shfl_up(v, o);
+        if (lane >= o) v += u;
+    }
+    incl[wv][lane] = v;
+    const unsigned total = (unsigned)__shfl(v, 63);
+    wave_lds_sync();
+    if (!FILL && lane == 0 && total) atomicAdd(&B.stat[1], total);
+    for (unsigned p0 = 0; p0 < total; p0 += 64) {
+        const unsigned p = p0 + (unsigned)lane;
+        if (p >= total) break;
+        int lo = 0, hi = 63;  // the first owner with incl > p
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (incl[wv][mid] > p)
+                hi = mid;
+            else
+                lo = mid + 1;
+        }
+        const unsigned q = p - (lo ? incl[wv][lo - 1] : 0u);
+        const int nx = box[wv][lo][2];
+        const int t = (box[wv][lo][1] + (int)(q / (unsigned)nx)) * B.tiles_x + box[wv][lo][0] + (int)(q % (unsigned)nx);
+        if (B.flag[t]) continue;
+        const float4 c0 = rec[wv][lo][0], c1 = rec[wv][lo][1];
+        if (cb_pair_test(B, t, c0, c1.w, &rec[wv][lo][2]))
+            cb_emit<FILL>(B, t, (int)((blockIdx.x * 4 + wv) * 64) + lo, c1.x);
+    }
 }
 
-// BLK = tiles per block edge: 8 at 4K and above, 4 below (a tile of a
-// 1080p frame spans 4x the angle of one at 7680 wide).
-template <bool FILL, int BLK>
-__global__ __launch_bounds__(256) void rt_cb_block(const SceneDev S, const FrameDev F, const unsigned* __restrict__ off,
-                                                   unsigned* __restrict__ cnt, unsigned* __restrict__ flag,
-                                                   int2* __restrict__ ent, unsigned* __restrict__ bstat)
+// The deferred (big) boxes, by the whole grid: every thread takes pairs
+// g, g + G, ... of each deferred triangle in turn.
+template <bool FILL>
+__global__ __launch_bounds__(256) void rt_cb_bin_big(const SceneDev S, const FrameDev F, CbDev B)
 {
-    constexpr int NT = BLK * BLK;
-    __shared__ float4 tcone[NT * 2];  // [w, cosW] [sinW, chord, ok, present]
-    __shared__ int lid[kCbBlockCap];
-    __shared__ float4 lrec[kCbBlockCap * kConeRec];
-    __shared__ int bstate[2];         // list length, use the list (0/1)
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int tiles_y = (F.height + 7) / 8;
-    const int bx0 = blockIdx.x * BLK, by0 = blockIdx.y * BLK;
-    // 1. the 64 tile cones (16 per wave), exactly as rt_cb_build computes them
-    for (int j = 0; j < NT / 4; ++j) {
-        const int lt = wave * (NT / 4) + j;
-        const int tx = bx0 + (lt % BLK), ty = by0 + (lt / BLK);
-        const bool inside = tx < S.cb_tiles_x && ty < tiles_y;
-        const bool present = inside && cb_tile_row_needed(F, ty);
-        if (inside && !present && lane == 0 && !FILL) {  // outside the frame's rows: no list
-            flag[ty * S.cb_tiles_x + tx] = 1u;
-            cnt[ty * S.cb_tiles_x + tx] = 0u;
-        }
-        WaveCone wc;
-        wc.ok = false;
-        if (present) {
-            const int px = tx * 8 + (lane & 7), py = ty * 8 + (lane >> 3);
-            const Vec3 D = camera_dir(F, px < F.width ? px : F.width - 1, py < F.height ? py : F.height - 1);
-            wc = wave_cone(D, true);
-        }
-        if (lane == 0) {
-            tcone[2 * lt] = make_float4(wc.w.x, wc.w.y, wc.w.z, wc.cosW);
-            tcone[2 * lt + 1] = make_float4(wc.sinW, wc.chord, wc.ok ? 1.f : 0.f, present ? 1.f : 0.f);
-        }
-    }
-    __syncthreads();
-    // 2. the block cone (wave 0, lane t = tile t, in double) and its list
-    if (wave == 0) {
-        const float4 a = tcone[2 * (lane % NT)], b = tcone[2 * (lane % NT) + 1];
-        const bool present = lane < NT && b.w != 0.f, ok = b.z != 0.f;
-        bool use = !__any(present & !ok) && __any(present);
-        const double wx = present ? (double)a.x : 0.0, wy = present ? (double)a.y : 0.0,
-                     wz = present ? (double)a.z : 0.0;
-        const double sx = wave_sum_d(wx), sy = wave_sum_d(wy), sz = wave_sum_d(wz);
-        const double sn = sqrt(sx * sx + sy * sy + sz * sz);
-        use = use && sn > 0.0;
-        WaveCone bc;
-        bc.ok = false;
-        float Mb = 0.f, Eb = 0.f;
-        if (use) {
-            // the float axis the tests use, and each tile's angle to it
-            bc.w = make3((float)(sx / sn), (float)(sy / sn), (float)(sz / sn));
-            const double bn = sqrt((double)bc.w.x * bc.w.x + (double)bc.w.y * bc.w.y + (double)bc.w.z * bc.w.z);
-            const double ux = bc.w.x / bn, uy = bc.w.y / bn, uz = bc.w.z / bn;
-            double al = 0.0, wt = 0.0, ch = 0.0;
-            if (present) {
-                const double tn = sqrt((double)a.x * a.x + (double)a.y * a.y + (double)a.z * a.z);
-                const double vx = a.x / tn, vy = a.y / tn, vz = a.z / tn;
-                const double cx = uy * vz - uz * vy, cy = uz * vx - ux * vz, cz = ux * vy - uy * vx;
-                // angle between the unit axes, plus the float axes' length slack
-                al = atan2(sqrt(cx * cx + cy * cy + cz * cz), ux * vx + uy * vy + uz * vz) + 1e-6 +
-                     fabs(tn - 1.0) + fabs(bn - 1.0);
-                wt = acos(fmin(1.0, (double)a.w)) + al;
-                ch = 2.0 * sin(0.5 * al) + fabs(tn - 1.0) + fabs(bn - 1.0) + (double)b.y;
-            }
-            const double Wb = wave_max_d(wt) * (1.0 + 1e-12) + 1e-9, amax = wave_max_d(al), Emax = wave_max_d(ch);
-            const double m = 5e-6, delta = 2.0 * asin(sqrt(0.5 * m));
-            double cb = cos(Wb), sb = sin(Wb);
-            float cf = (float)cb;
-            if ((double)cf > cb) cf = nextafterf(cf, -INFINITY);
-            float sf = (float)sb;
-            if ((double)sf < sb) sf = nextafterf(sf, INFINITY);
-            bc.cosW = cf;
-            bc.sinW = sf;
-            bc.chord = 0.f;
-            bc.ok = Wb < 1.0 && cf >= 0.5f;
-            Mb = (float)((m + delta * sin(fmin(amax, 1.5)) + 1e-6) * (1.0 + 1e-6));
-            Eb = (float)((Emax + 2e-6 + 1e-6) * (1.0 + 1e-6));
-            use = bc.ok;
-        }
-        unsigned n = 0;
-        if (use) {
-            const unsigned long long below = (1ull << lane) - 1ull;
-            const float Mc = Mb + 2e-6f;
-            for (int c0i = 0; c0i < S.n_clu; c0i += 64) {
-                const int cl = c0i + lane;
-                float4 q0 = make_float4(0.f, 0.f, 0.f, 1.f), q1 = make_float4(INFINITY, 0.f, 0.f, 0.f);
-                if (cl < S.n_clu) {
-                    q0 = S.clu_cam[2 * cl];
-                    q1 = S.clu_cam[2 * cl + 1];
-                }
-                const int id = __float_as_int(q1.y);
-                unsigned long long cm = __ballot((cl < S.n_clu) & cone_overlap(bc, q0, q1.w, 0.0f, Mc));
-                while (cm) {
-                    const int bb = (int)__builtin_ctzll(cm);
-                    cm &= cm - 1;
-                    const int k = 64 * __builtin_amdgcn_readlane(id, bb) + lane;
-                    bool reach = false;
-                    float4 c0, c1, e0, e1, e2;
-                    if (k < S.n_tri) {
-                        c0 = S.cone_cam[2 * k];
-                        c1 = S.cone_cam[2 * k + 1];
-                        const float4* e = S.cone_cam + 2 * (size_t)S.n_tri + 3 * k;
-                        e0 = e[0];
-                        e1 = e[1];
-                        e2 = e[2];
-                        reach = cone_overlap(bc, c0, c1.w, 0.0f, Mb) &&
-                                !(dot(bc.w, make3(e0.x, e0.y, e0.z)) + Eb < e0.w) &&
-                                !(dot(bc.w, make3(e1.x, e1.y, e1.z)) + Eb < e1.w) &&
-                                !(dot(bc.w, make3(e2.x, e2.y, e2.z)) + Eb < e2.w);
-                    }
-                    const unsigned long long mm = __ballot(reach);
-                    const unsigned pos = n + (unsigned)__popcll(mm & below);
-                    if (reach && pos < (unsigned)kCbBlockCap) {
-                        lid[pos] = k;
-                        float4* r = lrec + kConeRec * pos;
-                        r[0] = c0;
-                        r[1] = c1;
-                        r[2] = e0;
-                        r[3] = e1;
-                        r[4] = e2;
-                    }
-                    n += (unsigned)__popcll(mm);
-                }
-            }
-            use = n <= (unsigned)kCbBlockCap;
-        }
-        if (lane == 0) {
-            bstate[0] = (int)n;
-            bstate[1] = use ? 1 : 0;
-            if (!FILL && bstat) {
-                atomicAdd(bstat, 1u);
-                if (!use) atomicAdd(bstat + 1, 1u);
-                atomicAdd(bstat + 2, use ? n : 0u);
-            }
-        }
-    }
-    __syncthreads();
-    // 3. every tile against the block list (or its own walk)
-    const bool use = bstate[1] != 0;
-    const unsigned nl = (unsigned)bstate[0];
-    const unsigned long long below = (1ull << lane) - 1ull;
-    for (int j = 0; j < NT / 4; ++j) {
-        const int lt = wave * (NT / 4) + j;
-        const float4 a = tcone[2 * lt], b = tcone[2 * lt + 1];
-        if (b.w == 0.f) continue;  // outside the frame
-        const int tx = bx0 + (lt % BLK), ty = by0 + (lt / BLK);
-        const int tile = ty * S.cb_tiles_x + tx;
-        WaveCone wc;
-        wc.w = make3(a.x, a.y, a.z);
-        wc.cosW = a.w;
-        wc.sinW = b.x;
-        wc.chord = b.y;
-        wc.ok = b.z != 0.f;
-        if (!wc.ok) {  // no list: the trace kernel's per-wave path
-            if (!FILL && lane == 0) {
-                flag[tile] = 1u;
-                cnt[tile] = 0u;
-            }
-            continue;
-        }
-        const unsigned base = FILL ? off[tile] : 0u;
-        unsigned n = 0;
-        if (use) {
-            for (unsigned q0 = 0; q0 < nl; q0 += 64) {
-                const unsigned q = q0 + (unsigned)lane;
-                bool reach = false;
-                float dmin = 0.0f;
-                int k = 0;
-                if (q < nl) {
-                    const float4* r = lrec + kConeRec * q;
-                    const float4 c0 = r[0], c1 = r[1];
-                    k = lid[q];
-                    dmin = c1.x;
-                    reach = cone_overlap(wc, c0, c1.w, 0.0f) && edges_open(wc, r + 2, 0.0f);
-                }
-                const unsigned long long m = __ballot(reach);
-                if (FILL && reach) ent[base + n + (unsigned)__popcll(m & below)] = make_int2(k, __float_as_int(dmin));
-                n += (unsigned)__popcll(m);
-            }
-        } else {
-            n = cb_tile_walk<FILL>(S, wc, base, ent);
-        }
-        if (!FILL && lane == 0) {
-            cnt[tile] = n;
-            flag[tile] = 0u;
+    const unsigned nbig = min(B.stat[0], (unsigned)S.n_tri);
+    const unsigned G = gridDim.x * blockDim.x, g = blockIdx.x * blockDim.x + threadIdx.x;
+    for (unsigned i = 0; i < nbig; ++i) {
+        const int k = B.big[i];
+        const float4 c0 = S.cone_cam[2 * k], c1 = S.cone_cam[2 * k + 1];
+        const float4* e = S.cone_cam + 2 * (size_t)S.n_tri + 3 * (size_t)k;
+        const float4 e3[3] = {e[0], e[1], e[2]};
+        const CbBox b = cb_box(c0, F, B);
+        const unsigned n = (unsigned)(b.nx * b.ny);
+        if (!FILL && g == 0) atomicAdd(&B.stat[1], n);
+        for (unsigned q = g; q < n; q += G) {
+            const int t = (b.ty0 + (int)(q / (unsigned)b.nx)) * B.tiles_x + b.tx0 + (int)(q % (unsigned)b.nx);
+            if (B.flag[t]) continue;
+            if (cb_pair_test(B, t, c0, c1.w, e3)) cb_emit<FILL>(B, t, k, c1.x);
         }
     }
 }
 
-// Keys: entry e's key = min dmin over entries [e, end) of its tile (one
-// thread per tile), so a wave may stop at the first key beyond its hits.
-// Lists of up to RT_CB_SORT entries are first sorted nearest-first (the
-// closest hit is order-free: lexicographic (t, index)), so the keys rise
-// with the walk and the exit comes at the first entry beyond every lane's
-// hit; longer lists keep cluster order.
+// Keys: entry e's key = min dmin over entries [e, end) of its tile, so a
+// wave may stop at the first key beyond its hits.  Lists of up to
+// RT_CB_SORT entries are first sorted nearest-first (the closest hit is
+// order-free: lexicographic (t, index)), so the keys rise with the walk and
+// the exit comes at the first entry beyond every lane's hit.
 #ifndef RT_CB_SORT
 #define RT_CB_SORT 256
 #endif
@@ -380,46 +309,20 @@ __device__ __forceinline__ float cb_dmin(int2 en)
     const float d = __int_as_float(en.y);
     return d == d ? d : -INFINITY;
 }
-__global__ void rt_cb_keys(const unsigned* __restrict__ off, int ntiles, int2* __restrict__ ent)
-{
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= ntiles) return;
-    const unsigned b = off[t], n = off[t + 1] - off[t];
-    if (n <= RT_CB_SORT) {  // insertion sort by (dmin, triangle)
-        for (unsigned i = 1; i < n; ++i) {
-            const int2 x = ent[b + i];
-            const float dx = cb_dmin(x);
-            unsigned j = i;
-            while (j > 0) {
-                const int2 y = ent[b + j - 1];
-                const float dy = cb_dmin(y);
-                if (dy < dx || (dy == dx && y.x < x.x)) break;
-                ent[b + j] = y;
-                --j;
-            }
-            ent[b + j] = x;
-        }
-    }
-    float m = INFINITY;
-    for (unsigned e = off[t + 1]; e > off[t]; --e) {
-        const float d = __int_as_float(ent[e - 1].y);
-        m = d == d ? fminf(m, d) : -INFINITY;
-        ent[e - 1].y = __float_as_int(m);
-    }
-}
 
-// The same keys, one wave per tile: a list of up to RT_CB_SORT (256)
-// entries is held in registers (4 per lane) and every entry's final place is
-// its rank under (dmin, triangle) — the order rt_cb_keys' insertion sort
-// produces, the pairs being distinct; once sorted, the suffix minimum of
-// entry e is its own dmin (NaN dmins sort first as -inf and key -inf).
-// Longer lists keep cluster order and get their suffix minima from lane 0.
-__global__ __launch_bounds__(256) void rt_cb_keys_wave(const unsigned* __restrict__ off, int ntiles,
-                                                       int2* __restrict__ ent)
+// One wave per tile: a list of up to RT_CB_SORT (256) entries is held in
+// registers (4 per lane) and every entry's final place is its rank under
+// (dmin, triangle) — the pairs are distinct; once sorted, the suffix minimum
+// of entry e is its own dmin (NaN dmins sort first as -inf and key -inf).
+// Longer lists are sorted in LDS by rt_cb_keys_long; flagged tiles (no list,
+// or overflowed) are skipped.
+__global__ __launch_bounds__(256) void rt_cb_keys_wave(const CbDev B, int ntiles)
 {
+    const unsigned* __restrict__ off = B.off;
+    int2* __restrict__ ent = B.ent;
     const int lane = threadIdx.x & 63;
     const int t = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
-    if (t >= ntiles) return;
+    if (t >= ntiles || B.flag[t]) return;
     const unsigned b = off[t], n = off[t + 1] - off[t];
     if (n <= 1) {
         if (n == 1 && lane == 0) ent[b].y = __float_as_int(cb_dmin(ent[b]));
@@ -427,12 +330,8 @@ __global__ __launch_bounds__(256) void rt_cb_keys_wave(const unsigned* __restric
     }
     if (n > RT_CB_SORT) {
         if (lane == 0) {
-            float m = INFINITY;
-            for (unsigned e = off[t + 1]; e > off[t]; --e) {
-                const float d = __int_as_float(ent[e - 1].y);
-                m = d == d ? fminf(m, d) : -INFINITY;
-                ent[e - 1].y = __float_as_int(m);
-            }
+            B.lng[atomicAdd(&B.stat[3], 1u)] = t;
+            atomicMax(&B.stat[4], n);
         }
         return;
     }
@@ -467,13 +366,80 @@ __global__ __launch_bounds__(256) void rt_cb_keys_wave(const unsigned* __restric
         if ((unsigned)(lane + 64 * q) < n) ent[b + rk[q]] = make_int2(id[q], __float_as_int(kd[q]));
 }
 
+// Lists longer than RT_CB_SORT (their tiles listed by rt_cb_keys_wave):
+// one workgroup per such tile sorts the list by (dmin, triangle) with a
+// bitonic sort in LDS (up to kCbLongCap entries; a longer list keeps its fill
+// order with suffix-minimum keys — exact, the early exit only later).  A
+// fixed grid walks the listed tiles (the host does not know how many).
+constexpr int kCbLongCap = 4096;
+__global__ __launch_bounds__(1024) void rt_cb_keys_long(const CbDev B)
+{
+    __shared__ unsigned long long sk[kCbLongCap];  // (dmin order bits << 32) | triangle
+    const unsigned* __restrict__ off = B.off;
+    int2* __restrict__ ent = B.ent;
+    const unsigned nlong = B.stat[3];
+    for (unsigned i = blockIdx.x; i < nlong; i += gridDim.x) {
+        const int t = B.lng[i];
+        const unsigned b = off[t], n = off[t + 1] - b;
+        if (n > (unsigned)kCbLongCap) {
+            if (threadIdx.x == 0) {
+                float m = INFINITY;
+                for (unsigned e = b + n; e > b; --e) {
+                    const float d = __int_as_float(ent[e - 1].y);
+                    m = d == d ? fminf(m, d) : -INFINITY;
+                    ent[e - 1].y = __float_as_int(m);
+                }
+            }
+            continue;
+        }
+        unsigned P = 1;
+        while (P < n) P <<= 1;
+        for (unsigned i = threadIdx.x; i < P; i += blockDim.x) {
+            unsigned long long key = ~0ull;
+            if (i < n) {
+                const int2 e = ent[b + i];
+                // order-preserving bits of the float key (NaN as -inf)
+                unsigned u = __float_as_uint(cb_dmin(e));
+                u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+                key = ((unsigned long long)u << 32) | (unsigned)e.x;
+            }
+            sk[i] = key;
+        }
+        __syncthreads();
+        for (unsigned kk = 2; kk <= P; kk <<= 1) {
+            for (unsigned j = kk >> 1; j > 0; j >>= 1) {
+                for (unsigned i = threadIdx.x; i < P; i += blockDim.x) {
+                    const unsigned l = i ^ j;
+                    if (l > i) {
+                        const unsigned long long x = sk[i], y = sk[l];
+                        const bool up = (i & kk) == 0;
+                        if ((x > y) == up) {
+                            sk[i] = y;
+                            sk[l] = x;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        for (unsigned i = threadIdx.x; i < n; i += blockDim.x) {
+            const unsigned long long key = sk[i];
+            unsigned u = (unsigned)(key >> 32);
+            u = (u & 0x80000000u) ? (u & 0x7fffffffu) : ~u;
+            ent[b + i] = make_int2((int)(unsigned)key, (int)u);
+        }
+        __syncthreads();
+    }
+}
+
 // The walk's records: entry e = the tricam record of its triangle, key in
-// [3].z (tricam's [3] = [e2 . Q, file index, 0, 0]).  One thread per entry.
-__global__ void rt_cb_expand(const int2* __restrict__ ent, unsigned n, const float4* __restrict__ tricam,
-                             float4* __restrict__ rec)
+// [3].z (tricam's [3] = [e2 . Q, file index, 0, 0]).  One thread per entry
+// of the capacity; entries past the build's total are left alone.
+__global__ void rt_cb_expand(const int2* __restrict__ ent, const unsigned long long* __restrict__ total,
+                             unsigned cap, const float4* __restrict__ tricam, float4* __restrict__ rec)
 {
     const unsigned e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= n) return;
+    if (e >= cap || (unsigned long long)e >= *total) return;
     const int2 en = ent[e];
     const float4* t = tricam + 4 * (size_t)en.x;
     float4* o = rec + 4 * (size_t)e;
@@ -483,6 +449,54 @@ __global__ void rt_cb_expand(const int2* __restrict__ ent, unsigned n, const flo
     float4 d = t[3];
     d.z = __int_as_float(en.y);
     o[3] = d;
+}
+
+// Diagnostic (rt_debug_cb_verify): a built camera buffer against brute
+// force — every tile with a list against every triangle.  A tile is bad
+// unless its list holds exactly the triangles whose camera wave test passes
+// (as many entries as passing triangles, every entry passing: the binning
+// never emits a pair twice), keyed by its own dmin, keys non-decreasing for
+// sorted lists.  out[0] += bad tiles, out[1] += passing pairs.
+__global__ __launch_bounds__(256) void rt_cb_verify(const SceneDev S, const CbDev B, unsigned* __restrict__ out)
+{
+    const int lane = (int)(threadIdx.x & 63);
+    const int t = (int)(blockIdx.x * 4 + (threadIdx.x >> 6));
+    if (t >= B.tiles_x * B.tiles_y || B.flag[t]) return;
+    unsigned n = 0;
+    for (int k0 = 0; k0 < S.n_tri; k0 += 64) {
+        const int k = k0 + lane;
+        bool pass = false;
+        if (k < S.n_tri)
+            pass = cb_pair_test(B, t, S.cone_cam[2 * k], S.cone_cam[2 * k + 1].w,
+                                S.cone_cam + 2 * (size_t)S.n_tri + 3 * (size_t)k);
+        n += (unsigned)__popcll(__ballot(pass));
+    }
+    const unsigned b = B.off[t], m = B.off[t + 1] - b;
+    bool bad = m != n;
+    for (unsigned i0 = 0; i0 < m; i0 += 64) {
+        const unsigned i = i0 + (unsigned)lane;
+        bool wrong = false;
+        if (i < m) {
+            const int2 e = B.ent[b + i];
+            if (e.x < 0 || e.x >= S.n_tri) {
+                wrong = true;
+            } else {
+                const float4 c1 = S.cone_cam[2 * e.x + 1];
+                wrong = !cb_pair_test(B, t, S.cone_cam[2 * e.x], c1.w,
+                                      S.cone_cam + 2 * (size_t)S.n_tri + 3 * (size_t)e.x);
+                const float d = cb_dmin(make_int2(0, __float_as_int(c1.x)));
+                if (m <= (unsigned)kCbLongCap) {
+                    wrong |= __float_as_int(d) != e.y;
+                    if (i + 1 < m) wrong |= !(__int_as_float(e.y) <= __int_as_float(B.ent[b + i + 1].y));
+                }
+            }
+        }
+        bad |= __any(wrong);
+    }
+    if (lane == 0) {
+        atomicAdd(&out[1], n);
+        if (bad) atomicAdd(&out[0], 1u);
+    }
 }
 
 }  // namespace rt

@@ -440,39 +440,52 @@ struct rt_ctx {
     float4* d_clu_light = nullptr;
     int n_clu = 0;
     float4* d_uni = nullptr;  // union records (small lists): camera, then one per light
+    // A camera buffer (rt_cambuf.h): per-tile lists for the camera of key,
+    // built on the stream that needs it; the entry array's capacity comes
+    // from the totals of earlier builds, read back without a host sync
+    // (h_tot after ev_tot), and grows when a build needed more.
+    struct CamBuf {
+        float4* tcone = nullptr;
+        unsigned* off = nullptr;
+        unsigned* cur = nullptr;
+        unsigned* flag = nullptr;
+        int* big = nullptr;
+        int* lng = nullptr;
+        unsigned* stat = nullptr;
+        void* scan = nullptr;
+        int2* ent = nullptr;
+        float4* rec = nullptr;      // inline records (RT_OPT_CB_INLINE_MAX_MB)
+        size_t cap = 0, rec_cap = 0, scan_words = 0;
+        int nt_alloc = 0, big_alloc = 0;
+        unsigned long long* h_tot = nullptr;  // pinned: [total][stat words 0..7 as 4 u64]
+        hipEvent_t ev_tot = nullptr, ev0 = nullptr, ev1 = nullptr;
+        bool tot_pending = false;   // h_tot written by an enqueued copy not yet seen
+        size_t observed = 0;        // largest total read back
+        size_t entries = 0;         // last total read back
+        unsigned hstat[8] = {};     // last stat words read back
+        bool inline_rec = false;    // rec holds the current records
+        int tiles_x = 0, ntiles = 0;
+        float key[30] = {};
+        bool valid = false;
+        double host_ms = 0.0, build_ms = 0.0;
+        bool timed = false;
+    };
+    CamBuf cb;
     // Camera state of rt_render_sequence_async: kSeqSlots slots of the
-    // per-camera records, apart from the state above; frame i of a sequence
-    // uses slot i % kSeqSlots on internal stream i % kSeqSlots, so up to
-    // kSeqSlots consecutive frames (different cameras) are in flight at once.
+    // per-camera records and camera buffers, apart from the state above;
+    // frame i of a sequence uses slot i % kSeqSlots on internal stream
+    // i % kSeqSlots, so up to kSeqSlots consecutive frames (different
+    // cameras) are in flight at once.
     struct CamSlot {
         float4 *tricam = nullptr, *cone_cam = nullptr, *clu_cam = nullptr, *uni = nullptr;
+        CamBuf cb;
     } seq[kSeqSlots];
     hipStream_t seq_streams[kSeqSlots] = {};
     hipEvent_t seq_fork = nullptr, seq_join[kSeqSlots] = {};
-    // camera buffer (rt_cb_build): per-tile lists for the camera of cb_key
-    unsigned* d_cb_off = nullptr;
-    unsigned* d_cb_flag = nullptr;
-    int2* d_cb_ent = nullptr;
-    float4* d_cb_rec = nullptr;  // 4 x float4 per entry (rt_cb_expand)
-    bool cb_inline = false;      // d_cb_rec holds the current records
-    size_t cb_cap = 0;          // entries allocated
-    size_t cb_rec_cap = 0;      // inline records allocated (entries)
-    hipEvent_t ev_cb0 = nullptr, ev_cb1 = nullptr;  // around the last build's device work
-    double cb_host_ms = 0.0;
-    bool cb_timed = false;
-    unsigned* d_cb_bstat = nullptr;  // block pre-cull: blocks, blocks walked per tile, staged members
-    bool cb_blocks = false;     // the last build used rt_cb_block
-    void* d_scan = nullptr;     // u64 scratch of the build scans
+    std::vector<void*> deferred;  // replaced buffers an enqueued render may read: freed at the next host sync
+    void* d_scan = nullptr;     // u64 scratch of the light-buffer build scans
     size_t scan_words = 0;
     unsigned long long* h_word = nullptr;  // pinned: totals read back by the builds
-    int cb_tiles_x = 0, cb_ntiles = 0;
-    // cam_pos, orient, half_w, half_h, inv_w, inv_h, width, height, and the
-    // tile rows the lists were built for: row_begin, row_end, band_rows,
-    // band_count, band_index (ints as float bits)
-    float cb_key[30] = {};
-    bool cb_valid = false;
-    double cb_build_ms = 0.0;
-    size_t cb_entries = 0;
     // light buffer (shadow cells), rt_lb_build
     unsigned* d_lb_off = nullptr;
     float4* d_lb_ent = nullptr;
@@ -510,6 +523,7 @@ struct rt_ctx {
     double opt_dcov_near = 0.0;
     double opt_cb_inline_mb = 0.0;
     double opt_host_chunk_mb = 8.0;
+    double opt_cb_capacity = 0.0;  // camera-buffer entries; 0 = automatic
     std::vector<double> far_ladder;       // big lists' far light buffers
     double upload_parts_ms[4] = {0, 0, 0, 0};  // copy+records, prepasses, light buffer, total
     double lb_parts_ms[5] = {0, 0, 0, 0, 0};    // lb_build phases (rt_debug_upload_info out[4..8])
@@ -522,6 +536,8 @@ struct rt_ctx {
     rt_stats last{};
     std::string err;
 };
+
+static void cb_free(rt_ctx::CamBuf& B);
 
 #define RT_EXPORT extern "C" __attribute__((visibility("default")))
 
@@ -560,11 +576,8 @@ RT_EXPORT int rt_create(int32_t dev, rt_ctx** out)
     HIP_TRY(c, hipEventCreateWithFlags(&c->ev_state, hipEventDisableTiming));
     HIP_TRY(c, hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
     for (hipEvent_t& e : c->ev_chunk) HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    HIP_TRY(c, hipEventCreate(&c->ev_cb0));
-    HIP_TRY(c, hipEventCreate(&c->ev_cb1));
     HIP_TRY(c, hipHostMalloc((void**)&c->h_word, 2 * sizeof(unsigned long long), hipHostMallocDefault));
     HIP_TRY(c, hipMalloc(&c->d_stats, kStatSlots * sizeof(StatsDev)));
-    HIP_TRY(c, hipMalloc(&c->d_cb_bstat, 4 * sizeof(unsigned)));
     c->far_ladder = {2.5, 6.0, 16.0, 64.0};
     return RT_OK;
 }
@@ -614,6 +627,16 @@ static void note_async(rt_ctx* c, hipStream_t s)
         c->async_streams.push_back(s);
 }
 
+// Buffers replaced while renders that read them may still have been in
+// flight (free_later): after a host sync of everything nothing reads them.
+// The internal sequence streams are joined into the caller's stream, which
+// is one of the synced async streams.
+static void free_deferred(rt_ctx* c)
+{
+    for (void* p : c->deferred) hipFree(p);
+    c->deferred.clear();
+}
+
 // Host sync of everything the context enqueued: afterwards no async render
 // or state write is in flight.
 static int sync_all(rt_ctx* c)
@@ -624,6 +647,7 @@ static int sync_all(rt_ctx* c)
     c->async_streams.clear();
     c->state_pending = false;
     c->state_stream = nullptr;
+    free_deferred(c);
     return RT_OK;
 }
 
@@ -669,12 +693,17 @@ RT_EXPORT int rt_set_option(rt_ctx* c, int32_t opt, double v)
     case RT_OPT_CB_INLINE_MAX_MB:
         if (v < 0) return RT_E_ARG;
         // the layout is chosen at a camera-buffer build: rebuild at the next render
-        if (v != c->opt_cb_inline_mb) c->cb_valid = false;
+        if (v != c->opt_cb_inline_mb) c->cb.valid = false;
         c->opt_cb_inline_mb = v;
         return RT_OK;
     case RT_OPT_HOST_CHUNK_MB:
         if (v < 0) return RT_E_ARG;
         c->opt_host_chunk_mb = v;
+        return RT_OK;
+    case RT_OPT_CB_CAPACITY:
+        if (v < 0 || v > 4e9 || v != std::floor(v)) return RT_E_ARG;
+        if (v != c->opt_cb_capacity) c->cb.valid = false;
+        c->opt_cb_capacity = v;
         return RT_OK;
     default: return RT_E_ARG;
     }
@@ -691,6 +720,7 @@ RT_EXPORT int rt_get_option(rt_ctx* c, int32_t opt, double* v)
     case RT_OPT_DCOV_NEAR: *v = c->opt_dcov_near; return RT_OK;
     case RT_OPT_CB_INLINE_MAX_MB: *v = c->opt_cb_inline_mb; return RT_OK;
     case RT_OPT_HOST_CHUNK_MB: *v = c->opt_host_chunk_mb; return RT_OK;
+    case RT_OPT_CB_CAPACITY: *v = c->opt_cb_capacity; return RT_OK;
     default: return RT_E_ARG;
     }
 }
@@ -761,15 +791,13 @@ RT_EXPORT void rt_destroy(rt_ctx* c)
     hipFree(c->d_lb_dcap);
     hipFree(c->d_lb_meta);
     hipFree(c->d_uni);
-    hipFree(c->d_cb_off);
-    hipFree(c->d_cb_flag);
-    hipFree(c->d_cb_ent);
-    hipFree(c->d_cb_rec);
+    cb_free(c->cb);
     for (auto& q : c->seq) {
         hipFree(q.tricam);
         hipFree(q.cone_cam);
         hipFree(q.clu_cam);
         hipFree(q.uni);
+        cb_free(q.cb);
     }
     hipFree(c->d_stats);
     hipFree(c->d_scratch);
@@ -785,11 +813,8 @@ RT_EXPORT void rt_destroy(rt_ctx* c)
         if (c->seq_join[j]) hipEventDestroy(c->seq_join[j]);
     }
     if (c->seq_fork) hipEventDestroy(c->seq_fork);
-    if (c->ev_cb0) hipEventDestroy(c->ev_cb0);
-    if (c->ev_cb1) hipEventDestroy(c->ev_cb1);
     if (c->h_word) hipHostFree(c->h_word);
     hipFree(c->d_scan);
-    hipFree(c->d_cb_bstat);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
 }
@@ -1287,7 +1312,7 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
     c->lb_entries = 0;
     hipFree(c->d_uni);
     c->d_uni = nullptr;
-    c->cb_valid = false;  // buffers are kept (reallocated on demand)
+    c->cb.valid = false;  // buffers are kept (reallocated on demand)
     c->cam_valid = false;
     c->lb_build_ms = 0.0;
     c->d_geom = c->d_mat = c->d_lights = c->d_tri = c->d_plane = c->d_quad = nullptr;
@@ -1390,9 +1415,9 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
         HIP_TRY(c, hipMalloc((void**)&c->d_clu_cam, (size_t)c->n_clu * 4 * sizeof(float4)));
         HIP_TRY(c, hipMalloc((void**)&c->d_clu_light, std::max<size_t>((size_t)c->n_clu * nl, 1) * 2 * sizeof(float4)));
         for (int j = 0; j < nl; ++j) {
-            hipLaunchKernelGGL(rt_cluster_prepass, dim3((unsigned)((c->n_clu + 63) / 64)), dim3(64), 0, st,
+            hipLaunchKernelGGL(rt_cluster_prepass, dim3(cluster_blocks(c->n_clu)), dim3(256), 0, st,
                                c->d_cone_light + kConeRec * ntr * j, (int)ntr, c->n_clu,
-                               c->d_clu_light + 2 * (size_t)c->n_clu * j);
+                               c->d_clu_light + 2 * (size_t)c->n_clu * j, 64);
             HIP_TRY(c, hipGetLastError());
         }
     }
@@ -1401,7 +1426,7 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
         HIP_TRY(c, hipMalloc((void**)&c->d_uni, (size_t)(nl + 1) * 2 * sizeof(float4)));
         for (int j = 0; j < nl && n_tri_o > 0; ++j) {
             hipLaunchKernelGGL(rt_cluster_prepass, dim3(1), dim3(64), 0, st, c->d_cone_light + kConeRec * ntr * j,
-                               n_tri_o, 1, c->d_uni + 2 * (1 + (size_t)j), n_tri_o);
+                               n_tri_o, 1, c->d_uni + 2 * (1 + (size_t)j), n_tri_o);  // one wave
             HIP_TRY(c, hipGetLastError());
         }
         if (n_tri_o == 0) {  // no opaque triangle: nothing for shadow rays to walk ("never" record)
@@ -1421,9 +1446,13 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
         hipFree(q.cone_cam);
         hipFree(q.clu_cam);
         hipFree(q.uni);
+        const rt_ctx::CamBuf keep = q.cb;  // its buffers are kept (resized on demand)
         q = rt_ctx::CamSlot{};
+        q.cb = keep;
+        q.cb.valid = false;
         if (ntr == 0) continue;
-        HIP_TRY(c, hipMalloc((void**)&q.tricam, (ntr <= (size_t)kTricamMaxTriangles ? ntr : 1) * 4 * sizeof(float4)));
+        // every triangle's camera record: the camera-buffer walk reads them
+        HIP_TRY(c, hipMalloc((void**)&q.tricam, ntr * 4 * sizeof(float4)));
         HIP_TRY(c, hipMalloc((void**)&q.cone_cam, ntr * kConeRec * sizeof(float4)));
         if (c->n_clu > 0) HIP_TRY(c, hipMalloc((void**)&q.clu_cam, (size_t)c->n_clu * 4 * sizeof(float4)));
         if (c->d_uni) {
@@ -1651,15 +1680,15 @@ static int camera_records(rt_ctx* c, const float* cp, hipStream_t st, bool all_t
                        c->d_trinrm, c->d_tricoef, c->n_tri, cp[0], cp[1], cp[2], 1, 0.0f, cone_cam);
     HIP_TRY(c, hipGetLastError());
     if (uni) {
-        hipLaunchKernelGGL(rt_cluster_prepass, dim3(1), dim3(64), 0, st, cone_cam, c->n_tri, 1, uni, c->n_tri);
+        hipLaunchKernelGGL(rt_cluster_prepass, dim3(1), dim3(64), 0, st, cone_cam, c->n_tri, 1, uni, c->n_tri);  // one wave
         HIP_TRY(c, hipGetLastError());
     }
     if (c->n_clu > 0) {
         float4* tmp = clu_cam + 2 * (size_t)c->n_clu;  // second half: unsorted
-        hipLaunchKernelGGL(rt_cluster_prepass, dim3((unsigned)((c->n_clu + 63) / 64)), dim3(64), 0, st, cone_cam,
-                           c->n_tri, c->n_clu, tmp);
+        hipLaunchKernelGGL(rt_cluster_prepass, dim3(cluster_blocks(c->n_clu)), dim3(256), 0, st, cone_cam,
+                           c->n_tri, c->n_clu, tmp, 64);
         HIP_TRY(c, hipGetLastError());
-        hipLaunchKernelGGL(rt_cluster_sort, dim3((unsigned)((c->n_clu + 255) / 256)), dim3(256), 0, st, tmp,
+        hipLaunchKernelGGL(rt_cluster_sort, dim3(cluster_blocks(c->n_clu)), dim3(256), 0, st, tmp,
                            c->n_clu, clu_cam);
         HIP_TRY(c, hipGetLastError());
     }
@@ -1676,7 +1705,7 @@ static int camera_prepass(rt_ctx* c, const rt_frame* f, hipStream_t st, bool all
     std::memcpy(c->cam_key, f->cam_pos, sizeof c->cam_key);
     c->cam_valid = true;
     c->tricam_all = all_tricam || c->n_tri <= kTricamMaxTriangles;
-    c->cb_valid = false;
+    c->cb.valid = false;
     return RT_OK;
 }
 
@@ -1689,113 +1718,257 @@ static SceneDev scene_dev(rt_ctx* c, bool lbuf, bool cbuf)
                     c->n_tri_opaque, c->n_plane_opaque, c->n_quad_opaque, c->n_translucent, c->shadow_split,
                     lbuf ? c->lb_levels : 0, c->d_lb_off, c->d_lb_ent, c->d_lb_dcap, c->d_lb_meta,
                     (c->d_uni && c->opt_union) ? c->d_uni : nullptr,
-                    c->d_cb_off, c->d_cb_ent, c->d_cb_flag, cbuf ? c->cb_tiles_x : 0,
-                    c->cb_inline ? c->d_cb_rec : nullptr};
+                    c->cb.off, c->cb.ent, c->cb.flag, cbuf ? c->cb.tiles_x : 0,
+                    c->cb.inline_rec ? c->cb.rec : nullptr};
 }
 
-// Camera buffer for the frame's camera, on stream st: per-tile counts, a
-// device scan into the offsets, one 8-byte read of the total (the entry
-// array's size), then the fill, keys and inline records.  Needs the camera
-// prepass done and st ordered after every render that may read the buffers.
-static int cb_build(rt_ctx* c, const rt_frame* f, hipStream_t st)
+// ---- the camera buffer (rt_cambuf.h), host side
+// A replaced buffer that an enqueued render or build may still read: freed
+// at the next host sync of the context (or kept for a captured graph).
+static void free_later(rt_ctx* c, void* p)
 {
-    const auto t0 = std::chrono::steady_clock::now();
-    const int tx = (f->width + 7) / 8, ty = (f->height + 7) / 8, nt = tx * ty;
-    if (nt > c->cb_ntiles || !c->d_cb_off) {
-        release(c, c->d_cb_off);
-        release(c, c->d_cb_flag);
-        c->d_cb_off = nullptr;
-        c->d_cb_flag = nullptr;
-        c->cb_ntiles = 0;
-        HIP_TRY(c, hipMalloc(&c->d_cb_off, (size_t)(nt + 1) * sizeof(unsigned)));
-        HIP_TRY(c, hipMalloc(&c->d_cb_flag, (size_t)std::max(nt, 1) * sizeof(unsigned)));
-        c->cb_ntiles = nt;
-    }
-    if (int rc = ensure_scan(c, scan_scratch((size_t)nt))) return rc;
-    c->cb_valid = false;
-    c->cb_tiles_x = tx;
-    SceneDev S = scene_dev(c, false, true);
-    FrameDev F;
-    frame_dev(f, F);
-    dim3 grid((tx + 1) / 2, (ty + 1) / 2);
-    // big lists: the block pre-cull (rt_cb_block: 8 x 8 tiles per workgroup
-    // at 4K and wider, 4 x 4 below — blocks of similar angular size)
-    const bool blocks = c->n_clu > 0;
-    const int blk = f->width >= 3840 ? 8 : 4;
-    dim3 bgrid((tx + blk - 1) / blk, (ty + blk - 1) / blk);
-    HIP_TRY(c, hipEventRecord(c->ev_cb0, st));
-    if (blocks) {
-        HIP_TRY(c, hipMemsetAsync(c->d_cb_bstat, 0, 4 * sizeof(unsigned), st));
-        if (blk == 8)
-            hipLaunchKernelGGL((rt_cb_block<false, 8>), bgrid, dim3(256), 0, st, S, F, (const unsigned*)nullptr,
-                               c->d_cb_off, c->d_cb_flag, (int2*)nullptr, c->d_cb_bstat);
-        else
-            hipLaunchKernelGGL((rt_cb_block<false, 4>), bgrid, dim3(256), 0, st, S, F, (const unsigned*)nullptr,
-                               c->d_cb_off, c->d_cb_flag, (int2*)nullptr, c->d_cb_bstat);
-    } else {
-        hipLaunchKernelGGL(rt_cb_build<false>, grid, dim3(256), 0, st, S, F, (const unsigned*)nullptr, c->d_cb_off,
-                           c->d_cb_flag, (int2*)nullptr);
-    }
-    HIP_TRY(c, hipGetLastError());
-    c->cb_blocks = blocks;
-    unsigned long long* tot = nullptr;
-    HIP_TRY(c, scan_u32(c->d_cb_off, (unsigned)nt, c->d_cb_off, (unsigned long long*)c->d_scan, st, &tot));
-    HIP_TRY(c, hipMemcpyAsync(c->h_word, tot, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
-    HIP_TRY(c, hipStreamSynchronize(st));
-    const unsigned long long run = *c->h_word;
-    if (run > 0xFFFFFFF0ull) {
-        c->err = "camera buffer too large";
-        return RT_E_UNSUPPORTED;
-    }
-    const bool want_inline = run > 0 && (double)run * 4 * sizeof(float4) <= c->opt_cb_inline_mb * 1048576.0;
-    if (run > c->cb_cap || !c->d_cb_ent) {
-        release(c, c->d_cb_ent);
-        c->d_cb_ent = nullptr;
-        c->cb_cap = 0;
-        HIP_TRY(c, hipMalloc(&c->d_cb_ent, std::max<size_t>(run, 1) * sizeof(int2)));
-        c->cb_cap = std::max<size_t>(run, 1);
-    }
-    if (want_inline && (run > c->cb_rec_cap || !c->d_cb_rec)) {
-        release(c, c->d_cb_rec);
-        c->d_cb_rec = nullptr;
-        c->cb_rec_cap = 0;
-        HIP_TRY(c, hipMalloc(&c->d_cb_rec, std::max<size_t>(run, 1) * 4 * sizeof(float4)));
-        c->cb_rec_cap = std::max<size_t>(run, 1);
-    }
-    if (blocks && blk == 8)
-        hipLaunchKernelGGL((rt_cb_block<true, 8>), bgrid, dim3(256), 0, st, S, F, (const unsigned*)c->d_cb_off,
-                           (unsigned*)nullptr, c->d_cb_flag, c->d_cb_ent, (unsigned*)nullptr);
-    else if (blocks)
-        hipLaunchKernelGGL((rt_cb_block<true, 4>), bgrid, dim3(256), 0, st, S, F, (const unsigned*)c->d_cb_off,
-                           (unsigned*)nullptr, c->d_cb_flag, c->d_cb_ent, (unsigned*)nullptr);
+    if (!p) return;
+    if (c->captured)
+        c->retired.push_back(p);
     else
-        hipLaunchKernelGGL(rt_cb_build<true>, grid, dim3(256), 0, st, S, F, (const unsigned*)c->d_cb_off,
-                           (unsigned*)nullptr, c->d_cb_flag, c->d_cb_ent);
-    HIP_TRY(c, hipGetLastError());
-    hipLaunchKernelGGL(rt_cb_keys_wave, dim3((nt + 3) / 4), dim3(256), 0, st, (const unsigned*)c->d_cb_off, nt,
-                       c->d_cb_ent);
-    HIP_TRY(c, hipGetLastError());
-    c->cb_inline = want_inline;
-    if (c->cb_inline) {
-        hipLaunchKernelGGL(rt_cb_expand, dim3((unsigned)((run + 255) / 256)), dim3(256), 0, st,
-                           (const int2*)c->d_cb_ent, (unsigned)run, (const float4*)c->d_tricam, c->d_cb_rec);
-        HIP_TRY(c, hipGetLastError());
+        c->deferred.push_back(p);
+}
+
+static void cb_free(rt_ctx::CamBuf& B)
+{
+    hipFree(B.tcone);
+    hipFree(B.off);
+    hipFree(B.cur);
+    hipFree(B.flag);
+    hipFree(B.big);
+    hipFree(B.lng);
+    hipFree(B.stat);
+    hipFree(B.scan);
+    hipFree(B.ent);
+    hipFree(B.rec);
+    if (B.h_tot) hipHostFree(B.h_tot);
+    if (B.ev_tot) hipEventDestroy(B.ev_tot);
+    if (B.ev0) hipEventDestroy(B.ev0);
+    if (B.ev1) hipEventDestroy(B.ev1);
+    B = rt_ctx::CamBuf{};
+}
+
+// The camera buffer needs the frame's orientation to be a rotation (rows
+// 0-2 orthonormal to 1e-5, no translation row: cb_box reads directions in
+// camera coordinates through it) and a sane film; other frames render
+// without one (the per-wave path: the same image).
+static bool cb_frame_ok(const rt_frame* f)
+{
+    const float* m = f->orient;
+    if (m[12] != 0.0f || m[13] != 0.0f || m[14] != 0.0f) return false;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            const double d = (double)m[4 * i] * m[4 * j] + (double)m[4 * i + 1] * m[4 * j + 1] +
+                             (double)m[4 * i + 2] * m[4 * j + 2];
+            if (!(std::fabs(d - (i == j ? 1.0 : 0.0)) <= 1e-5)) return false;
+        }
+    const float v[4] = {f->half_w, f->half_h, f->inv_w, f->inv_h};
+    for (float x : v)
+        if (!(x > 0.0f) || !std::isfinite(x)) return false;
+    return true;
+}
+
+// Read back the last build's total and counters if its copy has landed
+// (no wait).
+static void cb_harvest(rt_ctx::CamBuf& B)
+{
+    if (!B.tot_pending || hipEventQuery(B.ev_tot) != hipSuccess) {
+        (void)hipGetLastError();
+        return;
     }
-    HIP_TRY(c, hipEventRecord(c->ev_cb1, st));
-    cb_key_of(f, c->cb_key);
-    c->cb_valid = true;
-    c->cb_entries = run;
-    c->cb_host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    c->cb_timed = true;
+    B.tot_pending = false;
+    B.entries = (size_t)B.h_tot[0];
+    B.observed = std::max(B.observed, B.entries);
+    std::memcpy(B.hstat, B.h_tot + 1, sizeof B.hstat);
+}
+
+// Per-tile arrays for nt tiles, the per-build words, the deferred-triangle
+// list for the scene's triangles.
+static int cb_ensure(rt_ctx* c, rt_ctx::CamBuf& B, int nt)
+{
+    if (!B.ev_tot) {
+        HIP_TRY(c, hipEventCreateWithFlags(&B.ev_tot, hipEventDisableTiming));
+        HIP_TRY(c, hipEventCreate(&B.ev0));
+        HIP_TRY(c, hipEventCreate(&B.ev1));
+        HIP_TRY(c, hipHostMalloc((void**)&B.h_tot, 8 * sizeof(unsigned long long), hipHostMallocDefault));
+        HIP_TRY(c, hipMalloc((void**)&B.stat, 8 * sizeof(unsigned)));
+    }
+    if (nt > B.nt_alloc) {
+        free_later(c, B.tcone);
+        free_later(c, B.off);
+        free_later(c, B.cur);
+        free_later(c, B.flag);
+        free_later(c, B.lng);
+        free_later(c, B.scan);
+        B.tcone = nullptr;
+        B.off = B.cur = B.flag = nullptr;
+        B.lng = nullptr;
+        B.scan = nullptr;
+        B.nt_alloc = 0;
+        HIP_TRY(c, hipMalloc((void**)&B.tcone, (size_t)nt * 2 * sizeof(float4)));
+        HIP_TRY(c, hipMalloc((void**)&B.off, (size_t)(nt + 1) * sizeof(unsigned)));
+        HIP_TRY(c, hipMalloc((void**)&B.cur, (size_t)nt * sizeof(unsigned)));
+        HIP_TRY(c, hipMalloc((void**)&B.flag, (size_t)nt * sizeof(unsigned)));
+        HIP_TRY(c, hipMalloc((void**)&B.lng, (size_t)nt * sizeof(int)));
+        B.scan_words = scan_scratch((size_t)nt);
+        HIP_TRY(c, hipMalloc(&B.scan, B.scan_words * sizeof(unsigned long long)));
+        B.nt_alloc = nt;
+    }
+    if (c->n_tri > B.big_alloc) {
+        free_later(c, B.big);
+        B.big = nullptr;
+        B.big_alloc = 0;
+        HIP_TRY(c, hipMalloc((void**)&B.big, (size_t)c->n_tri * sizeof(int)));
+        B.big_alloc = c->n_tri;
+    }
     return RT_OK;
 }
 
-static bool cb_matches(const rt_ctx* c, const rt_frame* f)
+static int cb_grow(rt_ctx* c, rt_ctx::CamBuf& B, size_t want)
 {
-    if (!c->cb_valid) return false;
+    if (want <= B.cap && B.ent) return RT_OK;
+    if (want > 0xFFFFFFF0ull) {
+        c->err = "camera buffer too large";
+        return RT_E_UNSUPPORTED;
+    }
+    free_later(c, B.ent);
+    B.ent = nullptr;
+    B.cap = 0;
+    HIP_TRY(c, hipMalloc((void**)&B.ent, std::max<size_t>(want, 1) * sizeof(int2)));
+    B.cap = std::max<size_t>(want, 1);
+    return RT_OK;
+}
+
+// Entries a build should have room for: 1.25 x the largest total read back
+// (plus slack), or a first guess of 16 per tile.
+static size_t cb_want_cap(const rt_ctx::CamBuf& B, int nt)
+{
+    if (B.observed == 0) return std::max<size_t>(65536, (size_t)nt * 16);
+    return B.observed + B.observed / 4 + 4096;
+}
+
+static CbDev cb_dev(const rt_ctx::CamBuf& B, const rt_frame* f)
+{
+    CbDev d;
+    d.tcone = B.tcone;
+    d.off = B.off;
+    d.cur = B.cur;
+    d.flag = B.flag;
+    d.ent = B.ent;
+    d.big = B.big;
+    d.lng = B.lng;
+    d.stat = B.stat;
+    d.cap = (unsigned)B.cap;
+    d.tiles_x = (f->width + 7) / 8;
+    d.tiles_y = (f->height + 7) / 8;
+    // the widest tile cone: lanes lie within 4 pixels of the reference lane
+    // in each axis, and on the film plane z = -1 (|d0| >= 1) an angle is at
+    // most the distance; wave_cone's cosine slack (1e-6 plus rounding)
+    // widens it by < 1.7e-3 rad (rt_cb_tiles checks every tile against it)
+    const double px = 2.0 * f->half_w * (double)f->inv_w, py = 2.0 * f->half_h * (double)f->inv_h;
+    const double wb = std::sqrt(16.0 * px * px + 16.0 * py * py) * 1.01 + 2e-3;
+    d.wbound = (float)wb;
+    if ((double)d.wbound < wb) d.wbound = std::nextafter(d.wbound, INFINITY);
+    float cw = (float)std::cos((double)d.wbound);
+    if ((double)cw < std::cos((double)d.wbound)) cw = std::nextafter(cw, INFINITY);
+    d.cos_wbound = cw;
+    return d;
+}
+
+// Build the camera buffer B for frame f on stream st, from the per-camera
+// cone records in S (S.cone_cam; the tricam records for inline entries).
+// No host sync — except with `exact_first` (a synchronous render's first
+// build, when no total was ever read back: the count is read once and the
+// capacity sized to it).  Needs st ordered after every render that may read
+// B.  capturing: inside a hipGraph capture (no timing events, no read-back).
+static int cb_build(rt_ctx* c, rt_ctx::CamBuf& B, const rt_frame* f, const SceneDev& S, hipStream_t st,
+                    bool exact_first, bool capturing, bool allow_inline)
+{
+    const auto t0 = std::chrono::steady_clock::now();
+    const int tx = (f->width + 7) / 8, ty = (f->height + 7) / 8, nt = tx * ty;
+    B.valid = false;
+    if (int rc = cb_ensure(c, B, nt)) return rc;
+    if (!capturing) cb_harvest(B);
+    const size_t fixed = (size_t)c->opt_cb_capacity;  // RT_OPT_CB_CAPACITY (tests)
+    exact_first = exact_first && B.observed == 0 && !capturing && !fixed;
+    if (fixed && !capturing && B.cap != fixed) {
+        free_later(c, B.ent);
+        B.ent = nullptr;
+        B.cap = 0;
+    }
+    if (!exact_first) {  // no growth inside a capture (the caller checked B.cap > 0)
+        const size_t want = capturing ? B.cap : (fixed ? fixed : std::max(B.cap, cb_want_cap(B, nt)));
+        if (int rc = cb_grow(c, B, want)) return rc;
+    }
+    if (!capturing) HIP_TRY(c, hipEventRecord(B.ev0, st));
+    FrameDev F;
+    frame_dev(f, F);
+    CbDev D = cb_dev(B, f);
+    HIP_TRY(c, hipMemsetAsync(B.stat, 0, 8 * sizeof(unsigned), st));
+    const unsigned tb = (unsigned)((nt + 3) / 4), bb = (unsigned)std::max(1, (c->n_tri + 255) / 256);
+    constexpr unsigned kBigGrid = 256, kLongGrid = 64;
+    hipLaunchKernelGGL(rt_cb_tiles, dim3(tb), dim3(256), 0, st, F, D);
+    hipLaunchKernelGGL(rt_cb_bin<false>, dim3(bb), dim3(256), 0, st, S, F, D);
+    hipLaunchKernelGGL(rt_cb_bin_big<false>, dim3(kBigGrid), dim3(256), 0, st, S, F, D);
+    HIP_TRY(c, hipGetLastError());
+    unsigned long long* tot = nullptr;
+    HIP_TRY(c, scan_u32(B.off, (unsigned)nt, B.off, (unsigned long long*)B.scan, st, &tot));
+    if (exact_first) {
+        HIP_TRY(c, hipMemcpyAsync(B.h_tot, tot, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+        HIP_TRY(c, hipStreamSynchronize(st));
+        B.entries = (size_t)B.h_tot[0];
+        B.observed = std::max(B.observed, B.entries);
+        if (int rc = cb_grow(c, B, cb_want_cap(B, nt))) return rc;
+        D.ent = B.ent;
+        D.cap = (unsigned)B.cap;
+    }
+    hipLaunchKernelGGL(rt_cb_bin<true>, dim3(bb), dim3(256), 0, st, S, F, D);
+    hipLaunchKernelGGL(rt_cb_bin_big<true>, dim3(kBigGrid), dim3(256), 0, st, S, F, D);
+    hipLaunchKernelGGL(rt_cb_keys_wave, dim3(tb), dim3(256), 0, st, D, nt);
+    hipLaunchKernelGGL(rt_cb_keys_long, dim3(kLongGrid), dim3(1024), 0, st, D);
+    HIP_TRY(c, hipGetLastError());
+    // inline records while the capacity fits RT_OPT_CB_INLINE_MAX_MB
+    B.inline_rec = allow_inline && (double)B.cap * 4 * sizeof(float4) <= c->opt_cb_inline_mb * 1048576.0;
+    if (B.inline_rec) {
+        if (B.rec_cap < B.cap || !B.rec) {
+            free_later(c, B.rec);
+            B.rec = nullptr;
+            B.rec_cap = 0;
+            HIP_TRY(c, hipMalloc((void**)&B.rec, B.cap * 4 * sizeof(float4)));
+            B.rec_cap = B.cap;
+        }
+        hipLaunchKernelGGL(rt_cb_expand, dim3((unsigned)((B.cap + 255) / 256)), dim3(256), 0, st,
+                           (const int2*)B.ent, (const unsigned long long*)tot, (unsigned)B.cap,
+                           (const float4*)S.tricam, B.rec);
+        HIP_TRY(c, hipGetLastError());
+    }
+    if (!capturing) {
+        HIP_TRY(c, hipMemcpyAsync(B.h_tot, tot, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+        HIP_TRY(c, hipMemcpyAsync(B.h_tot + 1, B.stat, 8 * sizeof(unsigned), hipMemcpyDeviceToHost, st));
+        HIP_TRY(c, hipEventRecord(B.ev_tot, st));
+        B.tot_pending = true;
+        HIP_TRY(c, hipEventRecord(B.ev1, st));
+        B.timed = true;
+    }
+    cb_key_of(f, B.key);
+    B.tiles_x = tx;
+    B.ntiles = nt;
+    B.valid = true;
+    B.host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return RT_OK;
+}
+
+static bool cb_matches(const rt_ctx::CamBuf& B, const rt_frame* f)
+{
+    if (!B.valid) return false;
     float key[30];
     cb_key_of(f, key);
-    return std::memcmp(key, c->cb_key, sizeof key) == 0;
+    return std::memcmp(key, B.key, sizeof key) == 0;
 }
 
 static bool frame_ok(const rt_frame* f)
@@ -1805,12 +1978,15 @@ static bool frame_ok(const rt_frame* f)
              (f->band_rows != 0 && rt_band_rows(f->height, f->band_rows, f->band_count, f->band_index) < 0));
 }
 
-// Make the per-camera state current for frame f, ordered on stream st.
-// sync_path: a synchronous call on c->stream (fenced behind every async
-// render at its start), which may also build the camera buffer.  Async:
-// a camera prepass fences st behind the other streams' renders and marks
-// the state as written on st; otherwise st waits for a pending write made
-// on another stream.  Capturing: nothing may be written (RT_E_STATE).
+// Make the per-camera state current for frame f, ordered on stream st: the
+// camera prepass when the camera moved, and the camera buffer when the
+// frame's kernel uses one and it is not current.  sync_path: a synchronous
+// call on c->stream (fenced behind every async render at its start).
+// Async (round 3: the camera buffer too, no host sync): a write fences st
+// behind the other streams' renders and marks the state as written on st;
+// otherwise st waits for a pending write made on another stream.
+// Capturing: nothing may be written (an unprepared camera is RT_E_STATE; a
+// prepared camera whose buffer is not current renders without it).
 static int prepare_state(rt_ctx* c, const rt_frame* f, hipStream_t st, bool sync_path, bool capturing, bool cb_want)
 {
     if (capturing && c->state_pending && c->state_stream != st) {
@@ -1823,7 +1999,7 @@ static int prepare_state(rt_ctx* c, const rt_frame* f, hipStream_t st, bool sync
         if (int rc = wait_state(c, st)) return rc;
     }
     const bool need_prep = camera_needs_prepass(c, f, cb_want);
-    const bool need_cb = sync_path && cb_want && !(cb_matches(c, f) && !need_prep);
+    const bool need_cb = cb_want && !(cb_matches(c->cb, f) && !need_prep);
     if (capturing) {
         if (need_prep) {
             c->err = "hipGraph capture: the frame's camera is not prepared (rt_render or rt_prepare_camera first)";
@@ -1831,25 +2007,27 @@ static int prepare_state(rt_ctx* c, const rt_frame* f, hipStream_t st, bool sync
         }
         return RT_OK;
     }
+    if (!need_prep && !need_cb) return RT_OK;
+    if (!sync_path) {
+        if (int rc = fence_async(c, st)) return rc;
+    }
     if (need_prep) {
-        if (!sync_path) {
-            if (int rc = fence_async(c, st)) return rc;
-        }
         if (int rc = camera_prepass(c, f, st, cb_want)) return rc;
-        if (!sync_path) {
-            HIP_TRY(c, hipEventRecord(c->ev_state, st));
-            c->state_stream = st;
-            c->state_pending = true;
-        }
     }
     if (need_cb) {
-        if (int rc = cb_build(c, f, st)) return rc;
+        const SceneDev S = scene_dev(c, false, false);
+        if (int rc = cb_build(c, c->cb, f, S, st, sync_path, false, true)) return rc;
+    }
+    if (!sync_path) {
+        HIP_TRY(c, hipEventRecord(c->ev_state, st));
+        c->state_stream = st;
+        c->state_pending = true;
     }
     return RT_OK;
 }
 
-// sync_path: rt_render / rt_render_float on c->stream (may build the camera
-// buffer); else rt_render_async on the caller's stream (never builds it).
+// sync_path: rt_render / rt_render_float on c->stream; else rt_render_async
+// on the caller's stream (both build the camera buffer when it is not current).
 // host_out (synchronous renders into host memory): the output is copied
 // there — for a big slab in up to 8 row chunks (multiples of 16 rows, one
 // per RT_OPT_HOST_CHUNK_MB of output), chunk i's copy on c->copy_stream
@@ -1877,12 +2055,12 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
     int cap = 0, lb = 1;
     const int mode = c->opt_light_buffer;
     const bool lbuf = c->lb_ready && (mode == 1 || (mode == 2 && c->n_tri > kClusterMinTriangles));
-    const bool cb_want = depth == 0 && c->n_tri > 0 && c->opt_camera_buffer;
+    const bool cb_want = depth == 0 && c->n_tri > 0 && c->opt_camera_buffer && cb_frame_ok(f);
     const int rows = frame_rows(f);
     if (rows > 0) {
         if (int rc = prepare_state(c, f, st, sync_path, capturing, cb_want)) return rc;
     }
-    const bool cbuf = cb_want && cb_matches(c, f);
+    const bool cbuf = cb_want && cb_matches(c->cb, f);
     kernel_fn k = (f->flags & RT_FLAG_STATS) ? pick_kernel<true>(depth, c->n_tri, c->n_lights, lbuf, cbuf, cap, lb)
                                               : pick_kernel<false>(depth, c->n_tri, c->n_lights, lbuf, cbuf, cap, lb);
     if (!k) {
@@ -1964,6 +2142,7 @@ static int finish_sync(rt_ctx* c, const rt_frame* f, hipStream_t st, bool timed)
     c->async_streams.clear();
     c->state_pending = false;
     c->state_stream = nullptr;
+    free_deferred(c);
     if (timed) {
         float ms = 0.f;
         HIP_TRY(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
@@ -2099,20 +2278,35 @@ RT_EXPORT int rt_render_sequence_async(rt_ctx* c, const rt_frame* frames, int32_
     }
     for (int i = 0; i < n; ++i) {
         const rt_frame* f = frames + i;
-        const rt_ctx::CamSlot& q = c->seq[i % kSeqSlots];
+        rt_ctx::CamSlot& q = c->seq[i % kSeqSlots];
         hipStream_t fs = nstreams > 1 ? c->seq_streams[i % nstreams] : st;
         const int rows = frame_rows(f);
         if (rows == 0) continue;
+        const int depth = reachable_depth(c, f);
+        // the slot's camera buffer (round 3): built on the frame's stream like
+        // its records; inside a capture only into buffers already sized (a
+        // first capture renders without it — the same image)
+        const int nt = ((f->width + 7) / 8) * ((f->height + 7) / 8);
+        const bool cbuf = depth == 0 && c->n_tri > 0 && c->opt_camera_buffer && cb_frame_ok(f) &&
+                          (!capturing || (q.cb.cap > 0 && q.cb.nt_alloc >= nt && q.cb.big_alloc >= c->n_tri));
         if (c->n_tri > 0) {
-            if (int rc = camera_records(c, f->cam_pos, fs, false, q.tricam, q.cone_cam, q.uni, q.clu_cam)) return rc;
+            if (int rc = camera_records(c, f->cam_pos, fs, cbuf, q.tricam, q.cone_cam, q.uni, q.clu_cam)) return rc;
         }
         int cap = 0, lb = 1;
-        kernel_fn k = pick_kernel<false>(reachable_depth(c, f), c->n_tri, c->n_lights, lbuf, false, cap, lb);
+        kernel_fn k = pick_kernel<false>(depth, c->n_tri, c->n_lights, lbuf, cbuf, cap, lb);
         SceneDev S = scene_dev(c, lbuf, false);
         S.tricam = q.tricam;
         S.cone_cam = q.cone_cam;
         S.clu_cam = q.clu_cam;
         S.uni = (q.uni && c->opt_union) ? q.uni : nullptr;
+        if (cbuf) {
+            if (int rc = cb_build(c, q.cb, f, S, fs, false, capturing, false)) return rc;
+            S.cb_off = q.cb.off;
+            S.cb_ent = q.cb.ent;
+            S.cb_flag = q.cb.flag;
+            S.cb_tiles_x = q.cb.tiles_x;
+            S.cb_rec = nullptr;
+        }
         FrameDev F;
         frame_dev(f, F);
         unsigned* rgba = rgba8_dev ? (unsigned*)(rgba8_dev + (size_t)i * rgba8_stride) : nullptr;
@@ -2154,12 +2348,13 @@ RT_EXPORT int rt_prepare_camera(rt_ctx* c, const rt_frame* f)
     if (int rc = fence_async(c, c->stream)) return rc;
     if (int rc = wait_state(c, c->stream)) return rc;
     const int depth = reachable_depth(c, f);
-    const bool cb_want = depth == 0 && c->n_tri > 0 && c->opt_camera_buffer;
+    const bool cb_want = depth == 0 && c->n_tri > 0 && c->opt_camera_buffer && cb_frame_ok(f);
     if (int rc = prepare_state(c, f, c->stream, true, false, cb_want)) return rc;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     c->async_streams.clear();
     c->state_pending = false;
     c->state_stream = nullptr;
+    free_deferred(c);
     return RT_OK;
 }
 
@@ -2265,27 +2460,78 @@ RT_EXPORT int rt_debug_lb_info(rt_ctx* c, double* out, int n)
 RT_EXPORT int rt_debug_cb_info(rt_ctx* c, double* out, int n)
 {
     if (!c || !out || n < 4) return RT_E_ARG;
-    if (c->cb_timed) {
+    if (c->cpu) return not_cpu(c);
+    rt_ctx::CamBuf& B = c->cb;
+    if (B.timed) {
         float ms = 0.f;
-        HIP_TRY(c, hipEventSynchronize(c->ev_cb1));
-        HIP_TRY(c, hipEventElapsedTime(&ms, c->ev_cb0, c->ev_cb1));
-        c->cb_build_ms = ms;
-        c->cb_timed = false;
+        HIP_TRY(c, hipEventSynchronize(B.ev1));
+        HIP_TRY(c, hipEventElapsedTime(&ms, B.ev0, B.ev1));
+        B.build_ms = ms;
+        B.timed = false;
     }
-    out[0] = c->cb_valid ? 1.0 : 0.0;
-    out[1] = (double)c->cb_entries;
-    out[2] = c->cb_build_ms;
-    out[3] = (double)c->cb_ntiles;
-    if (n > 4) out[4] = c->cb_inline ? 1.0 : 0.0;
-    if (n > 5) out[5] = c->cb_host_ms;
-    if (n > 8) {  // block pre-cull: blocks, blocks whose tiles walked every cluster, staged members
-        unsigned b[4] = {0, 0, 0, 0};
-        if (c->cb_blocks) HIP_TRY(c, hipMemcpy(b, c->d_cb_bstat, sizeof b, hipMemcpyDeviceToHost));
-        out[6] = b[0];
-        out[7] = b[1];
-        out[8] = b[2];
+    if (B.tot_pending) {
+        HIP_TRY(c, hipEventSynchronize(B.ev_tot));
+        cb_harvest(B);
     }
+    out[0] = B.valid ? 1.0 : 0.0;
+    out[1] = (double)B.entries;
+    out[2] = B.build_ms;
+    out[3] = (double)B.ntiles;
+    if (n > 4) out[4] = B.inline_rec ? 1.0 : 0.0;
+    if (n > 5) out[5] = B.host_ms;
+    // binning counters: triangles binned by the whole grid, (triangle, tile)
+    // pairs tested, lists sorted in LDS (longer than 256), the longest list
+    if (n > 6) out[6] = B.hstat[0];
+    if (n > 7) out[7] = B.hstat[1];
+    if (n > 8) out[8] = B.hstat[3];
+    if (n > 9) out[9] = B.hstat[4];
+    if (n > 10) out[10] = (double)B.cap;
     return RT_OK;
+}
+
+// Diagnostic (include/rt_debug.h): the current camera buffer against brute
+// force (rt_cb_verify): out[0] = tiles whose list is not exactly the
+// passing triangles (or mis-keyed), out[1] = passing pairs, out[2] = tiles
+// with a list.  Synchronous.
+RT_EXPORT int rt_debug_cb_verify(rt_ctx* c, unsigned long long* out)
+{
+    if (!c || !out) return RT_E_ARG;
+    if (c->cpu) return not_cpu(c);
+    HIP_TRY(c, hipSetDevice(c->device));
+    if (int rc = sync_all(c)) return rc;
+    rt_ctx::CamBuf& B = c->cb;
+    if (!B.valid) {
+        c->err = "no current camera buffer";
+        return RT_E_STATE;
+    }
+    unsigned* d = nullptr;
+    HIP_TRY(c, hipMalloc((void**)&d, 2 * sizeof(unsigned)));
+    int rc = RT_OK;
+    if (hipMemset(d, 0, 2 * sizeof(unsigned)) != hipSuccess) rc = RT_E_HIP;
+    CbDev D{};
+    D.tcone = B.tcone;
+    D.off = B.off;
+    D.cur = B.cur;
+    D.flag = B.flag;
+    D.ent = B.ent;
+    D.cap = (unsigned)B.cap;
+    D.tiles_x = B.tiles_x;
+    D.tiles_y = B.ntiles / std::max(1, B.tiles_x);
+    const SceneDev S = scene_dev(c, false, true);
+    unsigned h[2] = {0, 0};
+    std::vector<unsigned> flags((size_t)B.ntiles);
+    if (rc == RT_OK) {
+        hipLaunchKernelGGL(rt_cb_verify, dim3((unsigned)((B.ntiles + 3) / 4)), dim3(256), 0, c->stream, S, D, d);
+        if (hipGetLastError() != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess ||
+            hipMemcpy(h, d, sizeof h, hipMemcpyDeviceToHost) != hipSuccess ||
+            hipMemcpy(flags.data(), B.flag, flags.size() * sizeof(unsigned), hipMemcpyDeviceToHost) != hipSuccess)
+            rc = RT_E_HIP;
+    }
+    hipFree(d);
+    out[0] = h[0];
+    out[1] = h[1];
+    out[2] = (unsigned long long)std::count(flags.begin(), flags.end(), 0u);
+    return rc;
 }
 
 // Diagnostic (include/rt_debug.h): the last rt_upload_scene's host wall

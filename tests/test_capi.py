@@ -50,7 +50,7 @@ def test_every_export_is_declared():
 
 
 def test_abi_version():
-    assert rt_amd.lib().rt_abi_version() == 4
+    assert rt_amd.lib().rt_abi_version() == 5
 
 
 def test_struct_layouts_match_header():

@@ -49,6 +49,11 @@ for s in $STEPS; do
         unset RT_AMD_LIB
       done ;;
     fastmath) run fastmath_check 600 tools/fastmath_check ;;
+    camprof)
+      for c in ${CONFIGS:-c2 c3}; do
+        P=gpurun_out/camprof_$c
+        run camprof_$c 300 rocprofv3 --kernel-trace --stats --output-format csv -d $P -o run -- python tools/camera_probe.py --config $c
+      done ;;
 
     prof) P=gpurun_out/prof_${CONFIG:-c2}
           run rocprof_${CONFIG:-c2} 400 rocprofv3 --kernel-trace --stats --output-format csv -d $P -o run -- python bench.py --steps ${PROF_STEPS:-200} --no-cpu-baseline --no-host-boundary --config ${CONFIG:-c2}
