@@ -477,13 +477,12 @@ def main():
     cbinfo = None  # the camera buffer, built by that synchronous render (per camera)
     if hasattr(L, "rt_debug_cb_info"):
         L.rt_debug_cb_info.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
-        ci = (ctypes.c_double * 11)()
-        if L.rt_debug_cb_info(ctx._h, ci, 11) == 0 and ci[0]:
+        ci = (ctypes.c_double * 10)()
+        if L.rt_debug_cb_info(ctx._h, ci, 10) == 0 and ci[0]:
             cbinfo = {"entries": int(ci[1]), "build_ms": round(ci[2], 3), "tiles": int(ci[3]),
                       "inline_records": bool(ci[4]), "build_host_ms": round(ci[5], 3),
-                      "binning": {"grid_binned_triangles": int(ci[6]), "pairs_tested": int(ci[7]),
-                                  "lists_over_256": int(ci[8]), "longest_list": int(ci[9]),
-                                  "capacity": int(ci[10])}}
+                      "binning": {"candidate_pairs": int(ci[6]), "lists_over_256": int(ci[7]),
+                                  "longest_list": int(ci[8]), "capacity": int(ci[9])}}
     brute = algorithmic_flops(types, st.primary_rays, st.bounce_rays, st.shadow_rays)
     flops = executed_flops(st)
     brute_tests = (st.primary_rays + st.bounce_rays + st.shadow_rays) * int(types.shape[0])

@@ -233,10 +233,16 @@ enum {
                                    and copy in row chunks of this many MiB of output,
                                    each copy overlapping the next chunk (default 8;
                                    0 = one kernel, then one copy) */
-    RT_OPT_CB_CAPACITY = 8      /* launch (ABI 5): camera-buffer entries allocated;
+    RT_OPT_CB_CAPACITY = 8,     /* launch (ABI 5): camera-buffer entries allocated;
                                    0 (default) = sized from earlier builds' totals.  A
                                    tile whose list does not fit renders by the per-wave
                                    path (tests: a small value exercises that path) */
+    RT_OPT_ASYNC_RING = 9       /* launch (ABI 5): rt_render_async of a new camera in
+                                   a scene of more than 1,024 triangles builds its
+                                   camera state in a ring of two slots on an internal
+                                   stream, overlapping the renders already enqueued
+                                   (1, default) / in the context's state on the
+                                   caller's stream (0) */
 };
 int rt_set_option(rt_ctx*, int32_t option, double value);
 int rt_get_option(rt_ctx*, int32_t option, double* value);

@@ -24,9 +24,9 @@ int rt_debug_lb_info(rt_ctx*, double* out, int n);
 
 /* Camera buffer of the last build: out[0] current (0/1), out[1] entries,
  * out[2] device ms of the build's kernels, out[3] tiles, out[4] inline
- * records (0/1), out[5] host wall ms of the build's enqueue; out[6..10]
- * binning counters: triangles binned by the whole grid, (triangle, tile)
- * pairs tested, lists longer than 256, the longest, the entry capacity. */
+ * records (0/1), out[5] host wall ms of the build's enqueue; out[6..9]
+ * binning counters: candidate (triangle, tile) pairs tested, lists longer
+ * than 256, the longest of them, the entry capacity. */
 int rt_debug_cb_info(rt_ctx*, double* out, int n);
 
 /* The current camera buffer checked against brute force (every tile with

@@ -15,10 +15,12 @@
 // evaluated only for (triangle, tile) pairs whose tile lies in the
 // triangle's screen box — a box that provably contains every tile where the
 // test can pass (cb_box below) — instead of every tile walking every
-// cluster.  Per camera: rt_cb_tiles (the tile cones), rt_cb_bin<false> /
-// rt_cb_bin_big<false> (counts per tile), a device scan (offsets),
-// rt_cb_bin<true> / rt_cb_bin_big<true> (the entries, each at an atomic slot
-// of its tile), rt_cb_keys_wave (order and early-exit keys).  The entry
+// cluster.  Per camera: rt_cb_tiles (the tile cones), rt_cb_boxes and a
+// scan of their sizes (the candidate pairs), rt_cb_pairs<false> (the test
+// of every pair: a count per tile, a pass mask per run of 64), a scan
+// (offsets), rt_cb_pairs<true> (each passing pair at an atomic slot of its
+// tile), rt_cb_keys_small / _wave / _long (order and early-exit keys) —
+// one candidate pair per lane, only per-tile atomics.  The entry
 // array has a fixed capacity chosen by the host from earlier builds; a tile
 // whose list would end past it is flagged and takes the per-wave path (the
 // same image), and the host grows the array once it reads the total back —
@@ -43,17 +45,21 @@ __device__ __forceinline__ bool cb_tile_row_needed(const FrameDev& F, int ty)
 }
 
 // Per-build device state (one per camera buffer: the context's, and one per
-// sequence slot).  stat words: [0] triangles deferred to rt_cb_bin_big,
-// [1] (triangle, tile) pairs tested, [2] (unused), [3] lists longer than
-// RT_CB_SORT (their tiles in lng[]), [4] the longest of them.
+// sequence slot).  stat words: [1] candidate pairs, [3] lists longer than RT_CB_SORT (their tiles in
+// lng[]), [4] the longest of them, [5] lists of 33..RT_CB_SORT entries
+// (their tiles in mid[]).
 struct CbDev {
     float4* __restrict__ tcone;   // 2 per tile: [w cosW] [sinW chord 0 0]
     unsigned* __restrict__ off;   // nt + 1: counts, scanned in place into offsets
     unsigned* __restrict__ cur;   // nt: fill cursors
     unsigned* __restrict__ flag;  // nt: 1 = no list (per-wave path)
     int2* __restrict__ ent;       // cap entries {triangle, dmin bits}
-    int* __restrict__ big;        // n_tri: triangles deferred to the grid-wide pass
+    int4* __restrict__ box;       // n_tri: triangle screen boxes (tx0, ty0, nx, tiles)
+    unsigned* __restrict__ tcnt;  // n_tri + 1: box sizes, scanned in place into pair offsets
+    unsigned long long* __restrict__ rmask;  // rcap: the count pass's pass mask per run of 64 pairs
+    unsigned rcap;                // runs rmask holds (runs beyond: their tiles are flagged)
     int* __restrict__ lng;        // nt: tiles whose lists rt_cb_keys_long sorts
+    int* __restrict__ mid;        // nt: tiles whose lists rt_cb_keys_wave sorts
     unsigned* __restrict__ stat;  // 8 words (above)
     unsigned cap;                 // entries allocated
     int tiles_x, tiles_y;
@@ -84,7 +90,7 @@ __global__ __launch_bounds__(256) void rt_cb_tiles(const FrameDev F, CbDev B)
     const bool use = present && wc.ok && wc.cosW >= B.cos_wbound;
     if (lane == 0) {
         B.tcone[2 * t] = make_float4(wc.w.x, wc.w.y, wc.w.z, wc.cosW);
-        B.tcone[2 * t + 1] = make_float4(wc.sinW, wc.chord, 0.f, 0.f);
+        B.tcone[2 * t + 1] = make_float4(wc.sinW, wc.chord, use ? 0.f : 1.f, 0.f);  // z: no list
         B.flag[t] = use ? 0u : 1u;
         B.off[t] = 0u;
         B.cur[t] = 0u;
@@ -97,22 +103,22 @@ __global__ __launch_bounds__(256) void rt_cb_tiles(const FrameDev F, CbDev B)
 // Why.  With c0 = [a, cosT] (cosT > 0), the test passing means (float
 // rounding included: dot, |w|, |a|, cosW/sinW/sinT margins, the 2e-6
 // margin) cos angle(w, a) >= cos(W + T) - 4.4e-6, W = acos(cosW) <= wbound,
-// T = acos(cosT), hence angle(w, a) <= T + wbound + 2.97e-3 (the worst case,
-// at W + T = 0, is sqrt(2 * 4.4e-6)).  w is the direction of the tile's
+// T = acos(cosT), hence angle(w, a) <= acos(cos(T + wbound) - 4.4e-6)
+// (at most T + wbound + 2.97e-3, at T + wbound = 0).  w is the direction of the tile's
 // reference lane 36 = pixel (8tx + 4, 8ty + 4) clamped to the frame:
 // normalize(d0 M), d0 = (X, Y, -1), X = (2 px inv_w - 1) half_w, likewise Y;
 // M's rows r0 r1 r2 orthonormal to 1e-5 (checked by the host, which gives up
 // the buffer otherwise) put w in camera coordinates as normalize(d0) within
 // 2e-5.  So the reference pixel's d0 lies in the cone of half-angle
-// Th = T + wbound + 6.2e-3 around a_c = (a.r0, a.r1, a.r2): the rays
+// Th = acos(cos(T + wbound) - 4.4e-6) + 3e-5 around a_c = (a.r0, a.r1, a.r2): the rays
 // through the sphere of radius sin Th around the unit a_c.  Its extent in
 // X = x / (-z) is that of the disk (a_c.x, a_c.z; sin Th) seen from the
 // origin in the xz plane: the two tangents, when the disk misses the
 // origin and both lie in front (z < 0; then so does the whole wedge, which
-// is narrower than pi) — else every column.  Likewise Y.  Pixels from X by
+// is narrower than pi) — else the whole film.  Likewise Y.  Pixels from X by
 // the inverse of the affine map, 2 pixels of slack each side; the tiles
 // whose pixel ranges meet that span.  cosT <= 0 (an "always test" record)
-// or Th >= 80 degrees: every tile.
+// or Th >= 80 degrees: the whole film (then the edge planes alone, below).
 struct CbBox {
     int tx0, ty0, nx, ny;
 };
@@ -130,18 +136,16 @@ __device__ __forceinline__ bool cb_span(double cx, double cz, double rho, double
     hi = fmax(s1, s2);
     return isfinite(lo) && isfinite(hi);
 }
-// tile range [t0, t1] of a pixel span from slope span [lo, hi] (X or Y).
-__device__ __forceinline__ void cb_tiles_of(bool bounded, double lo, double hi, float half, float inv, int npx,
-                                            int ntiles, int& t0, int& t1)
+// tile range [t0, t1] of the pixels whose slope (X or Y) lies in [lo, hi]
+// (the inverse of X = (2 px inv - 1) half, 2 pixels of slack each side).
+__device__ __forceinline__ void cb_tiles_of(double lo, double hi, float half, float inv, int npx, int ntiles,
+                                            int& t0, int& t1)
 {
-    t0 = 0;
-    t1 = ntiles - 1;
-    if (!bounded) return;
     const double s = 1.0 / (2.0 * (double)inv);
     double p0 = floor((lo / (double)half + 1.0) * s) - 2.0, p1 = ceil((hi / (double)half + 1.0) * s) + 2.0;
     p0 = fmax(p0, 0.0);
     p1 = fmin(p1, (double)(npx - 1));
-    if (p1 < p0) {
+    if (!(p1 >= p0)) {
         t0 = 1;
         t1 = 0;
         return;
@@ -149,33 +153,104 @@ __device__ __forceinline__ void cb_tiles_of(bool bounded, double lo, double hi, 
     t0 = (int)(p0 / 8.0);
     t1 = min(ntiles - 1, (int)(p1 / 8.0));
 }
-__device__ __forceinline__ CbBox cb_box(const float4 c0, const FrameDev& F, const CbDev& B)
+// Clip the convex polygon (x[i], y[i]), i < n, to a X + b Y >= c.
+__device__ __forceinline__ int cb_clip(double* x, double* y, int n, double a, double b, double c)
 {
-    CbBox b{0, 0, B.tiles_x, B.tiles_y};
-    if (!(c0.w > 0.0f)) return b;  // always tested: every tile
-    const double Th = acos(fmin(1.0, (double)c0.w)) + (double)B.wbound + 6.2e-3;
-    if (!(Th < 1.396)) return b;
-    const double an = sqrt((double)c0.x * c0.x + (double)c0.y * c0.y + (double)c0.z * c0.z);
-    if (!(an > 0.5) || !isfinite(an)) return b;
-    const double ax = c0.x / an, ay = c0.y / an, az = c0.z / an;
-    const double cx = ax * F.orient[0] + ay * F.orient[1] + az * F.orient[2];
-    const double cy = ax * F.orient[4] + ay * F.orient[5] + az * F.orient[6];
-    const double cz = ax * F.orient[8] + ay * F.orient[9] + az * F.orient[10];
-    const double rho = sin(Th);
-    double xlo = 0, xhi = 0, ylo = 0, yhi = 0;
-    const bool bx = cb_span(cx, cz, rho, xlo, xhi);
-    const bool by = cb_span(cy, cz, rho, ylo, yhi);
+    double ox[8], oy[8];
+    int m = 0;
+    for (int i = 0; i < n; ++i) {
+        const int j = i + 1 == n ? 0 : i + 1;
+        const double fi = a * x[i] + b * y[i] - c, fj = a * x[j] + b * y[j] - c;
+        if (fi >= 0.0 && m < 8) {
+            ox[m] = x[i];
+            oy[m] = y[i];
+            ++m;
+        }
+        if ((fi >= 0.0) != (fj >= 0.0) && m < 8) {
+            const double u = fi / (fi - fj);
+            ox[m] = x[i] + u * (x[j] - x[i]);
+            oy[m] = y[i] + u * (y[j] - y[i]);
+            ++m;
+        }
+    }
+    for (int i = 0; i < m; ++i) {
+        x[i] = ox[i];
+        y[i] = oy[i];
+    }
+    return m;
+}
+// The edge planes tighten the box (round 3): a tile passes only if
+// edge_open holds for its reference direction w, i.e. (float rounding,
+// w's 2e-5 from normalize(d0), chord <= wbound + 2e-6 included)
+// w . n >= c = lim - wbound - 3.5e-5, so d0 = (X, Y, -1) with 1 <= |d0| <=
+// Dm (the film's corner) satisfies d0 . n_c >= c |d0| >= (c < 0 ? c Dm :
+// c): a half-plane of the film.  The box is that of the film rectangle
+// (within the cone's span) clipped by the three half-planes.
+__device__ __forceinline__ CbBox cb_box(const float4 c0, const float4* e, const FrameDev& F, const CbDev& B)
+{
+    const double hw = (double)F.half_w * (1.0 + 1e-6) + 1e-9, hh = (double)F.half_h * (1.0 + 1e-6) + 1e-9;
+    double xlo = -hw, xhi = hw, ylo = -hh, yhi = hh;
+    const double r[3][3] = {{F.orient[0], F.orient[1], F.orient[2]},
+                            {F.orient[4], F.orient[5], F.orient[6]},
+                            {F.orient[8], F.orient[9], F.orient[10]}};
+    if (c0.w > 0.0f) {
+        const double X = acos(fmin(1.0, (double)c0.w)) + (double)B.wbound;
+        const double an = sqrt((double)c0.x * c0.x + (double)c0.y * c0.y + (double)c0.z * c0.z);
+        if (X < 1.39 && an > 0.5 && isfinite(an)) {
+            const double Th = acos(fmax(-1.0, cos(X) - 4.4e-6)) + 3e-5;  // + the orientation's 2e-5
+            const double ax = c0.x / an, ay = c0.y / an, az = c0.z / an;
+            const double cx = ax * r[0][0] + ay * r[0][1] + az * r[0][2];
+            const double cy = ax * r[1][0] + ay * r[1][1] + az * r[1][2];
+            const double cz = ax * r[2][0] + ay * r[2][1] + az * r[2][2];
+            const double rho = sin(Th);
+            double lo, hi;
+            if (cb_span(cx, cz, rho, lo, hi)) {
+                xlo = fmax(xlo, lo);
+                xhi = fmin(xhi, hi);
+            }
+            if (cb_span(cy, cz, rho, lo, hi)) {
+                ylo = fmax(ylo, lo);
+                yhi = fmin(yhi, hi);
+            }
+            if (!(xlo <= xhi) || !(ylo <= yhi)) return CbBox{0, 0, 0, 0};
+        }
+    }
+    double px[8] = {xlo, xhi, xhi, xlo}, py[8] = {ylo, ylo, yhi, yhi};
+    int n = 4;
+    const double Dm = sqrt(1.0 + hw * hw + hh * hh) * (1.0 + 1e-6);
+    for (int q = 0; q < 3 && n > 0; ++q) {
+        const float4 E = e[q];
+        if (!(E.w > -3.0f)) continue;  // an always-open record
+        const double nn = sqrt((double)E.x * E.x + (double)E.y * E.y + (double)E.z * E.z);
+        if (!(nn > 0.5) || !isfinite(nn)) continue;
+        const double nx = (E.x * r[0][0] + E.y * r[0][1] + E.z * r[0][2]) / nn;
+        const double ny = (E.x * r[1][0] + E.y * r[1][1] + E.z * r[1][2]) / nn;
+        const double nz = (E.x * r[2][0] + E.y * r[2][1] + E.z * r[2][2]) / nn;
+        const double c = (double)E.w - (double)B.wbound - 3.5e-5;
+        const double k = c < 0.0 ? c * Dm : c;
+        n = cb_clip(px, py, n, nx, ny, k + nz);  // nx X + ny Y - nz >= k
+    }
+    if (n == 0) return CbBox{0, 0, 0, 0};
+    double ax0 = px[0], ax1 = px[0], ay0 = py[0], ay1 = py[0];
+    for (int i = 1; i < n; ++i) {
+        ax0 = fmin(ax0, px[i]);
+        ax1 = fmax(ax1, px[i]);
+        ay0 = fmin(ay0, py[i]);
+        ay1 = fmax(ay1, py[i]);
+    }
     int x0, x1, y0, y1;
-    cb_tiles_of(bx, xlo, xhi, F.half_w, F.inv_w, F.width, B.tiles_x, x0, x1);
-    cb_tiles_of(by, ylo, yhi, F.half_h, F.inv_h, F.height, B.tiles_y, y0, y1);
+    cb_tiles_of(ax0, ax1, F.half_w, F.inv_w, F.width, B.tiles_x, x0, x1);
+    cb_tiles_of(ay0, ay1, F.half_h, F.inv_h, F.height, B.tiles_y, y0, y1);
     if (x1 < x0 || y1 < y0) return CbBox{0, 0, 0, 0};
     return CbBox{x0, y0, x1 - x0 + 1, y1 - y0 + 1};
 }
 
-// The camera wave test of triangle k's records for tile t (rt_cb_tiles' cone).
+// The camera wave test of triangle k's records for tile t (rt_cb_tiles'
+// cone); false for a tile without a list.
 __device__ __forceinline__ bool cb_pair_test(const CbDev& B, int t, const float4 c0, float sinT, const float4* e)
 {
     const float4 a = B.tcone[2 * t], b = B.tcone[2 * t + 1];
+    if (b.z != 0.0f) return false;
     WaveCone wc;
     wc.w = make3(a.x, a.y, a.z);
     wc.cosW = a.w;
@@ -184,114 +259,112 @@ __device__ __forceinline__ bool cb_pair_test(const CbDev& B, int t, const float4
     wc.ok = true;
     return cone_overlap(wc, c0, sinT, 0.0f) && edges_open(wc, e, 0.0f);
 }
-// One passing pair: count it (FILL false), or write its entry at its tile's
-// next slot — unless the tile's list would end past the capacity: then the
-// tile is flagged (no list: the per-wave path) and nothing is written.
-template <bool FILL>
-__device__ __forceinline__ void cb_emit(const CbDev& B, int t, int k, float dmin)
+
+// Triangle boxes (one thread per triangle): box[k] = (tx0, ty0, nx, nx*ny),
+// tcnt[k] = nx * ny, the candidate pairs the pair passes expand.
+__global__ __launch_bounds__(256) void rt_cb_boxes(const SceneDev S, const FrameDev F, CbDev B)
 {
-    if (!FILL) {
-        atomicAdd(&B.off[t], 1u);
-        return;
-    }
-    const unsigned e1 = B.off[t + 1];
-    if (e1 > B.cap) {
-        B.flag[t] = 1u;
-        return;
-    }
-    const unsigned slot = B.off[t] + atomicAdd(&B.cur[t], 1u);
-    B.ent[slot] = make_int2(k, __float_as_int(dmin));
+    const int k = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (k >= S.n_tri) return;
+    const float4* e = S.cone_cam + 2 * (size_t)S.n_tri + 3 * (size_t)k;
+    const float4 e3[3] = {e[0], e[1], e[2]};
+    const CbBox b = cb_box(S.cone_cam[2 * k], e3, F, B);
+    const unsigned n = (unsigned)(b.nx * b.ny);
+    B.box[k] = make_int4(b.tx0, b.ty0, b.nx, (int)n);
+    B.tcnt[k] = n;
 }
 
-// Boxes up to this many tiles are binned by their own wave (rt_cb_bin);
-// larger ones (an always-tested record, a triangle near the camera) by the
-// whole grid (rt_cb_bin_big), so no wave walks a long box alone.
-constexpr int kCbWaveTiles = 2048;
-
-// One wave per 64 consecutive triangles (4 waves per workgroup): each lane
-// boxes its triangle; the wave then walks the concatenation of the 64 boxes
-// one pair per lane per step (the owner of pair p by a binary search over
-// the boxes' prefix sums in LDS), so a step tests 64 pairs whatever the box
-// sizes.  FILL false: count per tile and defer the big boxes; true: write.
+// One pass over every candidate (triangle, tile) pair, one pair per lane:
+// a fixed grid of waves, each taking a contiguous range of runs of 64
+// consecutive pairs (the pairs of triangle k are [pre[k], pre[k + 1]), pre
+// = the exclusive scan of the box sizes).  The range's first owner comes
+// from a binary search over pre[]; every run then finds its lanes' owners
+// among the next 64 triangles' prefixes (a search over lanes by shuffles;
+// another window for runs that cross more than 64 triangles), starting
+// from the previous run's last owner.
+// Count pass (FILL false): the camera wave test of each pair, a count per
+// passing pair's tile, and the run's pass mask (one word per run).  Fill
+// pass: only runs with passing pairs, only their passing lanes — each at the
+// next slot of its tile (a tile whose list would end past the capacity is
+// flagged instead: the per-wave path).  Only per-tile counters are atomic:
+// no global counter to serialise on.
 template <bool FILL>
-__global__ __launch_bounds__(256) void rt_cb_bin(const SceneDev S, const FrameDev F, CbDev B)
+__global__ __launch_bounds__(256) void rt_cb_pairs(const SceneDev S, CbDev B)
 {
-    __shared__ float4 rec[4][64][5];
-    __shared__ int box[4][64][3];  // tx0, ty0, nx
-    __shared__ unsigned incl[4][64];
-    const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6);
-    const int k = (int)((blockIdx.x * 4 + wv) * 64) + lane;
-    unsigned n = 0;
-    if (k < S.n_tri) {
-        const float4 c0 = S.cone_cam[2 * k];
-        const CbBox b = cb_box(c0, F, B);
-        n = (unsigned)(b.nx * b.ny);
-        if (n > (unsigned)kCbWaveTiles) {
-            if (!FILL) B.big[atomicAdd(&B.stat[0], 1u)] = k;
-            n = 0;
-        }
-        if (n) {
-            rec[wv][lane][0] = c0;
-            rec[wv][lane][1] = S.cone_cam[2 * k + 1];
-            const float4* e = S.cone_cam + 2 * (size_t)S.n_tri + 3 * (size_t)k;
-            rec[wv][lane][2] = e[0];
-            rec[wv][lane][3] = e[1];
-            rec[wv][lane][4] = e[2];
-            box[wv][lane][0] = b.tx0;
-            box[wv][lane][1] = b.ty0;
-            box[wv][lane][2] = b.nx;
-        }
-    }
-    // inclusive prefix of the box sizes over the wave
-    unsigned v = n;
-    for (int o = 1; o < 64; o <<= 1) {
-        const unsigned u = __shfl_up(v, o);
-        if (lane >= o) v += u;
-    }
-    incl[wv][lane] = v;
-    const unsigned total = (unsigned)__shfl(v, 63);
-    wave_lds_sync();
-    if (!FILL && lane == 0 && total) atomicAdd(&B.stat[1], total);
-    for (unsigned p0 = 0; p0 < total; p0 += 64) {
-        const unsigned p = p0 + (unsigned)lane;
-        if (p >= total) break;
-        int lo = 0, hi = 63;  // the first owner with incl > p
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (incl[wv][mid] > p)
-                hi = mid;
+    const int lane = (int)(threadIdx.x & 63);
+    const unsigned np = B.tcnt[S.n_tri];  // total candidate pairs (the scan's last word)
+    const unsigned nw = gridDim.x * (blockDim.x >> 6);
+    const unsigned w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const unsigned nruns = (np + 63) / 64, per = (nruns + nw - 1) / nw;
+    const unsigned r0 = w * per, r1 = min(nruns, r0 + per);
+    if (r0 >= r1) return;  // wave-uniform
+    if (!FILL && lane == 0 && w == 0) B.stat[1] = np;
+    int lo = 0;
+    {
+        int hi = S.n_tri - 1;
+        const unsigned p0 = r0 * 64;
+        while (lo < hi) {  // the last k with pre[k] <= p0 (wave-uniform)
+            const int mid = (lo + hi + 1) >> 1;
+            if (B.tcnt[mid] <= p0)
+                lo = mid;
             else
-                lo = mid + 1;
+                hi = mid - 1;
         }
-        const unsigned q = p - (lo ? incl[wv][lo - 1] : 0u);
-        const int nx = box[wv][lo][2];
-        const int t = (box[wv][lo][1] + (int)(q / (unsigned)nx)) * B.tiles_x + box[wv][lo][0] + (int)(q % (unsigned)nx);
-        if (B.flag[t]) continue;
-        const float4 c0 = rec[wv][lo][0], c1 = rec[wv][lo][1];
-        if (cb_pair_test(B, t, c0, c1.w, &rec[wv][lo][2]))
-            cb_emit<FILL>(B, t, (int)((blockIdx.x * 4 + wv) * 64) + lo, c1.x);
     }
-}
-
-// The deferred (big) boxes, by the whole grid: every thread takes pairs
-// g, g + G, ... of each deferred triangle in turn.
-template <bool FILL>
-__global__ __launch_bounds__(256) void rt_cb_bin_big(const SceneDev S, const FrameDev F, CbDev B)
-{
-    const unsigned nbig = min(B.stat[0], (unsigned)S.n_tri);
-    const unsigned G = gridDim.x * blockDim.x, g = blockIdx.x * blockDim.x + threadIdx.x;
-    for (unsigned i = 0; i < nbig; ++i) {
-        const int k = B.big[i];
-        const float4 c0 = S.cone_cam[2 * k], c1 = S.cone_cam[2 * k + 1];
-        const float4* e = S.cone_cam + 2 * (size_t)S.n_tri + 3 * (size_t)k;
-        const float4 e3[3] = {e[0], e[1], e[2]};
-        const CbBox b = cb_box(c0, F, B);
-        const unsigned n = (unsigned)(b.nx * b.ny);
-        if (!FILL && g == 0) atomicAdd(&B.stat[1], n);
-        for (unsigned q = g; q < n; q += G) {
-            const int t = (b.ty0 + (int)(q / (unsigned)b.nx)) * B.tiles_x + b.tx0 + (int)(q % (unsigned)b.nx);
-            if (B.flag[t]) continue;
-            if (cb_pair_test(B, t, c0, c1.w, e3)) cb_emit<FILL>(B, t, k, c1.x);
+    for (unsigned run = r0; run < r1; ++run) {
+        unsigned long long mask = ~0ull;
+        if (FILL) {
+            if (run >= B.rcap) continue;  // no mask kept: its tiles were flagged
+            mask = B.rmask[run];
+            if (!mask) continue;  // no passing pair: nothing to place (wave-uniform)
+        }
+        const unsigned p = run * 64 + (unsigned)lane;
+        int own = -1;
+        for (int base = lo; base < S.n_tri; base += 64) {
+            // window of 64 owners: lane j holds pre[base + j]
+            const int kj = base + lane;
+            const unsigned pj = kj < S.n_tri ? B.tcnt[kj] : 0xFFFFFFFFu;
+            // my owner in this window: the last j with pre[base + j] <= p
+            int j = (unsigned)__shfl((int)pj, 0) <= p ? 0 : -1;
+            for (int step = 32; step > 0; step >>= 1) {
+                const int c = j + step;
+                const unsigned pc = (unsigned)__shfl((int)pj, c & 63);
+                if (c <= 63 && pc <= p) j = c;
+            }
+            // j = 63 with the next window's first prefix <= p: look further
+            const bool beyond = j == 63 && base + 64 < S.n_tri && B.tcnt[base + 64] <= p;
+            if (own < 0 && j >= 0 && !beyond) own = base + j;
+            if (!__any(own < 0 && p < np)) break;
+        }
+        // the next run starts at this run's last owner
+        lo = __builtin_amdgcn_readlane(own < 0 ? lo : own, 63);
+        bool pass = false;
+        int t = 0;
+        float dmin = 0.0f;
+        if (p < np && own >= 0 && ((mask >> lane) & 1ull)) {
+            const int k = own;
+            const int4 bx = B.box[k];
+            const unsigned q = p - B.tcnt[k];
+            t = (bx.y + (int)(q / (unsigned)bx.z)) * B.tiles_x + bx.x + (int)(q % (unsigned)bx.z);
+            const float4 c1 = S.cone_cam[2 * k + 1];
+            dmin = c1.x;
+            pass = FILL || cb_pair_test(B, t, S.cone_cam[2 * k], c1.w, S.cone_cam + 2 * (size_t)S.n_tri + 3 * (size_t)k);
+        }
+        if (!FILL) {
+            const unsigned long long m = __ballot(pass);
+            if (run < B.rcap) {
+                if (lane == 0) B.rmask[run] = m;
+                if (pass) atomicAdd(&B.off[t], 1u);
+            } else if (pass) {
+                B.flag[t] = 1u;  // past the mask capacity: the per-wave path
+            }
+        } else if (pass) {
+            if (B.off[t + 1] > B.cap) {
+                B.flag[t] = 1u;
+            } else {
+                const unsigned slot = B.off[t] + atomicAdd(&B.cur[t], 1u);
+                B.ent[slot] = make_int2(own, __float_as_int(dmin));
+            }
         }
     }
 }
@@ -310,36 +383,58 @@ __device__ __forceinline__ float cb_dmin(int2 en)
     return d == d ? d : -INFINITY;
 }
 
-// One wave per tile: a list of up to RT_CB_SORT (256) entries is held in
-// registers (4 per lane) and every entry's final place is its rank under
-// (dmin, triangle) — the pairs are distinct; once sorted, the suffix minimum
-// of entry e is its own dmin (NaN dmins sort first as -inf and key -inf).
-// Longer lists are sorted in LDS by rt_cb_keys_long; flagged tiles (no list,
-// or overflowed) are skipped.
-__global__ __launch_bounds__(256) void rt_cb_keys_wave(const CbDev B, int ntiles)
+// Order-preserving 64-bit sort key of an entry: the dmin's float bits
+// mapped to an unsigned order (NaN as -inf), then the triangle.
+__device__ __forceinline__ unsigned long long cb_sort_key(int2 e)
 {
-    const unsigned* __restrict__ off = B.off;
-    int2* __restrict__ ent = B.ent;
-    const int lane = threadIdx.x & 63;
-    const int t = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
-    if (t >= ntiles || B.flag[t]) return;
-    const unsigned b = off[t], n = off[t + 1] - off[t];
-    if (n <= 1) {
-        if (n == 1 && lane == 0) ent[b].y = __float_as_int(cb_dmin(ent[b]));
-        return;
-    }
-    if (n > RT_CB_SORT) {
-        if (lane == 0) {
-            B.lng[atomicAdd(&B.stat[3], 1u)] = t;
-            atomicMax(&B.stat[4], n);
-        }
-        return;
-    }
-    float kd[4];
-    int id[4];
-    unsigned rk[4];
+    unsigned u = __float_as_uint(cb_dmin(e));
+    u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+    return ((unsigned long long)u << 32) | (unsigned)e.x;
+}
+__device__ __forceinline__ int2 cb_unkey(unsigned long long key)
+{
+    unsigned u = (unsigned)(key >> 32);
+    u = (u & 0x80000000u) ? (u & 0x7fffffffu) : ~u;
+    return make_int2((int)(unsigned)key, (int)u);
+}
+// A list of up to N entries sorted in registers by a bitonic network (the
+// indices are constants after unrolling; padding keys sort last).
+template <int N>
+__device__ __forceinline__ void cb_sort_regs(int2* __restrict__ ent, unsigned b, unsigned n)
+{
+    unsigned long long a[N];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int i = 0; i < N; ++i) a[i] = (unsigned)i < n ? cb_sort_key(ent[b + i]) : ~0ull;
+#pragma unroll
+    for (int k = 2; k <= N; k <<= 1)
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1)
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                const int l = i ^ j;
+                if (l > i) {
+                    const unsigned long long x = a[i], y = a[l];
+                    const bool sw = ((i & k) == 0) ? (x > y) : (x < y);
+                    a[i] = sw ? y : x;
+                    a[l] = sw ? x : y;
+                }
+            }
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+        if ((unsigned)i < n) ent[b + i] = cb_unkey(a[i]);
+}
+
+// Rank sort of one list of up to 64 Q entries by a wave, Q per lane in
+// registers: every entry's final place is its rank under (dmin, triangle).
+template <int Q>
+__device__ __forceinline__ void cb_sort_rank_q(int2* __restrict__ ent, unsigned b, unsigned n)
+{
+    const int lane = threadIdx.x & 63;
+    float kd[Q];
+    int id[Q];
+    unsigned rk[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
         const unsigned i = (unsigned)(lane + 64 * q);
         kd[q] = INFINITY;
         id[q] = 0x7fffffff;
@@ -351,22 +446,70 @@ __global__ __launch_bounds__(256) void rt_cb_keys_wave(const CbDev B, int ntiles
         }
     }
 #pragma unroll
-    for (int qq = 0; qq < 4; ++qq) {
-        if ((unsigned)(64 * qq) >= n) break;
+    for (int qq = 0; qq < Q; ++qq) {
         const int lim = (int)min(64u, n - 64u * (unsigned)qq);
         for (int j = 0; j < lim; ++j) {
             const float kj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(kd[qq]), j));
             const int ij = __builtin_amdgcn_readlane(id[qq], j);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) rk[q] += (unsigned)((kj < kd[q]) | ((kj == kd[q]) & (ij < id[q])));
+            for (int q = 0; q < Q; ++q) rk[q] += (unsigned)((kj < kd[q]) | ((kj == kd[q]) & (ij < id[q])));
         }
     }
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+    for (int q = 0; q < Q; ++q)
         if ((unsigned)(lane + 64 * q) < n) ent[b + rk[q]] = make_int2(id[q], __float_as_int(kd[q]));
 }
+__device__ __forceinline__ void rt_cb_sort_rank(const CbDev& B, int t)
+{
+    const unsigned b = B.off[t], n = B.off[t + 1] - b;
+    if (n <= 64)
+        cb_sort_rank_q<1>(B.ent, b, n);
+    else if (n <= 128)
+        cb_sort_rank_q<2>(B.ent, b, n);
+    else
+        cb_sort_rank_q<4>(B.ent, b, n);
+}
 
-// Lists longer than RT_CB_SORT (their tiles listed by rt_cb_keys_wave):
+// Keys, one thread per tile (round 3: the per-tile wave cost ~1.6 us of
+// latency per tile at 7680 x 4320): lists of up to 32 entries are sorted in
+// registers; longer ones are queued for rt_cb_keys_wave (up to RT_CB_SORT)
+// or rt_cb_keys_long.  Once sorted, each entry's suffix minimum is its own
+// dmin, which the entry already holds.  Flagged tiles (no list, or
+// overflowed) are skipped.
+__global__ __launch_bounds__(256) void rt_cb_keys_small(const CbDev B, int ntiles)
+{
+    const int t = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (t >= ntiles || B.flag[t]) return;
+    const unsigned b = B.off[t], n = B.off[t + 1] - b;
+    if (n <= 1) {
+        if (n == 1) B.ent[b].y = __float_as_int(cb_dmin(B.ent[b]));
+    } else if (n <= 8) {
+        cb_sort_regs<8>(B.ent, b, n);
+    } else if (n <= 16) {
+        cb_sort_regs<16>(B.ent, b, n);
+    } else if (n <= 32) {
+        cb_sort_regs<32>(B.ent, b, n);
+    } else if (n <= RT_CB_SORT) {
+        B.mid[atomicAdd(&B.stat[5], 1u)] = t;
+    } else {
+        B.lng[atomicAdd(&B.stat[3], 1u)] = t;
+        atomicMax(&B.stat[4], n);
+    }
+}
+
+// Lists of 33..RT_CB_SORT (256) entries, one wave per queued tile: held in
+// registers (4 per lane) and every entry's final place is its rank under
+// (dmin, triangle) — the pairs are distinct (NaN dmins sort first as -inf
+// and key -inf).  A fixed grid of waves walks the queue.
+__global__ __launch_bounds__(256) void rt_cb_keys_wave(const CbDev B)
+{
+    const unsigned nq = B.stat[5];
+    const unsigned nw = gridDim.x * 4, w0 = blockIdx.x * 4 + (threadIdx.x >> 6);
+    for (unsigned qi = w0; qi < nq; qi += nw) {
+        rt_cb_sort_rank(B, B.mid[qi]);
+    }
+}
+// Lists longer than RT_CB_SORT (their tiles queued by rt_cb_keys_small):
 // one workgroup per such tile sorts the list by (dmin, triangle) with a
 // bitonic sort in LDS (up to kCbLongCap entries; a longer list keeps its fill
 // order with suffix-minimum keys — exact, the early exit only later).  A

@@ -414,6 +414,9 @@ using namespace rt;
 #define RT_SEQ_STREAMS 4
 #endif
 constexpr int kSeqSlots = RT_SEQ_STREAMS;
+// camera states of rt_render_async's ring (big lists): frame k+1's built
+// while frame k renders
+constexpr int kAsyncSlots = 2;
 
 struct rt_ctx {
     int device = 0;
@@ -449,8 +452,14 @@ struct rt_ctx {
         unsigned* off = nullptr;
         unsigned* cur = nullptr;
         unsigned* flag = nullptr;
-        int* big = nullptr;
+        int4* box = nullptr;        // n_tri triangle screen boxes
+        unsigned* tcnt = nullptr;   // n_tri + 1 box sizes -> pair offsets
+        unsigned long long* rmask = nullptr;  // pass mask per run of 64 candidate pairs
+        size_t rcap = 0;            // runs rmask holds
+        size_t observed_pairs = 0;  // largest candidate-pair count read back
+        size_t built_cap = 0, built_rcap = 0;  // capacities of the last build (for its read-back)
         int* lng = nullptr;
+        int* mid = nullptr;
         unsigned* stat = nullptr;
         void* scan = nullptr;
         int2* ent = nullptr;
@@ -467,6 +476,10 @@ struct rt_ctx {
         int tiles_x = 0, ntiles = 0;
         float key[30] = {};
         bool valid = false;
+        // a captured render references off / flag / ent / rec: the next
+        // build writes fresh arrays (the captured ones are retired intact,
+        // the capture-time lists that a replay reads)
+        bool pinned = false;
         double host_ms = 0.0, build_ms = 0.0;
         bool timed = false;
     };
@@ -482,6 +495,23 @@ struct rt_ctx {
     } seq[kSeqSlots];
     hipStream_t seq_streams[kSeqSlots] = {};
     hipEvent_t seq_fork = nullptr, seq_join[kSeqSlots] = {};
+    // rt_render_async's own camera states for big lists (round 3): a ring
+    // of kAsyncSlots slots built on an internal stream, so that frame k+1's
+    // camera records and camera buffer are built while frame k's trace
+    // kernel runs.  A slot is rebuilt only after the renders that read it
+    // (its `done` event: each reader records it, after waiting for the
+    // previous one, so it covers them all); a render waits for its slot's
+    // `ready` event.
+    struct ASlot {
+        CamSlot cs;
+        float key[30] = {};
+        bool valid = false, read = false;
+        hipEvent_t ready = nullptr, done = nullptr;
+        unsigned long long used = 0;
+    } aring[kAsyncSlots];
+    hipStream_t abuild = nullptr;
+    unsigned long long ause = 0;
+    bool opt_async_ring = true;
     std::vector<void*> deferred;  // replaced buffers an enqueued render may read: freed at the next host sync
     void* d_scan = nullptr;     // u64 scratch of the light-buffer build scans
     size_t scan_words = 0;
@@ -644,6 +674,7 @@ static int sync_all(rt_ctx* c)
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     if (c->copy_stream) HIP_TRY(c, hipStreamSynchronize(c->copy_stream));
     for (hipStream_t s : c->async_streams) HIP_TRY(c, hipStreamSynchronize(s));
+    if (c->abuild) HIP_TRY(c, hipStreamSynchronize(c->abuild));
     c->async_streams.clear();
     c->state_pending = false;
     c->state_stream = nullptr;
@@ -700,6 +731,7 @@ RT_EXPORT int rt_set_option(rt_ctx* c, int32_t opt, double v)
         if (v < 0) return RT_E_ARG;
         c->opt_host_chunk_mb = v;
         return RT_OK;
+    case RT_OPT_ASYNC_RING: c->opt_async_ring = v != 0; return RT_OK;
     case RT_OPT_CB_CAPACITY:
         if (v < 0 || v > 4e9 || v != std::floor(v)) return RT_E_ARG;
         if (v != c->opt_cb_capacity) c->cb.valid = false;
@@ -721,6 +753,7 @@ RT_EXPORT int rt_get_option(rt_ctx* c, int32_t opt, double* v)
     case RT_OPT_CB_INLINE_MAX_MB: *v = c->opt_cb_inline_mb; return RT_OK;
     case RT_OPT_HOST_CHUNK_MB: *v = c->opt_host_chunk_mb; return RT_OK;
     case RT_OPT_CB_CAPACITY: *v = c->opt_cb_capacity; return RT_OK;
+    case RT_OPT_ASYNC_RING: *v = c->opt_async_ring ? 1 : 0; return RT_OK;
     default: return RT_E_ARG;
     }
 }
@@ -799,6 +832,16 @@ RT_EXPORT void rt_destroy(rt_ctx* c)
         hipFree(q.uni);
         cb_free(q.cb);
     }
+    for (auto& a : c->aring) {
+        hipFree(a.cs.tricam);
+        hipFree(a.cs.cone_cam);
+        hipFree(a.cs.clu_cam);
+        hipFree(a.cs.uni);
+        cb_free(a.cs.cb);
+        if (a.ready) hipEventDestroy(a.ready);
+        if (a.done) hipEventDestroy(a.done);
+    }
+    if (c->abuild) hipStreamDestroy(c->abuild);
     hipFree(c->d_stats);
     hipFree(c->d_scratch);
     if (c->ev0) hipEventDestroy(c->ev0);
@@ -1460,6 +1503,26 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
             HIP_TRY(c, hipMemcpyAsync(q.uni, c->d_uni, (size_t)(nl + 1) * 2 * sizeof(float4), hipMemcpyDeviceToDevice, st));
         }
     }
+    // the async ring's slots (big lists only): records of their own, sized
+    // here; their camera buffers are kept (resized on demand)
+    for (auto& a : c->aring) {
+        hipFree(a.cs.tricam);
+        hipFree(a.cs.cone_cam);
+        hipFree(a.cs.clu_cam);
+        hipFree(a.cs.uni);
+        a.cs.tricam = a.cs.cone_cam = a.cs.clu_cam = a.cs.uni = nullptr;
+        a.cs.cb.valid = false;
+        a.valid = false;
+        a.read = false;
+        if (ntr <= (size_t)kClusterMinTriangles) continue;
+        HIP_TRY(c, hipMalloc((void**)&a.cs.tricam, ntr * 4 * sizeof(float4)));
+        HIP_TRY(c, hipMalloc((void**)&a.cs.cone_cam, ntr * kConeRec * sizeof(float4)));
+        HIP_TRY(c, hipMalloc((void**)&a.cs.clu_cam, (size_t)c->n_clu * 4 * sizeof(float4)));
+        if (!a.ready) HIP_TRY(c, hipEventCreateWithFlags(&a.ready, hipEventDisableTiming));
+        if (!a.done) HIP_TRY(c, hipEventCreateWithFlags(&a.done, hipEventDisableTiming));
+    }
+    if (ntr > (size_t)kClusterMinTriangles && !c->abuild)
+        HIP_TRY(c, hipStreamCreateWithFlags(&c->abuild, hipStreamNonBlocking));
     HIP_TRY(c, hipStreamSynchronize(st));
     c->upload_parts_ms[1] = since(tp0);
     const auto tl0 = std::chrono::steady_clock::now();
@@ -1740,8 +1803,11 @@ static void cb_free(rt_ctx::CamBuf& B)
     hipFree(B.off);
     hipFree(B.cur);
     hipFree(B.flag);
-    hipFree(B.big);
+    hipFree(B.box);
+    hipFree(B.tcnt);
+    hipFree(B.rmask);
     hipFree(B.lng);
+    hipFree(B.mid);
     hipFree(B.stat);
     hipFree(B.scan);
     hipFree(B.ent);
@@ -1785,11 +1851,15 @@ static void cb_harvest(rt_ctx::CamBuf& B)
     B.entries = (size_t)B.h_tot[0];
     B.observed = std::max(B.observed, B.entries);
     std::memcpy(B.hstat, B.h_tot + 1, sizeof B.hstat);
+    B.observed_pairs = std::max(B.observed_pairs, (size_t)B.hstat[1]);
+    // a build that did not fit (tiles sent down the per-wave path) is
+    // rebuilt at its camera's next render, now that the sizes are known
+    if (B.entries > B.built_cap || ((size_t)B.hstat[1] + 63) / 64 > B.built_rcap) B.valid = false;
 }
 
 // Per-tile arrays for nt tiles, the per-build words, the deferred-triangle
 // list for the scene's triangles.
-static int cb_ensure(rt_ctx* c, rt_ctx::CamBuf& B, int nt)
+static int cb_ensure(rt_ctx* c, rt_ctx::CamBuf& B, int nt, bool capturing)
 {
     if (!B.ev_tot) {
         HIP_TRY(c, hipEventCreateWithFlags(&B.ev_tot, hipEventDisableTiming));
@@ -1798,16 +1868,17 @@ static int cb_ensure(rt_ctx* c, rt_ctx::CamBuf& B, int nt)
         HIP_TRY(c, hipHostMalloc((void**)&B.h_tot, 8 * sizeof(unsigned long long), hipHostMallocDefault));
         HIP_TRY(c, hipMalloc((void**)&B.stat, 8 * sizeof(unsigned)));
     }
-    if (nt > B.nt_alloc) {
+    if (nt > B.nt_alloc || c->n_tri > B.big_alloc) {
         free_later(c, B.tcone);
         free_later(c, B.off);
         free_later(c, B.cur);
         free_later(c, B.flag);
         free_later(c, B.lng);
+        free_later(c, B.mid);
         free_later(c, B.scan);
         B.tcone = nullptr;
         B.off = B.cur = B.flag = nullptr;
-        B.lng = nullptr;
+        B.lng = B.mid = nullptr;
         B.scan = nullptr;
         B.nt_alloc = 0;
         HIP_TRY(c, hipMalloc((void**)&B.tcone, (size_t)nt * 2 * sizeof(float4)));
@@ -1815,16 +1886,31 @@ static int cb_ensure(rt_ctx* c, rt_ctx::CamBuf& B, int nt)
         HIP_TRY(c, hipMalloc((void**)&B.cur, (size_t)nt * sizeof(unsigned)));
         HIP_TRY(c, hipMalloc((void**)&B.flag, (size_t)nt * sizeof(unsigned)));
         HIP_TRY(c, hipMalloc((void**)&B.lng, (size_t)nt * sizeof(int)));
-        B.scan_words = scan_scratch((size_t)nt);
+        HIP_TRY(c, hipMalloc((void**)&B.mid, (size_t)nt * sizeof(int)));
+        B.scan_words = scan_scratch((size_t)std::max(nt, c->n_tri));
         HIP_TRY(c, hipMalloc(&B.scan, B.scan_words * sizeof(unsigned long long)));
         B.nt_alloc = nt;
     }
     if (c->n_tri > B.big_alloc) {
-        free_later(c, B.big);
-        B.big = nullptr;
+        free_later(c, B.box);
+        free_later(c, B.tcnt);
+        B.box = nullptr;
+        B.tcnt = nullptr;
         B.big_alloc = 0;
-        HIP_TRY(c, hipMalloc((void**)&B.big, (size_t)c->n_tri * sizeof(int)));
+        HIP_TRY(c, hipMalloc((void**)&B.box, (size_t)c->n_tri * sizeof(int4)));
+        HIP_TRY(c, hipMalloc((void**)&B.tcnt, (size_t)(c->n_tri + 1) * sizeof(unsigned)));
         B.big_alloc = c->n_tri;
+    }
+    // pass masks: 1.25 x the largest candidate count read back, or a first
+    // guess of 64 candidates per triangle
+    const size_t runs = B.observed_pairs ? (B.observed_pairs / 64) * 5 / 4 + 1024
+                                         : std::max<size_t>(16384, (size_t)c->n_tri);
+    if (runs > B.rcap && !capturing) {  // a capture keeps the masks it has (the runs past them: per-wave)
+        free_later(c, B.rmask);
+        B.rmask = nullptr;
+        B.rcap = 0;
+        HIP_TRY(c, hipMalloc((void**)&B.rmask, runs * sizeof(unsigned long long)));
+        B.rcap = runs;
     }
     return RT_OK;
 }
@@ -1860,18 +1946,24 @@ static CbDev cb_dev(const rt_ctx::CamBuf& B, const rt_frame* f)
     d.cur = B.cur;
     d.flag = B.flag;
     d.ent = B.ent;
-    d.big = B.big;
+    d.box = B.box;
+    d.tcnt = B.tcnt;
+    d.rmask = B.rmask;
+    d.rcap = (unsigned)std::min<size_t>(B.rcap, 0xFFFFFFF0u);
     d.lng = B.lng;
+    d.mid = B.mid;
     d.stat = B.stat;
     d.cap = (unsigned)B.cap;
     d.tiles_x = (f->width + 7) / 8;
     d.tiles_y = (f->height + 7) / 8;
     // the widest tile cone: lanes lie within 4 pixels of the reference lane
     // in each axis, and on the film plane z = -1 (|d0| >= 1) an angle is at
-    // most the distance; wave_cone's cosine slack (1e-6 plus rounding)
-    // widens it by < 1.7e-3 rad (rt_cb_tiles checks every tile against it)
+    // most the distance; wave_cone lowers the cosine by 1e-6 (plus < 5e-7
+    // of rounding).  rt_cb_tiles checks every tile against it: a wider tile
+    // gets no list, so the bound is an efficiency matter, not a correctness one.
     const double px = 2.0 * f->half_w * (double)f->inv_w, py = 2.0 * f->half_h * (double)f->inv_h;
-    const double wb = std::sqrt(16.0 * px * px + 16.0 * py * py) * 1.01 + 2e-3;
+    const double amax = std::min(1.0, std::sqrt(16.0 * px * px + 16.0 * py * py) * 1.001);
+    const double wb = std::acos(std::max(-1.0, std::cos(amax) - 2e-6)) + 1e-6;
     d.wbound = (float)wb;
     if ((double)d.wbound < wb) d.wbound = std::nextafter(d.wbound, INFINITY);
     float cw = (float)std::cos((double)d.wbound);
@@ -1884,7 +1976,7 @@ static CbDev cb_dev(const rt_ctx::CamBuf& B, const rt_frame* f)
 // cone records in S (S.cone_cam; the tricam records for inline entries).
 // No host sync — except with `exact_first` (a synchronous render's first
 // build, when no total was ever read back: the count is read once and the
-// capacity sized to it).  Needs st ordered after every render that may read
+// capacity sized to it before the fill).  Needs st ordered after every render that may read
 // B.  capturing: inside a hipGraph capture (no timing events, no read-back).
 static int cb_build(rt_ctx* c, rt_ctx::CamBuf& B, const rt_frame* f, const SceneDev& S, hipStream_t st,
                     bool exact_first, bool capturing, bool allow_inline)
@@ -1892,8 +1984,20 @@ static int cb_build(rt_ctx* c, rt_ctx::CamBuf& B, const rt_frame* f, const Scene
     const auto t0 = std::chrono::steady_clock::now();
     const int tx = (f->width + 7) / 8, ty = (f->height + 7) / 8, nt = tx * ty;
     B.valid = false;
-    if (int rc = cb_ensure(c, B, nt)) return rc;
+    if (B.pinned) {
+        free_later(c, B.off);
+        free_later(c, B.flag);
+        free_later(c, B.ent);
+        free_later(c, B.rec);
+        B.off = B.flag = nullptr;
+        B.ent = nullptr;
+        B.rec = nullptr;
+        B.nt_alloc = 0;  // every per-tile array is reallocated
+        B.cap = B.rec_cap = 0;
+        B.pinned = false;
+    }
     if (!capturing) cb_harvest(B);
+    if (int rc = cb_ensure(c, B, nt, capturing)) return rc;
     const size_t fixed = (size_t)c->opt_cb_capacity;  // RT_OPT_CB_CAPACITY (tests)
     exact_first = exact_first && B.observed == 0 && !capturing && !fixed;
     if (fixed && !capturing && B.cap != fixed) {
@@ -1901,24 +2005,42 @@ static int cb_build(rt_ctx* c, rt_ctx::CamBuf& B, const rt_frame* f, const Scene
         B.ent = nullptr;
         B.cap = 0;
     }
-    if (!exact_first) {  // no growth inside a capture (the caller checked B.cap > 0)
-        const size_t want = capturing ? B.cap : (fixed ? fixed : std::max(B.cap, cb_want_cap(B, nt)));
+    // no growth inside a capture (the caller checked B.cap > 0)
+    const size_t want = capturing ? B.cap : (fixed ? fixed : std::max(B.cap, cb_want_cap(B, nt)));
+    if (!exact_first)
         if (int rc = cb_grow(c, B, want)) return rc;
-    }
     if (!capturing) HIP_TRY(c, hipEventRecord(B.ev0, st));
     FrameDev F;
     frame_dev(f, F);
     CbDev D = cb_dev(B, f);
+    const unsigned tb = (unsigned)((nt + 3) / 4);
+    constexpr unsigned kPairGrid = 2048, kMidGrid = 2048, kLongGrid = 64;
     HIP_TRY(c, hipMemsetAsync(B.stat, 0, 8 * sizeof(unsigned), st));
-    const unsigned tb = (unsigned)((nt + 3) / 4), bb = (unsigned)std::max(1, (c->n_tri + 255) / 256);
-    constexpr unsigned kBigGrid = 256, kLongGrid = 64;
     hipLaunchKernelGGL(rt_cb_tiles, dim3(tb), dim3(256), 0, st, F, D);
-    hipLaunchKernelGGL(rt_cb_bin<false>, dim3(bb), dim3(256), 0, st, S, F, D);
-    hipLaunchKernelGGL(rt_cb_bin_big<false>, dim3(kBigGrid), dim3(256), 0, st, S, F, D);
+    hipLaunchKernelGGL(rt_cb_boxes, dim3((unsigned)((c->n_tri + 255) / 256)), dim3(256), 0, st, S, F, D);
+    HIP_TRY(c, hipGetLastError());
+    HIP_TRY(c, scan_u32(B.tcnt, (unsigned)c->n_tri, B.tcnt, (unsigned long long*)B.scan, st, nullptr));
+    if (exact_first) {  // the pass masks sized to the candidate pairs (one read back)
+        HIP_TRY(c, hipMemcpyAsync(B.h_tot, B.tcnt + c->n_tri, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+        HIP_TRY(c, hipStreamSynchronize(st));
+        const size_t pairs = (size_t)*(const unsigned*)B.h_tot;
+        B.observed_pairs = std::max(B.observed_pairs, pairs);
+        const size_t runs = (pairs + 63) / 64 + 1024;
+        if (runs > B.rcap) {
+            free_later(c, B.rmask);
+            B.rmask = nullptr;
+            B.rcap = 0;
+            HIP_TRY(c, hipMalloc((void**)&B.rmask, runs * sizeof(unsigned long long)));
+            B.rcap = runs;
+        }
+        D.rmask = B.rmask;
+        D.rcap = (unsigned)std::min<size_t>(B.rcap, 0xFFFFFFF0u);
+    }
+    hipLaunchKernelGGL(rt_cb_pairs<false>, dim3(kPairGrid), dim3(256), 0, st, S, D);
     HIP_TRY(c, hipGetLastError());
     unsigned long long* tot = nullptr;
     HIP_TRY(c, scan_u32(B.off, (unsigned)nt, B.off, (unsigned long long*)B.scan, st, &tot));
-    if (exact_first) {
+    if (exact_first) {  // size the entries to the count (the fill is the only reader of the capacity)
         HIP_TRY(c, hipMemcpyAsync(B.h_tot, tot, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
         HIP_TRY(c, hipStreamSynchronize(st));
         B.entries = (size_t)B.h_tot[0];
@@ -1927,9 +2049,9 @@ static int cb_build(rt_ctx* c, rt_ctx::CamBuf& B, const rt_frame* f, const Scene
         D.ent = B.ent;
         D.cap = (unsigned)B.cap;
     }
-    hipLaunchKernelGGL(rt_cb_bin<true>, dim3(bb), dim3(256), 0, st, S, F, D);
-    hipLaunchKernelGGL(rt_cb_bin_big<true>, dim3(kBigGrid), dim3(256), 0, st, S, F, D);
-    hipLaunchKernelGGL(rt_cb_keys_wave, dim3(tb), dim3(256), 0, st, D, nt);
+    hipLaunchKernelGGL(rt_cb_pairs<true>, dim3(kPairGrid), dim3(256), 0, st, S, D);
+    hipLaunchKernelGGL(rt_cb_keys_small, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, st, D, nt);
+    hipLaunchKernelGGL(rt_cb_keys_wave, dim3(kMidGrid), dim3(256), 0, st, D);
     hipLaunchKernelGGL(rt_cb_keys_long, dim3(kLongGrid), dim3(1024), 0, st, D);
     HIP_TRY(c, hipGetLastError());
     // inline records while the capacity fits RT_OPT_CB_INLINE_MAX_MB
@@ -1959,6 +2081,8 @@ static int cb_build(rt_ctx* c, rt_ctx::CamBuf& B, const rt_frame* f, const Scene
     B.tiles_x = tx;
     B.ntiles = nt;
     B.valid = true;
+    B.built_cap = B.cap;
+    B.built_rcap = B.rcap;
     B.host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return RT_OK;
 }
@@ -1976,6 +2100,66 @@ static bool frame_ok(const rt_frame* f)
     return !(f->width <= 0 || f->height <= 0 || f->row_begin < 0 || f->row_end > f->height ||
              f->row_begin > f->row_end || f->max_bounces < 0 ||
              (f->band_rows != 0 && rt_band_rows(f->height, f->band_rows, f->band_count, f->band_index) < 0));
+}
+
+// The async ring (rt_render_async, big lists): the slot holding frame f's
+// camera (position, orientation, film and tile rows), or the least recently
+// used one rebuilt for it on c->abuild — after every render that read it —
+// while the renders already enqueued run.  st then waits for the slot.
+static int ring_prepare(rt_ctx* c, const rt_frame* f, hipStream_t st, rt_ctx::ASlot*& out)
+{
+    float key[30];
+    cb_key_of(f, key);
+    rt_ctx::ASlot* hit = nullptr;
+    for (auto& a : c->aring) {
+        cb_harvest(a.cs.cb);
+        if (a.valid && a.cs.cb.valid && std::memcmp(a.key, key, sizeof key) == 0) hit = &a;
+    }
+    if (!hit) {
+        hit = &c->aring[0];
+        for (auto& a : c->aring)
+            if (a.used < hit->used) hit = &a;
+        rt_ctx::ASlot& a = *hit;
+        a.valid = false;
+        if (a.read) HIP_TRY(c, hipStreamWaitEvent(c->abuild, a.done, 0));
+        if (int rc = camera_records(c, f->cam_pos, c->abuild, true, a.cs.tricam, a.cs.cone_cam, a.cs.uni,
+                                    a.cs.clu_cam))
+            return rc;
+        SceneDev S = scene_dev(c, false, false);
+        S.tricam = a.cs.tricam;
+        S.cone_cam = a.cs.cone_cam;
+        S.clu_cam = a.cs.clu_cam;
+        S.uni = nullptr;
+        if (int rc = cb_build(c, a.cs.cb, f, S, c->abuild, false, false, false)) return rc;
+        HIP_TRY(c, hipEventRecord(a.ready, c->abuild));
+        std::memcpy(a.key, key, sizeof key);
+        a.valid = true;
+    }
+    hit->used = ++c->ause;
+    HIP_TRY(c, hipStreamWaitEvent(st, hit->ready, 0));
+    // readers on several streams: the done event this render records must
+    // also cover the previous reader
+    if (hit->read) HIP_TRY(c, hipStreamWaitEvent(st, hit->done, 0));
+    out = hit;
+    return RT_OK;
+}
+
+// The slot's records and camera buffer in a render's scene.
+static void ring_scene(const rt_ctx::ASlot* a, SceneDev& S, bool cbuf)
+{
+    S.tricam = a->cs.tricam;
+    S.cone_cam = a->cs.cone_cam;
+    S.clu_cam = a->cs.clu_cam;
+    S.uni = nullptr;
+    if (cbuf) {
+        S.cb_off = a->cs.cb.off;
+        S.cb_ent = a->cs.cb.ent;
+        S.cb_flag = a->cs.cb.flag;
+        S.cb_tiles_x = a->cs.cb.tiles_x;
+    } else {
+        S.cb_tiles_x = 0;
+    }
+    S.cb_rec = nullptr;
 }
 
 // Make the per-camera state current for frame f, ordered on stream st: the
@@ -1998,8 +2182,13 @@ static int prepare_state(rt_ctx* c, const rt_frame* f, hipStream_t st, bool sync
     if (!sync_path && !capturing) {
         if (int rc = wait_state(c, st)) return rc;
     }
+    if (!capturing) cb_harvest(c->cb);
     const bool need_prep = camera_needs_prepass(c, f, cb_want);
-    const bool need_cb = cb_want && !(cb_matches(c->cb, f) && !need_prep);
+    // async renders build the camera buffer for big lists only: below
+    // kClusterMinTriangles the per-wave culling costs the kernel a few us
+    // (C2 -3.6% with the buffer), less than the build's launches
+    const bool need_cb = cb_want && !(cb_matches(c->cb, f) && !need_prep) &&
+                         (sync_path || c->n_tri > kClusterMinTriangles);
     if (capturing) {
         if (need_prep) {
             c->err = "hipGraph capture: the frame's camera is not prepared (rt_render or rt_prepare_camera first)";
@@ -2057,10 +2246,17 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
     const bool lbuf = c->lb_ready && (mode == 1 || (mode == 2 && c->n_tri > kClusterMinTriangles));
     const bool cb_want = depth == 0 && c->n_tri > 0 && c->opt_camera_buffer && cb_frame_ok(f);
     const int rows = frame_rows(f);
-    if (rows > 0) {
+    // big lists, async, a camera the context's own state does not hold:
+    // the async ring (its state built on c->abuild, overlapping the
+    // renders already enqueued)
+    rt_ctx::ASlot* ring = nullptr;
+    if (rows > 0 && !sync_path && !capturing && cb_want && c->opt_async_ring && c->abuild &&
+        c->n_tri > kClusterMinTriangles && (camera_needs_prepass(c, f, true) || !cb_matches(c->cb, f))) {
+        if (int rc = ring_prepare(c, f, st, ring)) return rc;
+    } else if (rows > 0) {
         if (int rc = prepare_state(c, f, st, sync_path, capturing, cb_want)) return rc;
     }
-    const bool cbuf = cb_want && cb_matches(c->cb, f);
+    const bool cbuf = cb_want && (ring ? ring->cs.cb.valid : cb_matches(c->cb, f));
     kernel_fn k = (f->flags & RT_FLAG_STATS) ? pick_kernel<true>(depth, c->n_tri, c->n_lights, lbuf, cbuf, cap, lb)
                                               : pick_kernel<false>(depth, c->n_tri, c->n_lights, lbuf, cbuf, cap, lb);
     if (!k) {
@@ -2068,6 +2264,7 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
         return RT_E_UNSUPPORTED;
     }
     SceneDev S = scene_dev(c, lbuf, cbuf);
+    if (ring) ring_scene(ring, S, cbuf);
     FrameDev F;
     frame_dev(f, F);
     c->last = rt_stats{};
@@ -2126,10 +2323,16 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
         timed = false;  // ev1 already recorded after the last kernel
     }
     if (timed) HIP_TRY(c, hipEventRecord(c->ev1, st));
-    if (capturing)
+    if (capturing) {
         c->captured = true;
-    else if (!sync_path)
+        if (cbuf) c->cb.pinned = true;
+    } else if (!sync_path) {
         note_async(c, st);
+    }
+    if (ring) {  // this render read the slot: its done event now covers it
+        HIP_TRY(c, hipEventRecord(ring->done, st));
+        ring->read = true;
+    }
     return RT_OK;
 }
 
@@ -2283,12 +2486,13 @@ RT_EXPORT int rt_render_sequence_async(rt_ctx* c, const rt_frame* frames, int32_
         const int rows = frame_rows(f);
         if (rows == 0) continue;
         const int depth = reachable_depth(c, f);
-        // the slot's camera buffer (round 3): built on the frame's stream like
-        // its records; inside a capture only into buffers already sized (a
-        // first capture renders without it — the same image)
+        // the slot's camera buffer (round 3, big lists as for rt_render_async):
+        // built on the frame's stream like its records; inside a capture only
+        // into buffers already sized (a first capture renders without it —
+        // the same image)
         const int nt = ((f->width + 7) / 8) * ((f->height + 7) / 8);
-        const bool cbuf = depth == 0 && c->n_tri > 0 && c->opt_camera_buffer && cb_frame_ok(f) &&
-                          (!capturing || (q.cb.cap > 0 && q.cb.nt_alloc >= nt && q.cb.big_alloc >= c->n_tri));
+        const bool cbuf = depth == 0 && c->n_tri > kClusterMinTriangles && c->opt_camera_buffer && cb_frame_ok(f) &&
+                          (!capturing || (q.cb.cap > 0 && q.cb.rcap > 0 && q.cb.nt_alloc >= nt && q.cb.big_alloc >= c->n_tri));
         if (c->n_tri > 0) {
             if (int rc = camera_records(c, f->cam_pos, fs, cbuf, q.tricam, q.cone_cam, q.uni, q.clu_cam)) return rc;
         }
@@ -2479,13 +2683,12 @@ RT_EXPORT int rt_debug_cb_info(rt_ctx* c, double* out, int n)
     out[3] = (double)B.ntiles;
     if (n > 4) out[4] = B.inline_rec ? 1.0 : 0.0;
     if (n > 5) out[5] = B.host_ms;
-    // binning counters: triangles binned by the whole grid, (triangle, tile)
-    // pairs tested, lists sorted in LDS (longer than 256), the longest list
-    if (n > 6) out[6] = B.hstat[0];
-    if (n > 7) out[7] = B.hstat[1];
-    if (n > 8) out[8] = B.hstat[3];
-    if (n > 9) out[9] = B.hstat[4];
-    if (n > 10) out[10] = (double)B.cap;
+    // binning counters: candidate (triangle, tile) pairs tested, lists
+    // sorted in LDS (longer than 256), the longest of them, the capacity
+    if (n > 6) out[6] = B.hstat[1];
+    if (n > 7) out[7] = B.hstat[3];
+    if (n > 8) out[8] = B.hstat[4];
+    if (n > 9) out[9] = (double)B.cap;
     return RT_OK;
 }
 

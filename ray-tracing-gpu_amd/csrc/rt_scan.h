@@ -88,6 +88,45 @@ __global__ __launch_bounds__(kScanThreads) void rt_scan_apply(const unsigned* in
     if (blockIdx.x == nb - 1 && threadIdx.x == 0) out[n] = (unsigned)bsum[nb];
 }
 
+// Small scans (n <= kScanSmallMax): one 1024-thread block, 64 consecutive
+// counts per thread — one launch instead of three (the per-camera builds
+// scan a count per 8x8 tile: 32,400 at 1080p).  bsum[0] = the 64-bit total.
+constexpr int kScanSmallThreads = 1024, kScanSmallItems = 64;
+constexpr unsigned kScanSmallMax = kScanSmallThreads * kScanSmallItems;
+__global__ __launch_bounds__(kScanSmallThreads) void rt_scan_small(const unsigned* in, unsigned n,
+                                                                   unsigned long long* __restrict__ bsum,
+                                                                   unsigned* out)
+{
+    __shared__ unsigned long long sh[kScanSmallThreads];
+    const int t = threadIdx.x;
+    const unsigned base = (unsigned)t * kScanSmallItems;
+    unsigned long long s = 0;
+    // all 64 loads issued before the sum (a dependent loop waited on each)
+    unsigned v[kScanSmallItems];
+#pragma unroll
+    for (int q = 0; q < kScanSmallItems; ++q) v[q] = base + q < n ? in[base + q] : 0u;
+#pragma unroll
+    for (int q = 0; q < kScanSmallItems; ++q) s += v[q];
+    sh[t] = s;
+    __syncthreads();
+    for (int o = 1; o < kScanSmallThreads; o <<= 1) {
+        const unsigned long long x = t >= o ? sh[t - o] : 0ull;
+        __syncthreads();
+        sh[t] += x;
+        __syncthreads();
+    }
+    unsigned long long run = sh[t] - s;
+#pragma unroll
+    for (int q = 0; q < kScanSmallItems; ++q) {
+        if (base + q < n) out[base + q] = (unsigned)run;
+        run += v[q];
+    }
+    if (t == kScanSmallThreads - 1) {
+        out[n] = (unsigned)sh[t];
+        bsum[0] = sh[t];
+    }
+}
+
 // Scratch words (u64) rt_scan needs for n counts.
 inline size_t scan_scratch(size_t n) { return (n + kScanTile - 1) / kScanTile + 1; }
 
@@ -96,6 +135,11 @@ inline size_t scan_scratch(size_t n) { return (n + kScanTile - 1) / kScanTile + 
 inline hipError_t scan_u32(const unsigned* in, unsigned n, unsigned* out, unsigned long long* bsum, hipStream_t st,
                            unsigned long long** total_dev)
 {
+    if (n <= kScanSmallMax) {
+        hipLaunchKernelGGL(rt_scan_small, dim3(1), dim3(kScanSmallThreads), 0, st, in, n, bsum, out);
+        if (total_dev) *total_dev = bsum;
+        return hipGetLastError();
+    }
     const unsigned nb = (unsigned)((n + kScanTile - 1) / kScanTile);
     hipLaunchKernelGGL(rt_scan_reduce, dim3(nb), dim3(kScanThreads), 0, st, in, n, bsum);
     hipLaunchKernelGGL(rt_scan_blocks, dim3(1), dim3(kScanThreads), 0, st, bsum, nb);

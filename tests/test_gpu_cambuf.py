@@ -5,8 +5,9 @@ triangle lists binned by triangle screen boxes, with no host round trip.
   triangle, the camera wave test of the per-wave path (rt_debug_cb_verify) —
   for the reference's cameras and for moved, yawed, pitched, rolled and
   wide-angle ones, odd frame sizes, slabs and bands;
-* rt_render_async of a moving camera builds the buffer itself and renders
-  the bits of a cold context (the reference's, pinned by test_gpu_parity);
+* rt_render_async of a moving camera builds the buffer itself (big lists)
+  and renders the bits of a cold context (the reference's, pinned by
+  test_gpu_parity);
 * a capacity too small for the lists (RT_OPT_CB_CAPACITY) sends the tiles
   that do not fit down the per-wave path: the same image;
 * the sequence path's per-slot buffers render cold-context bits.
@@ -35,7 +36,7 @@ def _verify(ctx):
     return list(out)
 
 
-def _cb_info(ctx, n=11):
+def _cb_info(ctx, n=10):
     L = rt_amd.lib()
     L.rt_debug_cb_info.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
     info = (ctypes.c_double * n)()
@@ -76,7 +77,8 @@ def _cameras(frame):
             _turned(frame, _rot(1, 170.0))]                         # looking back
 
 
-@pytest.mark.parametrize("which,w,h", [("scene2", 640, 360), ("scene2", 333, 197), ("scene9", 320, 240),
+@pytest.mark.parametrize("which,w,h", [("scene2", 640, 360), ("scene2", 333, 197), ("scene3", 320, 240),
+                                       ("scene1", 160, 120),
                                        ("hf", 640, 360), ("hf", 250, 131)])
 def test_lists_equal_brute_force(heightfield_path, which, w, h):
     path = heightfield_path if which == "hf" else scene(int(which[-1]))
@@ -118,14 +120,17 @@ def _cold(path, w, h, frames):
     return out
 
 
-@pytest.mark.parametrize("which", ["scene2", "hf"])
-def test_async_moving_camera_builds_and_matches(heightfield_path, which):
+@pytest.mark.parametrize("which,ring", [("scene2", 1), ("hf", 1), ("hf", 0)])
+def test_async_moving_camera_builds_and_matches(heightfield_path, which, ring):
+    """Big lists: each new camera's state is built by the async render —
+    in the async ring on the internal stream (ring 1), or in the context's
+    own state on the caller's stream (ring 0)."""
     path = heightfield_path if which == "hf" else scene(2)
     w, h = 480, 270
     s = rt_amd.Scene(path, w, h, 0)
     frames = rt_amd.camera_path(s.frame, 6, yaw_deg=1.5, step=(0.6, 0.0, -0.4))
     want = _cold(path, w, h, frames)
-    ctx = rt_amd.Context(0)
+    ctx = rt_amd.Context(0, async_ring=ring)
     ctx.upload(s)
     st = torch.cuda.current_stream()
     outs = []
@@ -135,8 +140,11 @@ def test_async_moving_camera_builds_and_matches(heightfield_path, which):
         outs.append(o)
     torch.cuda.synchronize()
     info = _cb_info(ctx)
-    assert info[0] == 1.0 and info[1] > 0  # the last camera's buffer, built by the async render
-    assert _verify(ctx)[0] == 0
+    if which == "hf" and not ring:  # the last camera's buffer, built by the async render
+        assert info[0] == 1.0 and info[1] > 0
+        assert _verify(ctx)[0] == 0
+    else:  # small lists: the per-wave path; big lists: the ring (context state untouched)
+        assert info[0] == 0.0
     for i, o in enumerate(outs):
         assert bits_equal(o.cpu().numpy(), want[i]), i
     ctx.close()
@@ -155,7 +163,7 @@ def test_overflowing_capacity_renders_the_same(heightfield_path, cap):
         bad, pairs, listed = _verify(ctx)
         assert bad == 0
         info = _cb_info(ctx)
-        assert info[10] == cap
+        assert info[9] == cap
         if info[1] > cap:  # some tiles did not fit: they render by the per-wave path
             assert listed < (w // 8 + 1) * (h // 8 + 1)
     ctx.close()
@@ -195,4 +203,31 @@ def test_sequence_slots_build_camera_buffers(heightfield_path):
         torch.cuda.synchronize()
         for i in range(len(frames)):
             assert bits_equal(ring[i].cpu().numpy(), want[i]), (rep, i)
+    ctx.close()
+
+
+def test_async_ring_two_streams_interleaved(heightfield_path):
+    """The ring's slots under renders of alternating and repeated cameras
+    on two streams, with no host sync between calls: every output equals
+    a cold context's render of its camera."""
+    w, h = 320, 200
+    s = rt_amd.Scene(heightfield_path, w, h, 0)
+    cams = rt_amd.camera_path(s.frame, 4, yaw_deg=2.0, step=(0.7, 0.0, -0.5))
+    want = _cold(heightfield_path, w, h, cams)
+    ctx = rt_amd.Context(0)
+    ctx.upload(s)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    order = [0, 1, 0, 2, 3, 3, 1, 2, 0, 3]
+    outs = []
+    for i, k in enumerate(order):
+        st = s1 if i % 2 == 0 else s2
+        o = torch.empty((h, w, 3), dtype=torch.float32, device="cuda")
+        o.record_stream(st)
+        ctx.render_async(cams[k], 0, o.data_ptr(), st.cuda_stream)
+        outs.append((k, o))
+        if i == 5:  # a synchronous render in the middle (the context's own state)
+            assert bits_equal(ctx.render_float(cams[1]), want[1])
+    ctx.sync()
+    for i, (k, o) in enumerate(outs):
+        assert bits_equal(o.cpu().numpy(), want[k]), (i, k)
     ctx.close()

@@ -25,6 +25,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c3", choices=sorted(bench.CONFIGS))
     ap.add_argument("--frames", type=int, default=20)
+    ap.add_argument("--ring", type=int, default=1, help="RT_OPT_ASYNC_RING")
+    ap.add_argument("--cb", type=int, default=1, help="RT_OPT_CAMERA_BUFFER")
     args = ap.parse_args()
     import torch
 
@@ -32,7 +34,7 @@ def main():
 
     name, W, H, depth = bench.CONFIGS[args.config]
     scene = rt_amd.Scene(bench.scene_path(name), W, H, depth)
-    ctx = rt_amd.Context(0)
+    ctx = rt_amd.Context(0, async_ring=args.ring, camera_buffer=args.cb)
     ctx.upload(scene)
     dev = torch.empty((H, W, 4), dtype=torch.uint8, device="cuda")
     stream = torch.cuda.current_stream().cuda_stream
@@ -47,7 +49,7 @@ def main():
             out.append(f)
         return out
 
-    res = {"config": args.config}
+    res = {"config": args.config, "ring": args.ring, "cb": args.cb}
     fr = cams(0.37, -0.21)
     ctx.render_async(scene.frame, dev.data_ptr(), 0, stream)
     torch.cuda.synchronize()
@@ -81,6 +83,15 @@ def main():
     ctx.render_sequence_async(path, ring.data_ptr(), H * W * 4, 0, 0, stream)
     torch.cuda.synchronize()
     res["sequence_ms"] = round((time.perf_counter() - t0) * 1e3 / n, 4)
+    import ctypes
+
+    L = rt_amd.lib()
+    L.rt_debug_cb_info.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+    ci = (ctypes.c_double * 10)()
+    ctx.prepare_camera(scene.frame)
+    if L.rt_debug_cb_info(ctx._h, ci, 10) == 0:
+        res["cbinfo"] = {"valid": ci[0], "entries": ci[1], "build_ms": round(ci[2], 4), "candidate_pairs": ci[6],
+                     "lists_over_256": ci[7], "longest": ci[8], "capacity": ci[9]}
     ctx.close()
     print(json.dumps(res), flush=True)
 

@@ -49,6 +49,11 @@ for s in $STEPS; do
         unset RT_AMD_LIB
       done ;;
     fastmath) run fastmath_check 600 tools/fastmath_check ;;
+    camprobe)
+      for c in ${CONFIGS:-c2 c3}; do
+        for r in 1 0; do run camprobe_${c}_ring$r 300 python tools/camera_probe.py --config $c --ring $r; done
+        run camprobe_${c}_nocb 300 python tools/camera_probe.py --config $c --cb 0
+      done ;;
     camprof)
       for c in ${CONFIGS:-c2 c3}; do
         P=gpurun_out/camprof_$c
