@@ -260,8 +260,9 @@ def progressive(ctx, frame, W, rows, n=60):
     return {"frames": n, "stream_fps": round(1.0 / direct, 1), "graph_fps": round(1.0 / graph, 1),
             "graph_ms_per_frame": round(graph * 1e3, 4),
             "note": "camera path (0.25 deg yaw + move per frame) rendered into an HBM ring by "
-                    "rt_render_sequence_async: per frame the camera prepasses and the trace kernel (per-wave "
-                    "camera culling, no camera buffer); enqueued directly vs one hipGraph replay per path"}
+                    "rt_render_sequence_async: per frame the camera prepasses, the slot's camera buffer where its "
+                    "build pays (big lists, >= 4 Mpx) and the trace kernel; enqueued directly vs one hipGraph "
+                    "replay per path"}
 
 
 def frame_costs(scene, frame, W, cold):
@@ -278,8 +279,8 @@ def frame_costs(scene, frame, W, cold):
       one-time code-object load), measured by main() before anything else;
     * moving camera: the camera translated every frame — synchronous
       rt_render into pinned host memory (prepass + camera buffer + kernel +
-      copy), and rt_render_async into device memory (prepass on the stream,
-      per-wave culling instead of the camera buffer), per frame."""
+      copy), and rt_render_async into device memory (prepass, and the
+      camera buffer where its build pays, on the stream), per frame."""
     import torch
 
     import rt_amd
@@ -339,7 +340,8 @@ def frame_costs(scene, frame, W, cold):
                             "async_device_ms_per_frame": round(async_ms, 4), "frames": nfr,
                             "note": "camera translated every frame; sync = rt_render into pinned host memory "
                                     "(camera prepass + camera buffer + kernel + PCIe copy); async = "
-                                    "rt_render_async into HBM (prepass on the stream, no camera buffer)"}
+                                    "rt_render_async into HBM, no host sync: the camera prepass, and the camera "
+                                    "buffer where its build pays (big lists, >= 4 Mpx), on the stream"}
     ctx.close()
     return res
 

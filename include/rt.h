@@ -147,8 +147,8 @@ int rt_render_float(rt_ctx*, const rt_frame*, float* rgb_out);
 /* Asynchronous, device pointers only, enqueued on `hip_stream` (a hipStream_t;
  * NULL = the HIP null stream, as in every HIP API).  Either output may be
  * NULL.  No host sync.  ABI 5: a new camera's per-camera state — the camera
- * buffer included — is built on `hip_stream` too, so a moving camera keeps
- * the fast path; allocation happens only when that state grows (its
+ * buffer included, where it pays (RT_OPT_CAMERA_BUFFER) — is built on
+ * `hip_stream` too; allocation happens only when that state grows (its
  * capacity follows earlier builds' totals, read back without waiting; a tile
  * whose list does not fit this time renders by the per-wave path — the same
  * image either way).
@@ -218,7 +218,11 @@ enum {
     RT_OPT_LIGHT_BUFFER = 1,    /* upload+launch: shadow rays through the light buffer:
                                    1 every depth-0 scene with opaque triangles (default),
                                    2 only above 1,024 triangles, 0 never (wave culling) */
-    RT_OPT_CAMERA_BUFFER = 2,   /* launch: per-camera tile lists, 1 (default) / 0 */
+    RT_OPT_CAMERA_BUFFER = 2,   /* launch: per-camera tile lists: 1 (default) built by
+                                   synchronous renders, and by async / sequence frames
+                                   of a new camera where the build pays (more than 1,024
+                                   triangles and at least 4 Mpx of output rows); 2 by
+                                   every frame; 0 never */
     RT_OPT_UNION_PRETEST = 3,   /* launch: small lists' union cone pre-test, 1 (default) / 0 */
     RT_OPT_LB_SCALE = 4,        /* upload: light-buffer cells per cone radius; 0 = auto (4,
                                    at least 128 cells per face edge; 6 above 1,024
@@ -237,12 +241,14 @@ enum {
                                    0 (default) = sized from earlier builds' totals.  A
                                    tile whose list does not fit renders by the per-wave
                                    path (tests: a small value exercises that path) */
-    RT_OPT_ASYNC_RING = 9       /* launch (ABI 5): rt_render_async of a new camera in
-                                   a scene of more than 1,024 triangles builds its
-                                   camera state in a ring of two slots on an internal
-                                   stream, overlapping the renders already enqueued
-                                   (1, default) / in the context's state on the
-                                   caller's stream (0) */
+    RT_OPT_ASYNC_RING = 9       /* launch (ABI 5): rt_render_async of a new camera
+                                   whose buffer is built (RT_OPT_CAMERA_BUFFER) builds
+                                   its camera state in a ring of two slots on an
+                                   internal stream, overlapping the renders already
+                                   enqueued (1) / in the context's state on the
+                                   caller's stream (0, default: the ring measured no
+                                   gain — the build's waves wait for the trace
+                                   kernel's to retire) */
 };
 int rt_set_option(rt_ctx*, int32_t option, double value);
 int rt_get_option(rt_ctx*, int32_t option, double* value);

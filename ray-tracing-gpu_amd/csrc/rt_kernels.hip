@@ -511,7 +511,7 @@ struct rt_ctx {
     } aring[kAsyncSlots];
     hipStream_t abuild = nullptr;
     unsigned long long ause = 0;
-    bool opt_async_ring = true;
+    bool opt_async_ring = false;
     std::vector<void*> deferred;  // replaced buffers an enqueued render may read: freed at the next host sync
     void* d_scan = nullptr;     // u64 scratch of the light-buffer build scans
     size_t scan_words = 0;
@@ -547,7 +547,7 @@ struct rt_ctx {
     std::vector<void*> retired;           // buffers a captured render may reference
     // Options (rt_set_option; rt.h RT_OPT_*)
     int opt_light_buffer = 1;
-    bool opt_camera_buffer = true;
+    int opt_camera_buffer = 1;  // 0 off, 1 auto, 2 async builds for every frame
     bool opt_union = true;
     double opt_lb_scale = 0.0;
     double opt_dcov_near = 0.0;
@@ -711,7 +711,11 @@ RT_EXPORT int rt_set_option(rt_ctx* c, int32_t opt, double v)
         if (v != 0 && v != 1 && v != 2) return RT_E_ARG;
         c->opt_light_buffer = (int)v;
         return RT_OK;
-    case RT_OPT_CAMERA_BUFFER: c->opt_camera_buffer = v != 0; return RT_OK;
+    case RT_OPT_CAMERA_BUFFER:
+        if (v != 0 && v != 1 && v != 2) return RT_E_ARG;
+        if ((int)v != c->opt_camera_buffer) c->cb.valid = false;
+        c->opt_camera_buffer = (int)v;
+        return RT_OK;
     case RT_OPT_UNION_PRETEST: c->opt_union = v != 0; return RT_OK;
     case RT_OPT_LB_SCALE:
         if (v < 0 || v > 1e6) return RT_E_ARG;
@@ -746,7 +750,7 @@ RT_EXPORT int rt_get_option(rt_ctx* c, int32_t opt, double* v)
     if (!c || !v) return RT_E_ARG;
     switch (opt) {
     case RT_OPT_LIGHT_BUFFER: *v = c->opt_light_buffer; return RT_OK;
-    case RT_OPT_CAMERA_BUFFER: *v = c->opt_camera_buffer ? 1 : 0; return RT_OK;
+    case RT_OPT_CAMERA_BUFFER: *v = c->opt_camera_buffer; return RT_OK;
     case RT_OPT_UNION_PRETEST: *v = c->opt_union ? 1 : 0; return RT_OK;
     case RT_OPT_LB_SCALE: *v = c->opt_lb_scale; return RT_OK;
     case RT_OPT_DCOV_NEAR: *v = c->opt_dcov_near; return RT_OK;
@@ -2102,6 +2106,21 @@ static bool frame_ok(const rt_frame* f)
              (f->band_rows != 0 && rt_band_rows(f->height, f->band_rows, f->band_count, f->band_index) < 0));
 }
 
+// Does building a new camera's buffer on the stream pay for an async or
+// sequence frame?  Measured (round 3, tools/camera_probe.py, moving camera):
+// the build costs ~0.24 ms + 0.017 ms per Mpx (its ~15 launches dominate
+// at 1080p), the buffer saves the trace kernel ~0.05-0.09 ms per Mpx of
+// per-wave culling on a big list (C3 1080p: 0.418 ms per frame per-wave,
+// 0.54 with the build; C5 7680 x 4320: 3.72 per-wave, 3.03 with it); on
+// small lists (<= 1,024 triangles) it saves a few us (C2 -3.6%).  So: big
+// lists from 4 Mpx of output rows; RT_OPT_CAMERA_BUFFER 2 builds for every
+// frame (tests).  Synchronous renders always build (they sync anyway).
+static bool cb_async_pays(const rt_ctx* c, const rt_frame* f)
+{
+    if (c->opt_camera_buffer == 2) return true;
+    return c->n_tri > kClusterMinTriangles && (double)f->width * frame_rows(f) >= 4e6;
+}
+
 // The async ring (rt_render_async, big lists): the slot holding frame f's
 // camera (position, orientation, film and tile rows), or the least recently
 // used one rebuilt for it on c->abuild — after every render that read it —
@@ -2184,11 +2203,7 @@ static int prepare_state(rt_ctx* c, const rt_frame* f, hipStream_t st, bool sync
     }
     if (!capturing) cb_harvest(c->cb);
     const bool need_prep = camera_needs_prepass(c, f, cb_want);
-    // async renders build the camera buffer for big lists only: below
-    // kClusterMinTriangles the per-wave culling costs the kernel a few us
-    // (C2 -3.6% with the buffer), less than the build's launches
-    const bool need_cb = cb_want && !(cb_matches(c->cb, f) && !need_prep) &&
-                         (sync_path || c->n_tri > kClusterMinTriangles);
+    const bool need_cb = cb_want && !(cb_matches(c->cb, f) && !need_prep) && (sync_path || cb_async_pays(c, f));
     if (capturing) {
         if (need_prep) {
             c->err = "hipGraph capture: the frame's camera is not prepared (rt_render or rt_prepare_camera first)";
@@ -2250,8 +2265,8 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
     // the async ring (its state built on c->abuild, overlapping the
     // renders already enqueued)
     rt_ctx::ASlot* ring = nullptr;
-    if (rows > 0 && !sync_path && !capturing && cb_want && c->opt_async_ring && c->abuild &&
-        c->n_tri > kClusterMinTriangles && (camera_needs_prepass(c, f, true) || !cb_matches(c->cb, f))) {
+    if (rows > 0 && !sync_path && !capturing && cb_want && c->opt_async_ring && c->abuild && cb_async_pays(c, f) &&
+        (camera_needs_prepass(c, f, true) || !cb_matches(c->cb, f))) {
         if (int rc = ring_prepare(c, f, st, ring)) return rc;
     } else if (rows > 0) {
         if (int rc = prepare_state(c, f, st, sync_path, capturing, cb_want)) return rc;
@@ -2491,7 +2506,7 @@ RT_EXPORT int rt_render_sequence_async(rt_ctx* c, const rt_frame* frames, int32_
         // into buffers already sized (a first capture renders without it —
         // the same image)
         const int nt = ((f->width + 7) / 8) * ((f->height + 7) / 8);
-        const bool cbuf = depth == 0 && c->n_tri > kClusterMinTriangles && c->opt_camera_buffer && cb_frame_ok(f) &&
+        const bool cbuf = depth == 0 && c->n_tri > 0 && c->opt_camera_buffer && cb_frame_ok(f) && cb_async_pays(c, f) &&
                           (!capturing || (q.cb.cap > 0 && q.cb.rcap > 0 && q.cb.nt_alloc >= nt && q.cb.big_alloc >= c->n_tri));
         if (c->n_tri > 0) {
             if (int rc = camera_records(c, f->cam_pos, fs, cbuf, q.tricam, q.cone_cam, q.uni, q.clu_cam)) return rc;
