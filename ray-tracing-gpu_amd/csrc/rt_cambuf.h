@@ -58,8 +58,8 @@ struct CbDev {
     unsigned* __restrict__ tcnt;  // n_tri + 1: box sizes, scanned in place into pair offsets
     unsigned long long* __restrict__ rmask;  // rcap: the count pass's pass mask per run of 64 pairs
     unsigned rcap;                // runs rmask holds (runs beyond: their tiles are flagged)
-    int* __restrict__ lng;        // nt: tiles whose lists rt_cb_keys_long sorts
-    int* __restrict__ mid;        // nt: tiles whose lists rt_cb_keys_wave sorts
+    int* __restrict__ lng;        // nt: tiles whose long lists rt_cb_keys_rest sorts in LDS
+    int* __restrict__ mid;        // nt: tiles whose 33..256-entry lists rt_cb_keys_rest sorts
     unsigned* __restrict__ stat;  // 8 words (above)
     unsigned cap;                 // entries allocated
     int tiles_x, tiles_y;
@@ -74,6 +74,7 @@ struct CbDev {
 // gets no list.  Also zeroes the counts and cursors.
 __global__ __launch_bounds__(256) void rt_cb_tiles(const FrameDev F, CbDev B)
 {
+    if (blockIdx.x == 0 && threadIdx.x < 8) B.stat[threadIdx.x] = 0u;  // the build's counters
     const int lane = (int)(threadIdx.x & 63);
     const int t = (int)(blockIdx.x * 4 + (threadIdx.x >> 6));
     const int nt = B.tiles_x * B.tiles_y;
@@ -258,6 +259,63 @@ __device__ __forceinline__ bool cb_pair_test(const CbDev& B, int t, const float4
     wc.chord = b.y;
     wc.ok = true;
     return cone_overlap(wc, c0, sinT, 0.0f) && edges_open(wc, e, 0.0f);
+}
+
+// Small lists (no clusters, <= 1,024 triangles): one wave per tile tests
+// every triangle, 64 per ballot — the binning's launches would cost more
+// than this walk (C2: 12 triangles).  The tile's cone is rt_cb_tiles' (and
+// stored like it, for rt_debug_cb_verify); FILL false: the count, true: the
+// entries in triangle order at the tile's offset (the keys sort them).
+template <bool FILL>
+__global__ __launch_bounds__(256) void rt_cb_walk(const SceneDev S, const FrameDev F, CbDev B)
+{
+    if (!FILL && blockIdx.x == 0 && threadIdx.x < 8) B.stat[threadIdx.x] = 0u;  // the build's counters
+    const int lane = (int)(threadIdx.x & 63);
+    const int t = (int)(blockIdx.x * 4 + (threadIdx.x >> 6));
+    const int nt = B.tiles_x * B.tiles_y;
+    if (t >= nt) return;  // wave-uniform
+    const int tx = t % B.tiles_x, ty = t / B.tiles_x;
+    const bool present = cb_tile_row_needed(F, ty);
+    WaveCone wc;
+    wc.ok = false;
+    if (present) {
+        const int px = tx * 8 + (lane & 7), py = ty * 8 + (lane >> 3);
+        const Vec3 D = camera_dir(F, px < F.width ? px : F.width - 1, py < F.height ? py : F.height - 1);
+        wc = wave_cone(D, true);
+    }
+    const bool use = present && wc.ok && wc.cosW >= B.cos_wbound;
+    if (!FILL && lane == 0) {
+        B.tcone[2 * t] = make_float4(wc.w.x, wc.w.y, wc.w.z, wc.cosW);
+        B.tcone[2 * t + 1] = make_float4(wc.sinW, wc.chord, use ? 0.f : 1.f, 0.f);
+        B.flag[t] = use ? 0u : 1u;
+    }
+    if (!use) {
+        if (!FILL && lane == 0) B.off[t] = 0u;
+        return;
+    }
+    unsigned n = 0, base = 0;
+    if (FILL) {
+        base = B.off[t];
+        if (B.off[t + 1] > B.cap) {  // the list does not fit: the per-wave path
+            if (lane == 0) B.flag[t] = 1u;
+            return;
+        }
+    }
+    const unsigned long long below = (1ull << lane) - 1ull;
+    for (int k0 = 0; k0 < S.n_tri; k0 += 64) {
+        const int k = k0 + lane;
+        bool reach = false;
+        float dmin = 0.0f;
+        if (k < S.n_tri) {
+            const float4 c0 = S.cone_cam[2 * k], c1 = S.cone_cam[2 * k + 1];
+            dmin = c1.x;
+            reach = cone_overlap(wc, c0, c1.w, 0.0f) && edges_open(wc, S.cone_cam + 2 * (size_t)S.n_tri + 3 * k, 0.0f);
+        }
+        const unsigned long long m = __ballot(reach);
+        if (FILL && reach) B.ent[base + n + (unsigned)__popcll(m & below)] = make_int2(k, __float_as_int(dmin));
+        n += (unsigned)__popcll(m);
+    }
+    if (!FILL && lane == 0) B.off[t] = n;
 }
 
 // Triangle boxes (one thread per triangle): box[k] = (tx0, ty0, nx, nx*ny),
@@ -472,8 +530,7 @@ __device__ __forceinline__ void rt_cb_sort_rank(const CbDev& B, int t)
 
 // Keys, one thread per tile (round 3: the per-tile wave cost ~1.6 us of
 // latency per tile at 7680 x 4320): lists of up to 32 entries are sorted in
-// registers; longer ones are queued for rt_cb_keys_wave (up to RT_CB_SORT)
-// or rt_cb_keys_long.  Once sorted, each entry's suffix minimum is its own
+// registers; longer ones are queued for rt_cb_keys_rest.  Once sorted, each entry's suffix minimum is its own
 // dmin, which the entry already holds.  Flagged tiles (no list, or
 // overflowed) are skipped.
 __global__ __launch_bounds__(256) void rt_cb_keys_small(const CbDev B, int ntiles)
@@ -497,31 +554,35 @@ __global__ __launch_bounds__(256) void rt_cb_keys_small(const CbDev B, int ntile
     }
 }
 
-// Lists of 33..RT_CB_SORT (256) entries, one wave per queued tile: held in
-// registers (4 per lane) and every entry's final place is its rank under
-// (dmin, triangle) — the pairs are distinct (NaN dmins sort first as -inf
-// and key -inf).  A fixed grid of waves walks the queue.
-__global__ __launch_bounds__(256) void rt_cb_keys_wave(const CbDev B)
-{
-    const unsigned nq = B.stat[5];
-    const unsigned nw = gridDim.x * 4, w0 = blockIdx.x * 4 + (threadIdx.x >> 6);
-    for (unsigned qi = w0; qi < nq; qi += nw) {
-        rt_cb_sort_rank(B, B.mid[qi]);
-    }
-}
-// Lists longer than RT_CB_SORT (their tiles queued by rt_cb_keys_small):
-// one workgroup per such tile sorts the list by (dmin, triangle) with a
-// bitonic sort in LDS (up to kCbLongCap entries; a longer list keeps its fill
-// order with suffix-minimum keys — exact, the early exit only later).  A
-// fixed grid walks the listed tiles (the host does not know how many).
+// The lists rt_cb_keys_small queued, one launch for both kinds:
+// * 33..RT_CB_SORT (256) entries: one wave per tile, held in registers (up
+//   to 4 per lane), every entry's final place is its rank under (dmin,
+//   triangle) — the pairs are distinct (NaN dmins sort first as -inf);
+// * longer: one workgroup per tile, a bitonic sort in LDS (up to kCbLongCap
+//   entries; a longer list keeps its fill order with suffix-minimum keys —
+//   exact, the early exit only later).
+// A fixed grid walks both queues (the host does not know their lengths).
+// Thread 0 of block 0 also publishes the build's total and counters to the
+// host (hout, pinned and device-visible), which reads them after the build's
+// event: no copy commands.
 constexpr int kCbLongCap = 4096;
-__global__ __launch_bounds__(1024) void rt_cb_keys_long(const CbDev B)
+__global__ __launch_bounds__(256) void rt_cb_keys_rest(const CbDev B, const unsigned long long* __restrict__ total,
+                                                       unsigned long long* hout)
 {
     __shared__ unsigned long long sk[kCbLongCap];  // (dmin order bits << 32) | triangle
+    if (hout && blockIdx.x == 0 && threadIdx.x == 0) {
+        hout[0] = *total;
+        for (int i = 0; i < 4; ++i)
+            hout[1 + i] = (unsigned long long)B.stat[2 * i] | ((unsigned long long)B.stat[2 * i + 1] << 32);
+        __threadfence_system();
+    }
+    const unsigned nq = B.stat[5];
+    const unsigned nw = gridDim.x * 4, w0 = blockIdx.x * 4 + (threadIdx.x >> 6);
+    for (unsigned qi = w0; qi < nq; qi += nw) rt_cb_sort_rank(B, B.mid[qi]);
     const unsigned* __restrict__ off = B.off;
     int2* __restrict__ ent = B.ent;
     const unsigned nlong = B.stat[3];
-    for (unsigned i = blockIdx.x; i < nlong; i += gridDim.x) {
+    for (unsigned i = blockIdx.x; i < nlong; i += gridDim.x) {  // block-uniform
         const int t = B.lng[i];
         const unsigned b = off[t], n = off[t + 1] - b;
         if (n > (unsigned)kCbLongCap) {
@@ -537,27 +598,18 @@ __global__ __launch_bounds__(1024) void rt_cb_keys_long(const CbDev B)
         }
         unsigned P = 1;
         while (P < n) P <<= 1;
-        for (unsigned i = threadIdx.x; i < P; i += blockDim.x) {
-            unsigned long long key = ~0ull;
-            if (i < n) {
-                const int2 e = ent[b + i];
-                // order-preserving bits of the float key (NaN as -inf)
-                unsigned u = __float_as_uint(cb_dmin(e));
-                u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-                key = ((unsigned long long)u << 32) | (unsigned)e.x;
-            }
-            sk[i] = key;
-        }
+        __syncthreads();
+        for (unsigned q = threadIdx.x; q < P; q += blockDim.x) sk[q] = q < n ? cb_sort_key(ent[b + q]) : ~0ull;
         __syncthreads();
         for (unsigned kk = 2; kk <= P; kk <<= 1) {
             for (unsigned j = kk >> 1; j > 0; j >>= 1) {
-                for (unsigned i = threadIdx.x; i < P; i += blockDim.x) {
-                    const unsigned l = i ^ j;
-                    if (l > i) {
-                        const unsigned long long x = sk[i], y = sk[l];
-                        const bool up = (i & kk) == 0;
+                for (unsigned q = threadIdx.x; q < P; q += blockDim.x) {
+                    const unsigned l = q ^ j;
+                    if (l > q) {
+                        const unsigned long long x = sk[q], y = sk[l];
+                        const bool up = (q & kk) == 0;
                         if ((x > y) == up) {
-                            sk[i] = y;
+                            sk[q] = y;
                             sk[l] = x;
                         }
                     }
@@ -565,13 +617,7 @@ __global__ __launch_bounds__(1024) void rt_cb_keys_long(const CbDev B)
                 __syncthreads();
             }
         }
-        for (unsigned i = threadIdx.x; i < n; i += blockDim.x) {
-            const unsigned long long key = sk[i];
-            unsigned u = (unsigned)(key >> 32);
-            u = (u & 0x80000000u) ? (u & 0x7fffffffu) : ~u;
-            ent[b + i] = make_int2((int)(unsigned)key, (int)u);
-        }
-        __syncthreads();
+        for (unsigned q = threadIdx.x; q < n; q += blockDim.x) ent[b + q] = cb_unkey(sk[q]);
     }
 }
 

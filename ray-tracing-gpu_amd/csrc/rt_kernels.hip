@@ -417,6 +417,7 @@ constexpr int kSeqSlots = RT_SEQ_STREAMS;
 // camera states of rt_render_async's ring (big lists): frame k+1's built
 // while frame k renders
 constexpr int kAsyncSlots = 2;
+constexpr int kCbWordSets = 16;  // camera buffers per context: 1 + sequence slots + ring slots
 
 struct rt_ctx {
     int device = 0;
@@ -516,6 +517,8 @@ struct rt_ctx {
     void* d_scan = nullptr;     // u64 scratch of the light-buffer build scans
     size_t scan_words = 0;
     unsigned long long* h_word = nullptr;  // pinned: totals read back by the builds
+    unsigned long long* h_cbwords = nullptr;  // pinned: kCbWordSets x 8 words, one set per camera buffer
+    int n_cbwords = 0;
     // light buffer (shadow cells), rt_lb_build
     unsigned* d_lb_off = nullptr;
     float4* d_lb_ent = nullptr;
@@ -607,6 +610,7 @@ RT_EXPORT int rt_create(int32_t dev, rt_ctx** out)
     HIP_TRY(c, hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
     for (hipEvent_t& e : c->ev_chunk) HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIP_TRY(c, hipHostMalloc((void**)&c->h_word, 2 * sizeof(unsigned long long), hipHostMallocDefault));
+    HIP_TRY(c, hipHostMalloc((void**)&c->h_cbwords, kCbWordSets * 8 * sizeof(unsigned long long), hipHostMallocDefault));
     HIP_TRY(c, hipMalloc(&c->d_stats, kStatSlots * sizeof(StatsDev)));
     c->far_ladder = {2.5, 6.0, 16.0, 64.0};
     return RT_OK;
@@ -861,6 +865,7 @@ RT_EXPORT void rt_destroy(rt_ctx* c)
     }
     if (c->seq_fork) hipEventDestroy(c->seq_fork);
     if (c->h_word) hipHostFree(c->h_word);
+    if (c->h_cbwords) hipHostFree(c->h_cbwords);
     hipFree(c->d_scan);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
@@ -1816,7 +1821,6 @@ static void cb_free(rt_ctx::CamBuf& B)
     hipFree(B.scan);
     hipFree(B.ent);
     hipFree(B.rec);
-    if (B.h_tot) hipHostFree(B.h_tot);
     if (B.ev_tot) hipEventDestroy(B.ev_tot);
     if (B.ev0) hipEventDestroy(B.ev0);
     if (B.ev1) hipEventDestroy(B.ev1);
@@ -1869,7 +1873,7 @@ static int cb_ensure(rt_ctx* c, rt_ctx::CamBuf& B, int nt, bool capturing)
         HIP_TRY(c, hipEventCreateWithFlags(&B.ev_tot, hipEventDisableTiming));
         HIP_TRY(c, hipEventCreate(&B.ev0));
         HIP_TRY(c, hipEventCreate(&B.ev1));
-        HIP_TRY(c, hipHostMalloc((void**)&B.h_tot, 8 * sizeof(unsigned long long), hipHostMallocDefault));
+        B.h_tot = c->h_cbwords + 8 * (c->n_cbwords++ % kCbWordSets);  // pinned words from rt_create
         HIP_TRY(c, hipMalloc((void**)&B.stat, 8 * sizeof(unsigned)));
     }
     if (nt > B.nt_alloc || c->n_tri > B.big_alloc) {
@@ -2018,8 +2022,24 @@ static int cb_build(rt_ctx* c, rt_ctx::CamBuf& B, const rt_frame* f, const Scene
     frame_dev(f, F);
     CbDev D = cb_dev(B, f);
     const unsigned tb = (unsigned)((nt + 3) / 4);
-    constexpr unsigned kPairGrid = 2048, kMidGrid = 2048, kLongGrid = 64;
-    HIP_TRY(c, hipMemsetAsync(B.stat, 0, 8 * sizeof(unsigned), st));
+    constexpr unsigned kPairGrid = 2048, kMidGrid = 2048;
+    const bool small = c->n_clu == 0;  // small lists: a tile walk instead of the binning
+    unsigned long long* tot = nullptr;
+    if (small) {
+        hipLaunchKernelGGL(rt_cb_walk<false>, dim3(tb), dim3(256), 0, st, S, F, D);
+        HIP_TRY(c, hipGetLastError());
+        HIP_TRY(c, scan_u32(B.off, (unsigned)nt, B.off, (unsigned long long*)B.scan, st, &tot));
+        if (exact_first) {
+            HIP_TRY(c, hipMemcpyAsync(B.h_tot, tot, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+            HIP_TRY(c, hipStreamSynchronize(st));
+            B.entries = (size_t)B.h_tot[0];
+            B.observed = std::max(B.observed, B.entries);
+            if (int rc = cb_grow(c, B, cb_want_cap(B, nt))) return rc;
+            D.ent = B.ent;
+            D.cap = (unsigned)B.cap;
+        }
+        hipLaunchKernelGGL(rt_cb_walk<true>, dim3(tb), dim3(256), 0, st, S, F, D);
+    } else {
     hipLaunchKernelGGL(rt_cb_tiles, dim3(tb), dim3(256), 0, st, F, D);
     hipLaunchKernelGGL(rt_cb_boxes, dim3((unsigned)((c->n_tri + 255) / 256)), dim3(256), 0, st, S, F, D);
     HIP_TRY(c, hipGetLastError());
@@ -2042,7 +2062,6 @@ static int cb_build(rt_ctx* c, rt_ctx::CamBuf& B, const rt_frame* f, const Scene
     }
     hipLaunchKernelGGL(rt_cb_pairs<false>, dim3(kPairGrid), dim3(256), 0, st, S, D);
     HIP_TRY(c, hipGetLastError());
-    unsigned long long* tot = nullptr;
     HIP_TRY(c, scan_u32(B.off, (unsigned)nt, B.off, (unsigned long long*)B.scan, st, &tot));
     if (exact_first) {  // size the entries to the count (the fill is the only reader of the capacity)
         HIP_TRY(c, hipMemcpyAsync(B.h_tot, tot, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
@@ -2054,9 +2073,10 @@ static int cb_build(rt_ctx* c, rt_ctx::CamBuf& B, const rt_frame* f, const Scene
         D.cap = (unsigned)B.cap;
     }
     hipLaunchKernelGGL(rt_cb_pairs<true>, dim3(kPairGrid), dim3(256), 0, st, S, D);
+    }
     hipLaunchKernelGGL(rt_cb_keys_small, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, st, D, nt);
-    hipLaunchKernelGGL(rt_cb_keys_wave, dim3(kMidGrid), dim3(256), 0, st, D);
-    hipLaunchKernelGGL(rt_cb_keys_long, dim3(kLongGrid), dim3(1024), 0, st, D);
+    hipLaunchKernelGGL(rt_cb_keys_rest, dim3(kMidGrid), dim3(256), 0, st, D, (const unsigned long long*)tot,
+                       capturing ? (unsigned long long*)nullptr : B.h_tot);
     HIP_TRY(c, hipGetLastError());
     // inline records while the capacity fits RT_OPT_CB_INLINE_MAX_MB
     B.inline_rec = allow_inline && (double)B.cap * 4 * sizeof(float4) <= c->opt_cb_inline_mb * 1048576.0;
@@ -2074,9 +2094,7 @@ static int cb_build(rt_ctx* c, rt_ctx::CamBuf& B, const rt_frame* f, const Scene
         HIP_TRY(c, hipGetLastError());
     }
     if (!capturing) {
-        HIP_TRY(c, hipMemcpyAsync(B.h_tot, tot, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
-        HIP_TRY(c, hipMemcpyAsync(B.h_tot + 1, B.stat, 8 * sizeof(unsigned), hipMemcpyDeviceToHost, st));
-        HIP_TRY(c, hipEventRecord(B.ev_tot, st));
+        HIP_TRY(c, hipEventRecord(B.ev_tot, st));  // rt_cb_keys_rest wrote h_tot
         B.tot_pending = true;
         HIP_TRY(c, hipEventRecord(B.ev1, st));
         B.timed = true;
