@@ -375,7 +375,11 @@ def main():
                          "RCCL's init, all-reduce and gather on a 1-GPU box)")
     ap.add_argument("--frame-sha", action="store_true",
                     help="rank 0 adds the SHA-256 of the last assembled RGBA8 frame (bottom row first)")
+    ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
+                    help="context option (rt_amd.OPTIONS) for an A/B run, e.g. --option bounce_refill=1; "
+                         "none changes an image")
     args = ap.parse_args()
+    ctx_opts = {k: float(v) for k, v in (o.split("=", 1) for o in args.option)}
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -401,7 +405,7 @@ def main():
     path = scene_path(name)
     scene = rt_amd.Scene(path, W, H, depth)
     t_cold = time.perf_counter()
-    ctx = rt_amd.Context(device)
+    ctx = rt_amd.Context(device, **ctx_opts)
     torch.cuda.synchronize()
     t_up = time.perf_counter()
     ctx.upload(scene)  # device copy + cone/cluster prepasses + light-buffer build (synchronous)
@@ -612,7 +616,8 @@ def main():
                                       ((f" + RCCL gather to rank 0 (double-buffered, {args.gather_batch} frame(s) "
                                         f"per collective, {args.gather_channels} B/px)" if args.dist_backend == "nccl"
                                         else " + gloo gather to rank 0 through host memory") if use_dist else ""),
-                       "slab_imbalance": round(imbalance, 3) if imbalance is not None else None},
+                       "slab_imbalance": round(imbalance, 3) if imbalance is not None else None,
+                       **({"options": ctx_opts} if ctx_opts else {})},
             "total_rays_per_s_M": round((tot_primary + tot_bounce + tot_shadow) * args.steps / elapsed / 1e6, 3),
             "rays_per_frame": {"primary": int(tot_primary), "bounce": int(tot_bounce), "shadow": int(tot_shadow)},
             "kernel_ms": round(kernel_ms, 4),

@@ -248,7 +248,12 @@ enum {
                                    enqueued (1) / in the context's state on the
                                    caller's stream (0, default: the ring measured no
                                    gain — the build's waves wait for the trace
-                                   kernel's to retire) */
+                                   kernel's to retire) */,
+    RT_OPT_BOUNCE_REFILL = 10   /* launch (ABI 5): scenes with bounces render with the
+                                   lane-refill kernel (persistent waves whose lanes take
+                                   a new pixel as soon as their ray tree ends) (1) / one
+                                   pixel per lane (0, default: the refill measured no
+                                   gain) */
 };
 int rt_set_option(rt_ctx*, int32_t option, double value);
 int rt_get_option(rt_ctx*, int32_t option, double* value);

@@ -358,6 +358,224 @@ __global__ __launch_bounds__(RT_TRACE_LB) __attribute__((amdgpu_waves_per_eu(wav
     }
 }
 
+// Lane refill for the bounce kernels (RT_OPT_BOUNCE_REFILL, an A/B switch;
+// off by default).  rt_trace_kernel<MAXD> gives each lane one pixel and walks
+// its ray tree to the end, so a wave runs as long as its deepest tree and the
+// lanes whose trees end early idle.  Here a persistent wave keeps its lanes
+// busy instead: each loop iteration advances every busy lane by one trace of
+// its depth-first walk and the unwinds up to its next trace, so the busy
+// lanes trace together; lanes whose pixel is done
+// take the next items of the wave's pool by ballot + prefix count.  The wave
+// claims pools of kRefillChunk 8 x 8 tiles (tile-major, so lanes start on
+// neighbouring pixels) with one atomic on work[0].  Every lane runs the same
+// per-ray arithmetic as radiance<MAXD>, so the images are the same bits.
+// Camera rays take the per-lane tests of the bounce kernels (WAVE 0); in a
+// scene without triangles the same loop as the bounce rays (closest_hit_camera
+// and closest_hit<false> differ only in the triangle loop).
+#ifndef RT_REFILL_CHUNK
+#define RT_REFILL_CHUNK 4
+#endif
+#ifndef RT_REFILL_PARTS
+#define RT_REFILL_PARTS 8
+#endif
+#ifndef RT_REFILL_STATIC
+#define RT_REFILL_STATIC 0
+#endif
+#ifndef RT_REFILL_STRIDE  // words between the parts' counters
+#define RT_REFILL_STRIDE 1024
+#endif
+constexpr unsigned kRefillChunk = RT_REFILL_CHUNK;
+constexpr unsigned kRefillParts = RT_REFILL_PARTS;
+template <int MAXD>
+__global__ __launch_bounds__(64) void rt_refill_kernel(const SceneDev S, const FrameDev F, unsigned* __restrict__ rgba,
+                                                       float* __restrict__ rgbf, unsigned* __restrict__ work, int gx,
+                                                       int gy)
+{
+    const int lane = threadIdx.x & 63;
+    const unsigned long long below = (1ull << lane) - 1ull;
+    const unsigned total = (unsigned)gx * (unsigned)gy * 64u;
+    const Color bg{F.bg[0], F.bg[1], F.bg[2]};
+    unsigned pool = 0, pool_end = 0;  // wave-uniform: the wave's unclaimed items
+    // The items are split into kRefillParts contiguous parts, one counter
+    // each; a wave starts on the part of its XCD (the workgroups are dealt
+    // round-robin to the XCDs) and moves on to the next part when that one
+    // runs dry.  One counter for the whole grid serialises the atomics.
+    unsigned part = kRefillParts > 1 ? (unsigned)blockIdx.x % kRefillParts : 0u, tries = 0;
+    bool drained = false, has = false;
+    Frame stk[MAXD];
+    Refr rf[MAXD];
+    int sp = 0;
+    float rior = 1.0f, energy = 1.0f;
+    Color ret{0.f, 0.f, 0.f};
+    bool trace = false, camera_ray = false;
+    Vec3 O{0.f, 0.f, 0.f}, D{0.f, 0.f, 0.f};
+    size_t o = 0;
+    Counters cnt;
+    for (;;) {
+        if (!drained) {
+            const unsigned long long need = __ballot(!has);
+            if (need) {
+#if RT_REFILL_STATIC  // A/B: each wave's own contiguous run of tiles, no atomics
+                if (pool == pool_end) {
+                    if (tries++ == 0) {
+                        const unsigned long long nt = total / 64u, g = gridDim.x;
+                        pool = (unsigned)(nt * blockIdx.x / g) * 64u;
+                        pool_end = (unsigned)(nt * (blockIdx.x + 1) / g) * 64u;
+                    }
+                    if (pool == pool_end) drained = true;
+                }
+#endif
+                while (pool == pool_end && !drained) {
+                    const unsigned lo = (unsigned)((unsigned long long)(total / 64u) * part / kRefillParts) * 64u;
+                    const unsigned hi = (unsigned)((unsigned long long)(total / 64u) * (part + 1) / kRefillParts) * 64u;
+                    unsigned b = 0;
+                    if (lane == 0) b = atomicAdd(work + part * RT_REFILL_STRIDE, kRefillChunk * 64u);
+                    b = lo + (unsigned)__builtin_amdgcn_readfirstlane((int)b);
+                    if (b < hi) {
+                        pool = b;
+                        pool_end = b + kRefillChunk * 64u < hi ? b + kRefillChunk * 64u : hi;
+                    } else if (++tries >= kRefillParts) {
+                        drained = true;
+                    } else {
+                        part = part + 1 < kRefillParts ? part + 1 : 0u;
+                    }
+                }
+                if (!drained) {
+                    const unsigned avail = pool_end - pool;
+                    const unsigned take = (unsigned)__popcll(need) < avail ? (unsigned)__popcll(need) : avail;
+                    const unsigned rank = (unsigned)__popcll(need & below);
+                    if (!has && rank < take) {
+                        const unsigned idx = pool + rank;
+                        const unsigned t = idx >> 6, l = idx & 63u;
+                        const int tile_x = (int)(t % (unsigned)gx), ly0 = (int)(t / (unsigned)gx) * 8;
+                        int py0 = F.row_begin + ly0, rend = F.row_end;
+                        if (F.band_rows > 0) {
+                            py0 = ((ly0 / F.band_rows) * F.band_count + F.band_index) * F.band_rows + ly0 % F.band_rows;
+                            rend = F.height;
+                        }
+                        const int px = tile_x * 8 + (int)(l & 7u), py = py0 + (int)(l >> 3);
+                        if (px < F.width && py < rend) {
+                            has = true;
+                            o = (size_t)(ly0 + (int)(l >> 3)) * F.width + px;
+                            D = camera_dir(F, px, py);
+                            O = make3(F.cam[0], F.cam[1], F.cam[2]);
+                            sp = 0;
+                            rior = 1.0f;
+                            energy = 1.0f;
+                            trace = true;
+                            camera_ray = true;
+                        }
+                    }
+                    pool += take;
+                }
+            }
+        }
+        if (!__any(has)) {
+            if (drained) break;
+            continue;
+        }
+        // one trace of radiance<MAXD>'s loop per busy lane, then its unwinds
+        // up to the next trace (the same operations in the same order: a
+        // trace that pushes goes on to its child at the next step, one that
+        // does not unwinds in this one)
+        bool pushed = false;
+        if (has && trace) {
+            float t;
+            int idx;
+            // Without triangles the camera-ray path is the generic one: one
+            // loop for camera and bounce lanes alike (a wave mixes them).
+            if (camera_ray && S.n_tri > 0) idx = closest_hit_primary<0>(S, O, D, t, cnt);
+            else idx = closest_hit<false>(S, O, D, t, cnt);
+            camera_ray = false;
+            ret = bg;
+            if (idx >= 0) {
+                const Vec3 N = hit_normal(S, idx, O, D, t);
+                const Mat m = load_mat(S, idx);
+                const Vec3 P = O + t * D;
+                const Color acc = shade_local<1, 0>(S, m, P, N, D, cnt);
+                const float er = m.kr * energy;
+                const float et = m.kt * energy;
+                const bool can = sp < F.max_bounces && sp < MAXD;
+                const bool doR = er > F.min_energy && can;
+                const bool doT = et > F.min_energy && can;
+                if (doR || doT) {
+                    Frame& fr = stk[sp];
+                    fr.acc = acc;
+                    fr.surf = idx;
+                    Vec3 Dt = D;
+                    float rior_t = rior;
+                    if (doT) {
+                        Vec3 n = N;
+                        float ratio;
+                        if (rior == m.ior) {
+                            rior_t = F.scene_ior;
+                            ratio = m.ior / F.scene_ior;
+                            n = -n;
+                        } else {
+                            rior_t = m.ior;
+                            ratio = F.scene_ior / m.ior;
+                        }
+                        Dt = refract(D, n, ratio);
+                    }
+                    O = P;
+                    if (doR) {
+                        fr.stage = doT ? 2 : 0;
+                        if (doT) rf[sp] = Refr{P, Dt, rior_t, et};
+                        D = reflect(D, N);
+                        rior = 0.0f;
+                        energy = er;
+                    } else {
+                        fr.stage = 1;
+                        D = Dt;
+                        rior = rior_t;
+                        energy = et;
+                    }
+                    ++sp;
+                    pushed = true;
+                } else {
+                    ret = acc;
+                }
+            }
+            if (!pushed) trace = false;
+        }
+        // unwind until the lane's next trace (or its end), so that at the
+        // next step every busy lane traces at once
+        while (has && !trace) {
+            if (sp == 0) {
+                if (rgbf) {
+                    rgbf[3 * o] = ret.r;
+                    rgbf[3 * o + 1] = ret.g;
+                    rgbf[3 * o + 2] = ret.b;
+                }
+                if (rgba) rgba[o] = unorm8(ret.r) | (unorm8(ret.g) << 8) | (unorm8(ret.b) << 16) | 0xFF000000u;
+                has = false;
+            } else {
+                Frame& fr = stk[sp - 1];
+                const Mat m = load_mat(S, fr.surf);
+                if (fr.stage != 1) {
+                    fr.acc += ret * m.kr;
+                    if (fr.stage == 2) {
+                        fr.stage = 1;
+                        const Refr r = rf[sp - 1];
+                        O = r.P;
+                        D = r.D;
+                        rior = r.rior;
+                        energy = r.energy;
+                        trace = true;
+                    } else {
+                        ret = fr.acc;
+                        --sp;
+                    }
+                } else {
+                    fr.acc += ret * m.kt;
+                    ret = fr.acc;
+                    --sp;
+                }
+            }
+        }
+    }
+}
+
 // Compiled bounce-stack capacities.  The host picks the smallest one that
 // covers the bounce depth the scene can actually reach.
 #define RT_STACK_DEPTHS(X) X(0) X(1) X(2) X(3) X(4) X(5) X(8) X(12) X(16) X(20) X(32)
@@ -513,6 +731,9 @@ struct rt_ctx {
     hipStream_t abuild = nullptr;
     unsigned long long ause = 0;
     bool opt_async_ring = false;
+    bool opt_refill = false;        // RT_OPT_BOUNCE_REFILL
+    unsigned* d_refill = nullptr;   // the refill kernel's work counters, one per launch of a chunked render
+    int n_cu = 0;
     std::vector<void*> deferred;  // replaced buffers an enqueued render may read: freed at the next host sync
     void* d_scan = nullptr;     // u64 scratch of the light-buffer build scans
     size_t scan_words = 0;
@@ -612,6 +833,8 @@ RT_EXPORT int rt_create(int32_t dev, rt_ctx** out)
     HIP_TRY(c, hipHostMalloc((void**)&c->h_word, 2 * sizeof(unsigned long long), hipHostMallocDefault));
     HIP_TRY(c, hipHostMalloc((void**)&c->h_cbwords, kCbWordSets * 8 * sizeof(unsigned long long), hipHostMallocDefault));
     HIP_TRY(c, hipMalloc(&c->d_stats, kStatSlots * sizeof(StatsDev)));
+    HIP_TRY(c, hipMalloc(&c->d_refill, 16 * kRefillParts * RT_REFILL_STRIDE * sizeof(unsigned)));
+    HIP_TRY(c, hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, dev));
     c->far_ladder = {2.5, 6.0, 16.0, 64.0};
     return RT_OK;
 }
@@ -740,6 +963,7 @@ RT_EXPORT int rt_set_option(rt_ctx* c, int32_t opt, double v)
         c->opt_host_chunk_mb = v;
         return RT_OK;
     case RT_OPT_ASYNC_RING: c->opt_async_ring = v != 0; return RT_OK;
+    case RT_OPT_BOUNCE_REFILL: c->opt_refill = v != 0; return RT_OK;
     case RT_OPT_CB_CAPACITY:
         if (v < 0 || v > 4e9 || v != std::floor(v)) return RT_E_ARG;
         if (v != c->opt_cb_capacity) c->cb.valid = false;
@@ -762,6 +986,7 @@ RT_EXPORT int rt_get_option(rt_ctx* c, int32_t opt, double* v)
     case RT_OPT_HOST_CHUNK_MB: *v = c->opt_host_chunk_mb; return RT_OK;
     case RT_OPT_CB_CAPACITY: *v = c->opt_cb_capacity; return RT_OK;
     case RT_OPT_ASYNC_RING: *v = c->opt_async_ring ? 1 : 0; return RT_OK;
+    case RT_OPT_BOUNCE_REFILL: *v = c->opt_refill ? 1 : 0; return RT_OK;
     default: return RT_E_ARG;
     }
 }
@@ -851,6 +1076,7 @@ RT_EXPORT void rt_destroy(rt_ctx* c)
     }
     if (c->abuild) hipStreamDestroy(c->abuild);
     hipFree(c->d_stats);
+    hipFree(c->d_refill);
     hipFree(c->d_scratch);
     if (c->ev0) hipEventDestroy(c->ev0);
     if (c->ev1) hipEventDestroy(c->ev1);
@@ -1684,6 +1910,46 @@ static void trace_dims(kernel_fn k, int width, int rows, dim3& grid, dim3& block
     lds = windows ? (unsigned)(block.x / 64 * kLdsWaveBytes) : 0u;
 }
 
+// The lane-refill kernel of a bounce-stack capacity (RT_OPT_BOUNCE_REFILL).
+static kernel_fn refill_kernel(int cap)
+{
+#define RT_REFILL(N) \
+    if (N > 0 && cap == N) return (kernel_fn)&rt_refill_kernel<(N > 0 ? N : 1)>;
+    RT_STACK_DEPTHS(RT_REFILL)
+#undef RT_REFILL
+    return nullptr;
+}
+
+// One trace launch over `rows` output rows: the tile grid, or with the
+// refill kernel persistent waves (as many as are resident at once) over the
+// same tiles, counting on work counter `slot`.
+static int launch_trace(rt_ctx* c, kernel_fn k, int cap, bool stats_on, SceneDev& S, FrameDev& F, int width,
+                        int rows, unsigned* oa, float* ob, StatsDev* stats, int slot, hipStream_t st)
+{
+    dim3 grid, block;
+    unsigned lds = 0;
+    trace_dims(k, width, rows, grid, block, lds);
+    kernel_fn rk = (c->opt_refill && cap > 0 && !stats_on) ? refill_kernel(cap) : nullptr;
+    if (rk) {
+        int per_cu = 0;
+        HIP_TRY(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)rk, 64, 0));
+        const long tiles = (long)grid.x * grid.y;
+        #ifndef RT_REFILL_GRID_MUL
+#define RT_REFILL_GRID_MUL 1
+#endif
+        const long waves = std::min(tiles, (long)std::max(1, per_cu) * std::max(1, c->n_cu) * RT_REFILL_GRID_MUL);
+        int gx = (int)grid.x, gy = (int)grid.y;
+        unsigned* work = c->d_refill + (size_t)slot * kRefillParts * RT_REFILL_STRIDE;
+        HIP_TRY(c, hipMemsetAsync(work, 0, kRefillParts * RT_REFILL_STRIDE * sizeof(unsigned), st));
+        void* args[] = {&S, &F, &oa, &ob, &work, &gx, &gy};
+        HIP_TRY(c, hipLaunchKernel((const void*)rk, dim3((unsigned)waves), dim3(64), args, 0, st));
+        return RT_OK;
+    }
+    void* args[] = {&S, &F, &oa, &ob, &stats};
+    HIP_TRY(c, hipLaunchKernel((const void*)k, grid, block, args, lds, st));
+    return RT_OK;
+}
+
 // Output rows of a launch: the slab, or this rank's band set.
 static int frame_rows(const rt_frame* f)
 {
@@ -2316,12 +2582,9 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
     const int nch = (host_out && f->band_rows == 0 && chunk > 0)
                         ? (int)std::min(8.0, std::floor((double)out_bytes / chunk))
                         : 1;
+    const bool stats_on = (f->flags & RT_FLAG_STATS) != 0;
     if (nch <= 1) {
-        dim3 grid, block;
-        unsigned lds = 0;
-        trace_dims(k, f->width, rows, grid, block, lds);
-        void* args[] = {&S, &F, &rgba_dev, &rgb_dev, &stats};
-        HIP_TRY(c, hipLaunchKernel((const void*)k, grid, block, args, lds, st));
+        if (int rc = launch_trace(c, k, cap, stats_on, S, F, f->width, rows, rgba_dev, rgb_dev, stats, 0, st)) return rc;
         if (host_out)
             HIP_TRY(c, hipMemcpyAsync(host_out, rgba_dev ? (void*)rgba_dev : (void*)rgb_dev,
                                       (size_t)rows * f->width * px_bytes, hipMemcpyDeviceToHost, st));
@@ -2337,11 +2600,7 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
             Fc.row_end = f->row_begin + r1;
             unsigned* oa = rgba_dev ? rgba_dev + (size_t)r0 * f->width : nullptr;
             float* ob = rgb_dev ? rgb_dev + (size_t)r0 * f->width * 3 : nullptr;
-            dim3 grid, block;
-            unsigned lds = 0;
-            trace_dims(k, f->width, r1 - r0, grid, block, lds);
-            void* args[] = {&S, &Fc, &oa, &ob, &stats};
-            HIP_TRY(c, hipLaunchKernel((const void*)k, grid, block, args, lds, st));
+            if (int rc = launch_trace(c, k, cap, stats_on, S, Fc, f->width, r1 - r0, oa, ob, stats, n, st)) return rc;
             HIP_TRY(c, hipEventRecord(c->ev_chunk[n], st));
         }
         if (timed) HIP_TRY(c, hipEventRecord(c->ev1, st));
