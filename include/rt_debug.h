@@ -23,7 +23,7 @@ extern "C" {
 int rt_debug_lb_info(rt_ctx*, double* out, int n);
 
 /* Camera buffer of the last build: out[0] current (0/1), out[1] entries,
- * out[2] device ms of the build's kernels, out[3] tiles, out[4] inline
+ * out[2] device ms of the last synchronous build's kernels, out[3] tiles, out[4] inline
  * records (0/1), out[5] host wall ms of the build's enqueue; out[6..9]
  * binning counters: candidate (triangle, tile) pairs tested, lists longer
  * than 256, the longest of them, the entry capacity. */
@@ -39,6 +39,11 @@ int rt_debug_cb_verify(rt_ctx*, unsigned long long* out3);
  * device copies, out[1] cone / cluster prepasses, out[2] light buffer,
  * out[3] total, out[4..8] the light-buffer build's phases. */
 int rt_debug_upload_info(rt_ctx*, double* out, int n);
+
+/* The builds' device prefix sum on host counts (n >= 1), in place like its
+ * callers: out (n + 1 words) = the exclusive prefixes then the total, both
+ * mod 2^32; *total = the 64-bit total. */
+int rt_debug_scan(int device, const unsigned* in, unsigned n, unsigned* out, unsigned long long* total);
 
 /* Run the wave-primitive self-test (wave min / max / sum, wave cones) over
  * `blocks` workgroups on `device`; *failures = lanes that disagreed. */

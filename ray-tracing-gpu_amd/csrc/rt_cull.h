@@ -396,12 +396,11 @@ __device__ __forceinline__ int closest_hit_primary(const SceneDev& S, const Vec3
     return S.use_tricam ? closest_hit_camera(S, O, D, t, cnt) : closest_hit<true>(S, O, D, t, cnt);
 }
 
-// tricam[] for camera position C (one thread per triangle).
-__global__ void rt_camera_prepass(const float4* __restrict__ tri, int n, float cx, float cy, float cz,
-                                  float4* __restrict__ tricam)
+// tricam[k] for camera position C: the camera-ray triangle values that
+// depend only on the origin (written by rt_cone_prepass's camera launch).
+__device__ __forceinline__ void camera_record(const float4* __restrict__ tri, int k, float cx, float cy, float cz,
+                                              float4* __restrict__ tricam)
 {
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n) return;
     const float4 a = tri[3 * k], b = tri[3 * k + 1], c = tri[3 * k + 2];
     const Vec3 p0 = make3(a.x, a.y, a.z), e1 = make3(a.w, b.x, b.y), e2 = make3(b.z, b.w, c.x);
     const Vec3 Sv = make3(cx, cy, cz) - p0;
@@ -493,10 +492,14 @@ __device__ double point_triangle_dist(const double* a, const double (*v)[3])
 
 __global__ void rt_cone_prepass(const float4* __restrict__ tri, const float4* __restrict__ sph,
                                 const float4* __restrict__ nrm, const float4* __restrict__ coef, int n, float ax,
-                                float ay, float az, int camera, float dtarget, float4* __restrict__ out)
+                                float ay, float az, int camera, float dtarget, float4* __restrict__ out,
+                                float4* __restrict__ tricam)
 {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
+    // the camera's tricam records in the same launch (one kernel less per
+    // camera: ~5 us of a moving frame's chain at C3)
+    if (tricam) camera_record(tri, k, ax, ay, az, tricam);
     const float4 s = sph[k], nr = nrm[k], cf = coef[k], p0 = tri[3 * k];
     const double vx = (double)s.x - ax, vy = (double)s.y - ay, vz = (double)s.z - az;
     const double dv = sqrt(vx * vx + vy * vy + vz * vz);

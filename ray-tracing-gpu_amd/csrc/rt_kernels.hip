@@ -1684,7 +1684,7 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
         }
         hipLaunchKernelGGL(rt_cone_prepass, dim3((unsigned)((ntr + 255) / 256)), dim3(256), 0, st, c->d_tri, c->d_trisph,
                            c->d_trinrm, c->d_tricoef, (int)ntr, l[0], l[1], l[2], 0, (float)(dfac * far),
-                           c->d_cone_light + kConeRec * ntr * j);
+                           c->d_cone_light + kConeRec * ntr * j, (float4*)nullptr);
         HIP_TRY(c, hipGetLastError());
         lb_dcov[j] = (double)(float)(dfac * far);
     }
@@ -1781,7 +1781,7 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
                     float4* out = d_cone_far + kConeRec * ntr * (v * nl + j);
                     hipLaunchKernelGGL(rt_cone_prepass, dim3((unsigned)((ntr + 255) / 256)), dim3(256), 0, st,
                                        c->d_tri, c->d_trisph, c->d_trinrm, c->d_tricoef, (int)ntr, l[0], l[1], l[2], 0,
-                                       (float)dfar, out);
+                                       (float)dfar, out, (float4*)nullptr);
                     HIP_TRY(c, hipGetLastError());
                     cones.push_back(out);
                     dcov.push_back((double)(float)dfar);
@@ -2009,13 +2009,9 @@ static bool camera_needs_prepass(const rt_ctx* c, const rt_frame* f, bool all_tr
 static int camera_records(rt_ctx* c, const float* cp, hipStream_t st, bool all_tricam, float4* tricam,
                           float4* cone_cam, float4* uni, float4* clu_cam)
 {
-    if (all_tricam || c->n_tri <= kTricamMaxTriangles) {
-        hipLaunchKernelGGL(rt_camera_prepass, dim3((c->n_tri + 255) / 256), dim3(256), 0, st, c->d_tri, c->n_tri,
-                           cp[0], cp[1], cp[2], tricam);
-        HIP_TRY(c, hipGetLastError());
-    }
+    float4* tc = (all_tricam || c->n_tri <= kTricamMaxTriangles) ? tricam : nullptr;
     hipLaunchKernelGGL(rt_cone_prepass, dim3((c->n_tri + 255) / 256), dim3(256), 0, st, c->d_tri, c->d_trisph,
-                       c->d_trinrm, c->d_tricoef, c->n_tri, cp[0], cp[1], cp[2], 1, 0.0f, cone_cam);
+                       c->d_trinrm, c->d_tricoef, c->n_tri, cp[0], cp[1], cp[2], 1, 0.0f, cone_cam, tc);
     HIP_TRY(c, hipGetLastError());
     if (uni) {
         hipLaunchKernelGGL(rt_cluster_prepass, dim3(1), dim3(64), 0, st, cone_cam, c->n_tri, 1, uni, c->n_tri);  // one wave
@@ -2283,7 +2279,11 @@ static int cb_build(rt_ctx* c, rt_ctx::CamBuf& B, const rt_frame* f, const Scene
     const size_t want = capturing ? B.cap : (fixed ? fixed : std::max(B.cap, cb_want_cap(B, nt)));
     if (!exact_first)
         if (int rc = cb_grow(c, B, want)) return rc;
-    if (!capturing) HIP_TRY(c, hipEventRecord(B.ev0, st));
+    // Device timing (rt_debug_cb_info) of synchronous builds only: a timing
+    // event's record drains the queue, which in an async frame is a gap of
+    // several us before and after the build (rocprofv3 timeline, C3).
+    const bool timed = !capturing && exact_first;
+    if (timed) HIP_TRY(c, hipEventRecord(B.ev0, st));
     FrameDev F;
     frame_dev(f, F);
     CbDev D = cb_dev(B, f);
@@ -2362,8 +2362,8 @@ static int cb_build(rt_ctx* c, rt_ctx::CamBuf& B, const rt_frame* f, const Scene
     if (!capturing) {
         HIP_TRY(c, hipEventRecord(B.ev_tot, st));  // rt_cb_keys_rest wrote h_tot
         B.tot_pending = true;
-        HIP_TRY(c, hipEventRecord(B.ev1, st));
-        B.timed = true;
+        if (timed) HIP_TRY(c, hipEventRecord(B.ev1, st));
+        B.timed = timed;
     }
     cb_key_of(f, B.key);
     B.tiles_x = tx;
@@ -2948,11 +2948,11 @@ RT_EXPORT int rt_debug_lb_info(rt_ctx* c, double* out, int n)
 }
 
 // Diagnostic (include/rt_debug.h): camera-buffer summary: out[0] = current
-// (0/1), out[1] = entries, out[2] = last build ms (device time of its
-// kernels, from its first to its last, plus nothing of the host), out[3] =
-// tiles, out[4] = inline records (0/1), out[5] = the build's host wall time
-// up to its last enqueue (ms); out[6..8] = block pre-cull blocks, blocks
-// that fell back to the per-tile walk, members staged over all blocks.
+// (0/1), out[1] = entries, out[2] = the last synchronous build's device ms
+// (its kernels, first to last; async builds are not timed), out[3] = tiles,
+// out[4] = inline records (0/1), out[5] = the build's host wall time up to
+// its last enqueue (ms); out[6..9] = candidate pairs, lists longer than
+// 256, the longest of them, the entry capacity.
 RT_EXPORT int rt_debug_cb_info(rt_ctx* c, double* out, int n)
 {
     if (!c || !out || n < 4) return RT_E_ARG;
@@ -3040,6 +3040,30 @@ RT_EXPORT int rt_debug_upload_info(rt_ctx* c, double* out, int n)
     // supercell counts + scan, supercell lists + cell counts + scan, entries
     for (int i = 0; i < 5 && 4 + i < n; ++i) out[4 + i] = c->lb_parts_ms[i];
     return RT_OK;
+}
+
+// Diagnostic (include/rt_debug.h): scan_u32 (the builds' device prefix sum)
+// of host counts, in place like its callers: out[0..n) the exclusive
+// prefixes mod 2^32, out[n] the total mod 2^32, *total the 64-bit total.
+RT_EXPORT int rt_debug_scan(int device, const unsigned* in, unsigned n, unsigned* out, unsigned long long* total)
+{
+    if (!in || !out || !total || n == 0) return RT_E_ARG;
+    if (hipSetDevice(device) != hipSuccess) return RT_E_HIP;
+    unsigned* d = nullptr;
+    unsigned long long* bs = nullptr;
+    int rc = RT_OK;
+    if (hipMalloc(&d, ((size_t)n + 1) * sizeof(unsigned)) != hipSuccess ||
+        hipMalloc(&bs, scan_scratch(n) * sizeof(unsigned long long)) != hipSuccess)
+        rc = RT_E_HIP;
+    unsigned long long* tot = nullptr;
+    if (rc == RT_OK && (hipMemcpy(d, in, (size_t)n * sizeof(unsigned), hipMemcpyHostToDevice) != hipSuccess ||
+                        scan_u32(d, n, d, bs, 0, &tot) != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
+                        hipMemcpy(out, d, ((size_t)n + 1) * sizeof(unsigned), hipMemcpyDeviceToHost) != hipSuccess ||
+                        hipMemcpy(total, tot, sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess))
+        rc = RT_E_HIP;
+    hipFree(d);
+    hipFree(bs);
+    return rc;
 }
 
 // Diagnostic (include/rt_debug.h): run rt_selftest_kernel over `blocks`

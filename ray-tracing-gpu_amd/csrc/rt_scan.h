@@ -7,6 +7,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 namespace rt {
 
 constexpr int kScanThreads = 256, kScanItems = 16;
@@ -88,47 +90,97 @@ __global__ __launch_bounds__(kScanThreads) void rt_scan_apply(const unsigned* in
     if (blockIdx.x == nb - 1 && threadIdx.x == 0) out[n] = (unsigned)bsum[nb];
 }
 
-// Small scans (n <= kScanSmallMax): one 1024-thread block, 64 consecutive
-// counts per thread — one launch instead of three (the per-camera builds
-// scan a count per 8x8 tile: 32,400 at 1080p).  bsum[0] = the 64-bit total.
-constexpr int kScanSmallThreads = 1024, kScanSmallItems = 64;
-constexpr unsigned kScanSmallMax = kScanSmallThreads * kScanSmallItems;
-__global__ __launch_bounds__(kScanSmallThreads) void rt_scan_small(const unsigned* in, unsigned n,
-                                                                   unsigned long long* __restrict__ bsum,
-                                                                   unsigned* out)
+// Small scans (n <= kScanSmallMax: the per-camera builds scan a count per
+// triangle, 50,176 for the C3 mesh, and per 8x8 tile, 32,400 at 1080p): two
+// launches over blocks of kScanSmallTile counts.  A block's four waves own
+// 256 consecutive counts each, as four chunks of 64 (lane l: count c * 64 +
+// l of chunk c), so every load and store is one coalesced wave access and
+// the four chunk scans are independent.  Pass 1 sums each block (bsum[b],
+// exact); pass 2 takes its block's prefix from the <= 64 sums before it (one
+// wave), scans its chunks, and block 0 writes the total.  Round 3: one
+// 1024-thread block with thread-owned runs of 64 consecutive counts made
+// each access 64 cache lines in one CU (57 us for the mesh's counts); a
+// wave walk of its chunks in series waited one load latency per chunk
+// (36 us); all chunks in registers spilled (77 us).  The prefixes are mod
+// 2^32 (the outputs are 32-bit); the total is 64-bit: bsum[nb].  out may
+// alias in (pass 2 reads each count before writing it, in the same block).
+constexpr int kScanSmallThreads = 256, kScanSmallTile = 1024;
+constexpr unsigned kScanSmallMax = 64u * kScanSmallTile;  // pass 2 sums <= 64 block totals in one wave
+__global__ __launch_bounds__(kScanSmallThreads) void rt_scan_small_reduce(const unsigned* __restrict__ in, unsigned n,
+                                                                          unsigned long long* __restrict__ bsum)
 {
-    __shared__ unsigned long long sh[kScanSmallThreads];
-    const int t = threadIdx.x;
-    const unsigned base = (unsigned)t * kScanSmallItems;
+    __shared__ unsigned long long ws[kScanSmallThreads / 64];
+    const unsigned base = blockIdx.x * (unsigned)kScanSmallTile + threadIdx.x;
     unsigned long long s = 0;
-    // all 64 loads issued before the sum (a dependent loop waited on each)
-    unsigned v[kScanSmallItems];
 #pragma unroll
-    for (int q = 0; q < kScanSmallItems; ++q) v[q] = base + q < n ? in[base + q] : 0u;
+    for (int q = 0; q < kScanSmallTile / kScanSmallThreads; ++q) {
+        const unsigned i = base + (unsigned)q * kScanSmallThreads;
+        s += i < n ? in[i] : 0u;
+    }
 #pragma unroll
-    for (int q = 0; q < kScanSmallItems; ++q) s += v[q];
-    sh[t] = s;
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = s;
     __syncthreads();
-    for (int o = 1; o < kScanSmallThreads; o <<= 1) {
-        const unsigned long long x = t >= o ? sh[t - o] : 0ull;
-        __syncthreads();
-        sh[t] += x;
-        __syncthreads();
-    }
-    unsigned long long run = sh[t] - s;
+    if (threadIdx.x == 0) bsum[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+__global__ __launch_bounds__(kScanSmallThreads) void rt_scan_small_apply(const unsigned* in, unsigned n,
+                                                                         unsigned long long* __restrict__ bsum,
+                                                                         unsigned nb, unsigned* out)
+{
+    __shared__ unsigned ws[kScanSmallThreads / 64];
+    __shared__ unsigned long long pre;
+    const int lane = (int)(threadIdx.x & 63), w = (int)(threadIdx.x >> 6);
+    const unsigned base = blockIdx.x * (unsigned)kScanSmallTile + (unsigned)w * 256u + (unsigned)lane;
+    unsigned v[4], ex[4];
 #pragma unroll
-    for (int q = 0; q < kScanSmallItems; ++q) {
-        if (base + q < n) out[base + q] = (unsigned)run;
-        run += v[q];
+    for (int c = 0; c < 4; ++c) {
+        const unsigned i = base + (unsigned)c * 64u;
+        v[c] = i < n ? in[i] : 0u;
     }
-    if (t == kScanSmallThreads - 1) {
-        out[n] = (unsigned)sh[t];
-        bsum[0] = sh[t];
+    if (w == 0) {  // this block's prefix; block 0: the total
+        const unsigned long long x = (unsigned)lane < nb ? bsum[lane] : 0ull;
+        unsigned long long p = (unsigned)lane < blockIdx.x ? x : 0ull, t = x;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            p += __shfl_xor(p, o);
+            t += __shfl_xor(t, o);
+        }
+        if (lane == 0) {
+            pre = p;
+            if (blockIdx.x == 0) {
+                out[n] = (unsigned)t;
+                bsum[nb] = t;
+            }
+        }
+    }
+    unsigned carry = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        unsigned x = v[c];
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const unsigned y = __shfl_up(x, o);
+            if (lane >= o) x += y;
+        }
+        ex[c] = carry + x - v[c];
+        carry += __shfl(x, 63);
+    }
+    if (lane == 0) ws[w] = carry;
+    __syncthreads();
+    unsigned off = (unsigned)pre;
+    for (int k = 0; k < w; ++k) off += ws[k];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const unsigned i = base + (unsigned)c * 64u;
+        if (i < n) out[i] = off + ex[c];
     }
 }
 
 // Scratch words (u64) rt_scan needs for n counts.
-inline size_t scan_scratch(size_t n) { return (n + kScanTile - 1) / kScanTile + 1; }
+inline size_t scan_scratch(size_t n)
+{
+    return std::max((n + kScanTile - 1) / kScanTile, (n + kScanSmallTile - 1) / kScanSmallTile) + 1;
+}
 
 // Exclusive scan of in[0..n) into out[0..n], out[n] = total, on stream st;
 // bsum (scan_scratch(n) u64) receives the 64-bit total at bsum[nb].  n >= 1.
@@ -136,8 +188,10 @@ inline hipError_t scan_u32(const unsigned* in, unsigned n, unsigned* out, unsign
                            unsigned long long** total_dev)
 {
     if (n <= kScanSmallMax) {
-        hipLaunchKernelGGL(rt_scan_small, dim3(1), dim3(kScanSmallThreads), 0, st, in, n, bsum, out);
-        if (total_dev) *total_dev = bsum;
+        const unsigned nb = (n + kScanSmallTile - 1) / kScanSmallTile;
+        hipLaunchKernelGGL(rt_scan_small_reduce, dim3(nb), dim3(kScanSmallThreads), 0, st, in, n, bsum);
+        hipLaunchKernelGGL(rt_scan_small_apply, dim3(nb), dim3(kScanSmallThreads), 0, st, in, n, bsum, nb, out);
+        if (total_dev) *total_dev = bsum + nb;
         return hipGetLastError();
     }
     const unsigned nb = (unsigned)((n + kScanTile - 1) / kScanTile);

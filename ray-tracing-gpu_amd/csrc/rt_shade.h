@@ -606,9 +606,11 @@ __device__ __forceinline__ bool lb_walk_lds(const SceneDev& S, bool use, int cel
 // PIPE: the per-lane walk issues the next entry's gathers before the
 // current entry's test (long lists: C3, C5); without it the walk holds 12
 // fewer VGPRs (short lists).
+// pre: the lanes' cell list bounds [pe, pn) were loaded ahead (lb_prefetch:
+// every lane that can use the slot has them).
 template <bool PIPE>
 __device__ __forceinline__ bool lb_slot(const SceneDev& S, int slot, const Vec3 P, const Vec3 L, float dist, bool cand,
-                                        bool& occ, Counters& cnt)
+                                        bool& occ, Counters& cnt, bool pre = false, unsigned pe = 0, unsigned pn = 0)
 {
     const float4 m0 = S.lb_meta[2 * slot], m1 = S.lb_meta[2 * slot + 1];
     const unsigned obase = __float_as_uint(m0.x), dbase = __float_as_uint(m0.y), ndcap = __float_as_uint(m0.z);
@@ -638,8 +640,16 @@ __device__ __forceinline__ bool lb_slot(const SceneDev& S, int slot, const Vec3 
     constexpr bool lds_one = false;
 #endif
     if (one_cell && !lds_one) {
-        const unsigned* o = S.lb_off + obase + cf;
-        const unsigned q0 = o[0], q1 = o[1];
+        unsigned q0, q1;
+        if (pre) {
+            const int fl = (int)__builtin_ctzll(bu);
+            q0 = (unsigned)__builtin_amdgcn_readlane((int)pe, fl);
+            q1 = (unsigned)__builtin_amdgcn_readlane((int)pn, fl);
+        } else {
+            const unsigned* o = S.lb_off + obase + cf;
+            q0 = o[0];
+            q1 = o[1];
+        }
 #ifdef RT_ABLATE_LBCELL  // timing-only build: no cell walk
         for (unsigned q = q0; q < q0; ++q) {
 #else
@@ -664,9 +674,14 @@ __device__ __forceinline__ bool lb_slot(const SceneDev& S, int slot, const Vec3 
             }
         }
     } else if (use) {
-        const unsigned* o = S.lb_off + obase + cell;
-        e = o[0];
-        end = o[1];
+        if (pre) {
+            e = pe;
+            end = pn;
+        } else {
+            const unsigned* o = S.lb_off + obase + cell;
+            e = o[0];
+            end = o[1];
+        }
     }
 #if RT_LB_LDS
     if ((RT_LB_LDS & (PIPE ? 1 : 2)) && (!one_cell || lds_one) && bu && lb_walk_lds(S, use, cell, e, end, P, L, dist, occ, cnt))
@@ -772,7 +787,8 @@ __device__ __forceinline__ bool lb_slot(const SceneDev& S, int slot, const Vec3 
 // no buffer covers take the per-lane loop over every triangle.
 template <bool PIPE>
 __device__ __forceinline__ void shadow_opaque_lb(const SceneDev& S, int l, const Vec3 P, const Vec3 L, float dist,
-                                                 bool& occ, Counters& cnt)
+                                                 bool& occ, Counters& cnt, bool pre = false, unsigned pe = 0,
+                                                 unsigned pn = 0)
 {
     for (int k = 0; k < S.n_plane_opaque; ++k) {
         if (!__any(!occ)) return;
@@ -782,7 +798,7 @@ __device__ __forceinline__ void shadow_opaque_lb(const SceneDev& S, int l, const
     {
     const float mx = fmaxf(fabsf(L.x), fmaxf(fabsf(L.y), fabsf(L.z)));
     const bool cand = !occ & (mx >= 0.5f);  // a direction the lookup takes
-    bool use = lb_slot<PIPE>(S, l, P, L, dist, cand, occ, cnt);
+    bool use = lb_slot<PIPE>(S, l, P, L, dist, cand, occ, cnt, pre, pe, pn);
     if constexpr (PIPE) {  // big lists: lanes beyond a buffer take the next
         for (int lv = 1; lv < S.lb_R; ++lv) {
             if (!__any(cand & !use & !occ)) break;
@@ -849,7 +865,11 @@ __device__ __forceinline__ void add_light(Color& res, const Mat& m, const float4
         // pow(x, 0) == 1 for every x (C99 F.9.4.4, glibc and ocml alike):
         // materials without a shininess never pay for powf.
         float pw = 1.0f;
+#ifdef RT_ABLATE_POWF  // timing-only build: no powf
+        if (m.shin != 0.0f) pw = ps * m.shin;
+#else
         if (m.shin != 0.0f) pw = powf(ps, m.shin);
+#endif
         const float pf = l0.w * m.ks * pw;
         res += LC * pf;
     }
@@ -857,6 +877,33 @@ __device__ __forceinline__ void add_light(Color& res, const Mat& m, const float4
 
 #ifndef RT_LB_PIPE
 #define RT_LB_PIPE(WAVE) (((WAVE) & 2) != 0)
+#endif
+
+// Light li's level-0 cell list bounds for every lane that can use its
+// buffer (gate, a direction the lookup takes, within dcov): the same light
+// vector, distance and cell lb_slot computes, loaded one light ahead so the
+// gathers overlap the previous light's walk instead of heading its own
+// dependent chain (cell -> bounds -> entries).
+__device__ __forceinline__ void lb_prefetch(const SceneDev& S, int li, const Vec3 P, const Vec3 N, bool active,
+                                            unsigned& e, unsigned& n)
+{
+    const float4 l0 = S.lights[2 * li];
+    const Vec3 Lr = make3(l0.x, l0.y, l0.z) - P;
+    const bool gate = active & (dot(Lr, N) > 0);
+    const float dist = sqrt_w(Lr.x * Lr.x + Lr.y * Lr.y + Lr.z * Lr.z);
+    const Vec3 L = Lr * recip_w(dist);
+    const float4 m0 = S.lb_meta[2 * li], m1 = S.lb_meta[2 * li + 1];
+    const int R = __float_as_int(m0.w);
+    const float mx = fmaxf(fabsf(L.x), fmaxf(fabsf(L.y), fabsf(L.z)));
+    e = n = 0;
+    if (gate & (mx >= 0.5f) & (dist <= m1.x) & (R > 0)) {
+        const unsigned* o = S.lb_off + __float_as_uint(m0.x) + lb_cell(-L, R);
+        e = o[0];
+        n = o[1];
+    }
+}
+#ifndef RT_LB_PREFETCH
+#define RT_LB_PREFETCH 0
 #endif
 template <int kLightBatch, int WAVE>
 __device__ __forceinline__ Color shade_local(const SceneDev& S, const Mat& m, const Vec3 P, const Vec3 N,
@@ -878,7 +925,13 @@ __device__ __forceinline__ Color shade_local(const SceneDev& S, const Mat& m, co
         return res;
     }
     if constexpr ((WAVE & 4) != 0) {  // light buffer: one light at a time, file order
+        // small lists: the next light's cell bounds are loaded a light ahead
+        constexpr bool PF = RT_LB_PREFETCH && !RT_LB_PIPE(WAVE);
+        unsigned ne = 0, nn = 0;
+        if (PF && S.n_lights > 0) lb_prefetch(S, 0, P, N, active, ne, nn);
         for (int li = 0; li < S.n_lights; ++li) {
+            const unsigned ce = ne, cn = nn;
+            if (PF && li + 1 < S.n_lights) lb_prefetch(S, li + 1, P, N, active, ne, nn);
             const float4 l0 = S.lights[2 * li], l1 = S.lights[2 * li + 1];
             const Vec3 Lr = make3(l0.x, l0.y, l0.z) - P;
             const bool gate = active & (dot(Lr, N) > 0);  // Scene.cpp:1756, unnormalised
@@ -888,7 +941,7 @@ __device__ __forceinline__ Color shade_local(const SceneDev& S, const Mat& m, co
             bool occ = !gate;
             RT_MARK(cnt, 2);
 #ifndef RT_ABLATE_SHADOW
-            shadow_opaque_lb<RT_LB_PIPE(WAVE)>(S, li, P, L, dist, occ, cnt);
+            shadow_opaque_lb<RT_LB_PIPE(WAVE)>(S, li, P, L, dist, occ, cnt, PF, ce, cn);
 #endif
             RT_MARK(cnt, 7);
             if (gate) {
