@@ -495,14 +495,21 @@ def main():
     run_tests = st.triangle_tests + st.plane_tests + st.quadric_tests
 
     counter = [0]
+    # the C entry point with its arguments converted once: the Python
+    # wrapper's per-call conversions (~10 us) would otherwise bound the
+    # launch rate of small frames (C1: 10 us kernels)
+    render_async = L.rt_render_async
+    c_ctx, c_frame, c_stream = ctx._h, ctypes.byref(frame), ctypes.c_void_p(stream)
+    c_single = ctypes.c_void_p(single.data_ptr())
 
     def step(ev=None):
         k = counter[0]
         counter[0] += 1
-        out = gather.target(k) if gather else single
+        out = ctypes.c_void_p(gather.target(k).data_ptr()) if gather else c_single
         if ev is not None:
             ev[0].record()
-        ctx.render_async(frame, out.data_ptr(), 0, stream)
+        if render_async(c_ctx, c_frame, out, None, c_stream) != 0:
+            raise RuntimeError(f"rt_render_async: {ctx._err()}")
         if ev is not None:
             ev[1].record()
         if gather:
