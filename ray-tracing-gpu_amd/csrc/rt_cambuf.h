@@ -15,7 +15,7 @@
 // evaluated only for (triangle, tile) pairs whose tile lies in the
 // triangle's screen box — a box that provably contains every tile where the
 // test can pass (cb_box below) — instead of every tile walking every
-// cluster.  Per camera: rt_cb_tiles (the tile cones), rt_cb_boxes and a
+// cluster.  Per camera: rt_cb_tiles_boxes (the tile cones, the boxes) and a
 // scan of their sizes (the candidate pairs), rt_cb_pairs<false> (the test
 // of every pair: a count per tile, a pass mask per run of 64), a scan
 // (offsets), rt_cb_pairs<true> (each passing pair at an atomic slot of its
@@ -72,11 +72,11 @@ struct CbDev {
 // outside the frame's rows, with a degenerate cone, or wider than the bound
 // the boxes assume (cosW < cos_wbound; never seen: the bound is analytic)
 // gets no list.  Also zeroes the counts and cursors.
-__global__ __launch_bounds__(256) void rt_cb_tiles(const FrameDev F, CbDev B)
+__device__ __forceinline__ void cb_tiles_block(const FrameDev& F, const CbDev& B, unsigned blk)
 {
-    if (blockIdx.x == 0 && threadIdx.x < 8) B.stat[threadIdx.x] = 0u;  // the build's counters
+    if (blk == 0 && threadIdx.x < 8) B.stat[threadIdx.x] = 0u;  // the build's counters
     const int lane = (int)(threadIdx.x & 63);
-    const int t = (int)(blockIdx.x * 4 + (threadIdx.x >> 6));
+    const int t = (int)(blk * 4 + (threadIdx.x >> 6));
     const int nt = B.tiles_x * B.tiles_y;
     if (t >= nt) return;  // wave-uniform
     const int tx = t % B.tiles_x, ty = t / B.tiles_x;
@@ -246,7 +246,7 @@ __device__ __forceinline__ CbBox cb_box(const float4 c0, const float4* e, const 
     return CbBox{x0, y0, x1 - x0 + 1, y1 - y0 + 1};
 }
 
-// The camera wave test of triangle k's records for tile t (rt_cb_tiles'
+// The camera wave test of triangle k's records for tile t (cb_tiles_block's
 // cone); false for a tile without a list.
 __device__ __forceinline__ bool cb_pair_test(const CbDev& B, int t, const float4 c0, float sinT, const float4* e)
 {
@@ -263,7 +263,7 @@ __device__ __forceinline__ bool cb_pair_test(const CbDev& B, int t, const float4
 
 // Small lists (no clusters, <= 1,024 triangles): one wave per tile tests
 // every triangle, 64 per ballot — the binning's launches would cost more
-// than this walk (C2: 12 triangles).  The tile's cone is rt_cb_tiles' (and
+// than this walk (C2: 12 triangles).  The tile's cone is cb_tiles_block's (and
 // stored like it, for rt_debug_cb_verify); FILL false: the count, true: the
 // entries in triangle order at the tile's offset (the keys sort them).
 template <bool FILL>
@@ -320,9 +320,9 @@ __global__ __launch_bounds__(256) void rt_cb_walk(const SceneDev S, const FrameD
 
 // Triangle boxes (one thread per triangle): box[k] = (tx0, ty0, nx, nx*ny),
 // tcnt[k] = nx * ny, the candidate pairs the pair passes expand.
-__global__ __launch_bounds__(256) void rt_cb_boxes(const SceneDev S, const FrameDev F, CbDev B)
+__device__ __forceinline__ void cb_boxes_block(const SceneDev& S, const FrameDev& F, const CbDev& B, unsigned blk)
 {
-    const int k = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    const int k = (int)(blk * 256 + threadIdx.x);
     if (k >= S.n_tri) return;
     const float4* e = S.cone_cam + 2 * (size_t)S.n_tri + 3 * (size_t)k;
     const float4 e3[3] = {e[0], e[1], e[2]};
@@ -332,11 +332,64 @@ __global__ __launch_bounds__(256) void rt_cb_boxes(const SceneDev S, const Frame
     B.tcnt[k] = n;
 }
 
+// One launch for both (they are independent): the boxes' blocks first
+// (fewer, each a long chain of double-precision steps per thread), then the
+// tile cones' — one launch less per camera, and the tiles fill the machine
+// while the boxes' few waves run (rocprofv3, C3: 8 + 25 us in series).
+__global__ __launch_bounds__(256) void rt_cb_tiles_boxes(const SceneDev S, const FrameDev F, CbDev B, unsigned nbb)
+{
+    if (blockIdx.x < nbb) cb_boxes_block(S, F, B, blockIdx.x);
+    else cb_tiles_block(F, B, blockIdx.x - nbb);
+}
+
+// One run of 64 pairs for the calling wave: each lane's owner triangle
+// (searched from lo, which moves to the run's last owner), its tile and
+// dmin; pass = the camera wave test (COUNT) or the run's pass-mask bit.
+template <bool FILL>
+__device__ __forceinline__ bool cb_run(const SceneDev& S, const CbDev& B, unsigned run, unsigned np,
+                                       unsigned long long mask, int& lo, int& own, int& t, float& dmin)
+{
+    const int lane = (int)(threadIdx.x & 63);
+    const unsigned p = run * 64 + (unsigned)lane;
+    own = -1;
+    for (int base = lo; base < S.n_tri; base += 64) {
+        // window of 64 owners: lane j holds pre[base + j]
+        const int kj = base + lane;
+        const unsigned pj = kj < S.n_tri ? B.tcnt[kj] : 0xFFFFFFFFu;
+        // my owner in this window: the last j with pre[base + j] <= p
+        int j = (unsigned)__shfl((int)pj, 0) <= p ? 0 : -1;
+        for (int step = 32; step > 0; step >>= 1) {
+            const int c = j + step;
+            const unsigned pc = (unsigned)__shfl((int)pj, c & 63);
+            if (c <= 63 && pc <= p) j = c;
+        }
+        // j = 63 with the next window's first prefix <= p: look further
+        const bool beyond = j == 63 && base + 64 < S.n_tri && B.tcnt[base + 64] <= p;
+        if (own < 0 && j >= 0 && !beyond) own = base + j;
+        if (!__any(own < 0 && p < np)) break;
+    }
+    // the next run starts at this run's last owner
+    lo = __builtin_amdgcn_readlane(own < 0 ? lo : own, 63);
+    bool pass = false;
+    t = 0;
+    dmin = 0.0f;
+    if (p < np && own >= 0 && ((mask >> lane) & 1ull)) {
+        const int k = own;
+        const int4 bx = B.box[k];
+        const unsigned q = p - B.tcnt[k];
+        t = (bx.y + (int)(q / (unsigned)bx.z)) * B.tiles_x + bx.x + (int)(q % (unsigned)bx.z);
+        const float4 c1 = S.cone_cam[2 * k + 1];
+        dmin = c1.x;
+        pass = FILL || cb_pair_test(B, t, S.cone_cam[2 * k], c1.w, S.cone_cam + 2 * (size_t)S.n_tri + 3 * (size_t)k);
+    }
+    return pass;
+}
+
 // One pass over every candidate (triangle, tile) pair, one pair per lane:
 // a fixed grid of waves, each taking a contiguous range of runs of 64
 // consecutive pairs (the pairs of triangle k are [pre[k], pre[k + 1]), pre
 // = the exclusive scan of the box sizes).  The range's first owner comes
-// from a binary search over pre[]; every run then finds its lanes' owners
+// from a 64-way ballot search over pre[]; every run then finds its lanes' owners
 // among the next 64 triangles' prefixes (a search over lanes by shuffles;
 // another window for runs that cross more than 64 triangles), starting
 // from the previous run's last owner.
@@ -381,38 +434,9 @@ __global__ __launch_bounds__(256) void rt_cb_pairs(const SceneDev S, CbDev B)
             mask = B.rmask[run];
             if (!mask) continue;  // no passing pair: nothing to place (wave-uniform)
         }
-        const unsigned p = run * 64 + (unsigned)lane;
-        int own = -1;
-        for (int base = lo; base < S.n_tri; base += 64) {
-            // window of 64 owners: lane j holds pre[base + j]
-            const int kj = base + lane;
-            const unsigned pj = kj < S.n_tri ? B.tcnt[kj] : 0xFFFFFFFFu;
-            // my owner in this window: the last j with pre[base + j] <= p
-            int j = (unsigned)__shfl((int)pj, 0) <= p ? 0 : -1;
-            for (int step = 32; step > 0; step >>= 1) {
-                const int c = j + step;
-                const unsigned pc = (unsigned)__shfl((int)pj, c & 63);
-                if (c <= 63 && pc <= p) j = c;
-            }
-            // j = 63 with the next window's first prefix <= p: look further
-            const bool beyond = j == 63 && base + 64 < S.n_tri && B.tcnt[base + 64] <= p;
-            if (own < 0 && j >= 0 && !beyond) own = base + j;
-            if (!__any(own < 0 && p < np)) break;
-        }
-        // the next run starts at this run's last owner
-        lo = __builtin_amdgcn_readlane(own < 0 ? lo : own, 63);
-        bool pass = false;
-        int t = 0;
-        float dmin = 0.0f;
-        if (p < np && own >= 0 && ((mask >> lane) & 1ull)) {
-            const int k = own;
-            const int4 bx = B.box[k];
-            const unsigned q = p - B.tcnt[k];
-            t = (bx.y + (int)(q / (unsigned)bx.z)) * B.tiles_x + bx.x + (int)(q % (unsigned)bx.z);
-            const float4 c1 = S.cone_cam[2 * k + 1];
-            dmin = c1.x;
-            pass = FILL || cb_pair_test(B, t, S.cone_cam[2 * k], c1.w, S.cone_cam + 2 * (size_t)S.n_tri + 3 * (size_t)k);
-        }
+        int own, t;
+        float dmin;
+        const bool pass = cb_run<FILL>(S, B, run, np, mask, lo, own, t, dmin);
         if (!FILL) {
             const unsigned long long m = __ballot(pass);
             if (run < B.rcap) {

@@ -2229,7 +2229,7 @@ static CbDev cb_dev(const rt_ctx::CamBuf& B, const rt_frame* f)
     // the widest tile cone: lanes lie within 4 pixels of the reference lane
     // in each axis, and on the film plane z = -1 (|d0| >= 1) an angle is at
     // most the distance; wave_cone lowers the cosine by 1e-6 (plus < 5e-7
-    // of rounding).  rt_cb_tiles checks every tile against it: a wider tile
+    // of rounding).  rt_cb_tiles_boxes checks every tile against it: a wider tile
     // gets no list, so the bound is an efficiency matter, not a correctness one.
     const double px = 2.0 * f->half_w * (double)f->inv_w, py = 2.0 * f->half_h * (double)f->inv_h;
     const double amax = std::min(1.0, std::sqrt(16.0 * px * px + 16.0 * py * py) * 1.001);
@@ -2306,8 +2306,8 @@ static int cb_build(rt_ctx* c, rt_ctx::CamBuf& B, const rt_frame* f, const Scene
         }
         hipLaunchKernelGGL(rt_cb_walk<true>, dim3(tb), dim3(256), 0, st, S, F, D);
     } else {
-    hipLaunchKernelGGL(rt_cb_tiles, dim3(tb), dim3(256), 0, st, F, D);
-    hipLaunchKernelGGL(rt_cb_boxes, dim3((unsigned)((c->n_tri + 255) / 256)), dim3(256), 0, st, S, F, D);
+    const unsigned nbb = (unsigned)((c->n_tri + 255) / 256);
+    hipLaunchKernelGGL(rt_cb_tiles_boxes, dim3(nbb + tb), dim3(256), 0, st, S, F, D, nbb);
     HIP_TRY(c, hipGetLastError());
     HIP_TRY(c, scan_u32(B.tcnt, (unsigned)c->n_tri, B.tcnt, (unsigned long long*)B.scan, st, nullptr));
     if (exact_first) {  // the pass masks sized to the candidate pairs (one read back)
