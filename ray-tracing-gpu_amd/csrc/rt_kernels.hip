@@ -1396,19 +1396,19 @@ static int lb_build(rt_ctx* c, int ntr, int n_opaque, const std::vector<const fl
             c->err = "light buffer too large";
             goto done;
         }
-        LB_TRY(hipMalloc(&c->d_lb_ent, std::max<size_t>(total, 1) * kLbEnt * sizeof(float4)));
-        LB_TRY(hipMalloc(&c->d_lb_dcap, std::max<size_t>(dperm_all.size(), 1) * kLbEnt * sizeof(float4)));
+        LB_TRY(hipMalloc(&c->d_lb_ent, std::max<size_t>(total, 1) * kLbEntF * sizeof(float)));
+        LB_TRY(hipMalloc(&c->d_lb_dcap, std::max<size_t>(dperm_all.size(), 1) * kLbEntF * sizeof(float)));
         LB_TRY(hipMalloc(&c->d_lb_meta, std::max(nl, 1) * 2 * sizeof(float4)));
         std::vector<float4> meta((size_t)std::max(nl, 1) * 2);
         for (int j = 0; j < nl; ++j) {
             const Slot& b = B[j];
             hipLaunchKernelGGL(rt_lb_cells, dim3(b.nsup), dim3(256), 0, st, cones[j], ntr, c->d_tri, b.R,
-                               (float)dcov[j], d_soff + b.sob, d_slists, c->d_lb_off + b.ob, nullptr, c->d_lb_ent);
+                               (float)dcov[j], d_soff + b.sob, d_slists, c->d_lb_off + b.ob, nullptr, (float*)c->d_lb_ent);
             LB_TRY(hipGetLastError());
             if (b.ndperm) {
                 hipLaunchKernelGGL(rt_lb_dcap, dim3((unsigned)((b.ndperm + 255) / 256)), dim3(256), 0, st, cones[j],
                                    c->d_tri, d_perm + perm_all.size() + b.dperm0, (int)b.ndperm,
-                                   c->d_lb_dcap + kLbEnt * b.dperm0);
+                                   (float*)c->d_lb_dcap + kLbEntF * b.dperm0);
                 LB_TRY(hipGetLastError());
             }
             unsigned obj = (unsigned)b.ob, db = (unsigned)b.dperm0, nd = (unsigned)b.ndperm;

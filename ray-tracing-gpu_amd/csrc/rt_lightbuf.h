@@ -30,7 +30,12 @@ namespace rt {
 // per-light list sorted by dcap, tested by the lanes with dist > dcap — the
 // per-lane predicate light_reach, split in two.
 constexpr int kLbGroup = 16;  // cells per supercell edge (two-level build)
-constexpr int kLbEnt = 3;     // float4 per light-buffer entry (48 B)
+// Light-buffer entry: 10 floats (40 B, 8-byte aligned) — [p0, key] [e1,
+// e2.x] [e2.y, e2.z]; RT_LB_E40 0 pads it to 48 B (the round-2 layout).
+#ifndef RT_LB_E40
+#define RT_LB_E40 1
+#endif
+constexpr int kLbEntF = RT_LB_E40 ? 10 : 12;  // floats per light-buffer entry
 
 __device__ __forceinline__ int lb_cell(const Vec3 d, int R)
 {
@@ -175,23 +180,44 @@ __global__ __launch_bounds__(256) void rt_lb_super(const float4* __restrict__ co
     if (!lists && threadIdx.x == 0) counts[s] = total;
 }
 
-// 48-byte light-buffer entry of triangle k (its tri[] record):
-//   [p0, key] [e1, e2.x] [e2.y e2.z, 0, 0]
+// Light-buffer entry of triangle k (its tri[] record), kLbEntF floats:
+//   [p0, key] [e1, e2.x] [e2.y e2.z]
 // key = dmin (cell lists) or dcap (dcap list).  (A per-lane cone test in
 // front of the exact test was measured to spare no wave any exact test: a
-// cell's list is already what its lanes' cones can reach.)
-// e2.y, e2.z of entry r: an 8-byte load (the entry's last 8 bytes are pad)
-__device__ __forceinline__ float2 lb_tail(const float4* r)
+// cell's list is already what its lanes' cones can reach.)  Read as two
+// 16-byte and one 8-byte load at 8-byte alignment.
+typedef float lb_v4 __attribute__((ext_vector_type(4), aligned(8)));
+typedef float lb_v2 __attribute__((ext_vector_type(2), aligned(8)));
+__device__ __forceinline__ const float* lb_rec(const float4* base, size_t q)
 {
-    return *reinterpret_cast<const float2*>(r + 2);
+    return reinterpret_cast<const float*>(base) + kLbEntF * q;
+}
+__device__ __forceinline__ float4 lb_a(const float* r)
+{
+    const lb_v4 v = *reinterpret_cast<const lb_v4*>(r);
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ float4 lb_b(const float* r)
+{
+    const lb_v4 v = *reinterpret_cast<const lb_v4*>(r + 4);
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ float2 lb_tail(const float* r)
+{
+    const lb_v2 v = *reinterpret_cast<const lb_v2*>(r + 8);
+    return make_float2(v.x, v.y);
 }
 
-__device__ __forceinline__ void lb_write(float4* o, const float4* __restrict__ tri, int k, float key)
+__device__ __forceinline__ void lb_write(float* o, const float4* __restrict__ tri, int k, float key)
 {
     const float4 a = tri[3 * k], b = tri[3 * k + 1], c = tri[3 * k + 2];
-    o[0] = make_float4(a.x, a.y, a.z, key);
-    o[1] = make_float4(a.w, b.x, b.y, b.z);
-    o[2] = make_float4(b.w, c.x, 0.0f, 0.0f);
+    lb_v2* w = reinterpret_cast<lb_v2*>(o);
+    w[0] = lb_v2{a.x, a.y};
+    w[1] = lb_v2{a.z, key};
+    w[2] = lb_v2{a.w, b.x};
+    w[3] = lb_v2{b.y, b.z};
+    w[4] = lb_v2{b.w, c.x};
+    if (kLbEntF == 12) w[5] = lb_v2{0.0f, 0.0f};
 }
 
 // Build pass 2: one thread per cell of a supercell, over the supercell's
@@ -199,7 +225,7 @@ __device__ __forceinline__ void lb_write(float4* o, const float4* __restrict__ t
 __global__ __launch_bounds__(256) void rt_lb_cells(const float4* __restrict__ cone, int n, const float4* __restrict__ tri,
                                                    int R, float dcov, const unsigned* __restrict__ soffs,
                                                    const int* __restrict__ slists, const unsigned* __restrict__ coffs,
-                                                   unsigned* __restrict__ ccounts, float4* __restrict__ ent)
+                                                   unsigned* __restrict__ ccounts, float* __restrict__ ent)
 {
     const int G = R / kLbGroup;
     const int s = blockIdx.x;
@@ -226,7 +252,7 @@ __global__ __launch_bounds__(256) void rt_lb_cells(const float4* __restrict__ co
         for (int x = 0; x < m; ++x) {
             const float4 c0 = rec[kConeRec * x], c1 = rec[kConeRec * x + 1];
             if (!lb_keep(wc, c0, c1, rec + kConeRec * x + 2, dcov)) continue;
-            if (ent) lb_write(ent + kLbEnt * (size_t)out++, tri, kid[x], c1.x);
+            if (ent) lb_write(ent + kLbEntF * (size_t)out++, tri, kid[x], c1.x);
             else ++cnt;
         }
     }
@@ -235,13 +261,13 @@ __global__ __launch_bounds__(256) void rt_lb_cells(const float4* __restrict__ co
 
 // The dcap list of one light: entries of perm (sorted by dcap), key = dcap.
 __global__ void rt_lb_dcap(const float4* __restrict__ cone, const float4* __restrict__ tri, const int* __restrict__ perm,
-                           int m, float4* __restrict__ out)
+                           int m, float* __restrict__ out)
 {
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= m) return;
     const int k = perm[q];
     const float4 c1 = cone[2 * k + 1];
-    lb_write(out + kLbEnt * (size_t)q, tri, k, c1.z == c1.z ? c1.z : -INFINITY);
+    lb_write(out + kLbEntF * (size_t)q, tri, k, c1.z == c1.z ? c1.z : -INFINITY);
 }
 
 }  // namespace rt

@@ -527,9 +527,9 @@ __device__ __forceinline__ bool lb_walk_lds(const SceneDev& S, bool use, int cel
                 }
                 const unsigned q = q0 + k + ((unsigned)s & wmask);
                 if (((gact >> gi) & 1u) && q < q1) {
-                    const float4* r = S.lb_ent + kLbEnt * (size_t)q;
-                    win.a[s] = r[0];
-                    win.b[s] = r[1];
+                    const float* r = lb_rec(S.lb_ent, q);
+                    win.a[s] = lb_a(r);
+                    win.b[s] = lb_b(r);
                     win.c[s] = lb_tail(r);
                 }
             }
@@ -546,9 +546,9 @@ __device__ __forceinline__ bool lb_walk_lds(const SceneDev& S, bool use, int cel
                     }
                     const unsigned q = q0 + k + (wmask + 1u) + ((unsigned)rk & wmask);
                     if (((gact >> gi) & 1u) && q < q1) {
-                        const float4* r = S.lb_ent + kLbEnt * (size_t)q;
-                        pa = r[0];
-                        pb = r[1];
+                        const float* r = lb_rec(S.lb_ent, q);
+                        pa = lb_a(r);
+                        pb = lb_b(r);
                         pc = lb_tail(r);
                         pv = true;
                     }
@@ -655,13 +655,13 @@ __device__ __forceinline__ bool lb_slot(const SceneDev& S, int slot, const Vec3 
 #else
         for (unsigned q = q0; q < q1; ++q) {
 #endif
-            const float4* r = S.lb_ent + kLbEnt * (size_t)q;
-            const float4 c0 = r[0];
+            const float* r = lb_rec(S.lb_ent, q);
+            const float4 c0 = lb_a(r);
             const bool act = use & !occ & (c0.w < dist);
             if (!__any(act)) break;
             ++cnt.tri;
             RT_EV(cnt, 4);
-            const float4 c1 = r[1];
+            const float4 c1 = lb_b(r);
             const float2 c2 = lb_tail(r);
             if (act) {
                 const Vec3 e1 = make3(c1.x, c1.y, c1.z), e2 = make3(c1.w, c2.x, c2.y);
@@ -702,9 +702,9 @@ __device__ __forceinline__ bool lb_slot(const SceneDev& S, int slot, const Vec3 
     bool have = e < end;
 #endif
     if (PG && have) {
-        const float4* r = S.lb_ent + kLbEnt * (size_t)e;
-        r0 = r[0];
-        r1 = r[1];
+        const float* r = lb_rec(S.lb_ent, e);
+        r0 = lb_a(r);
+        r1 = lb_b(r);
         r2 = lb_tail(r);
     }
     for (;;) {
@@ -713,9 +713,9 @@ __device__ __forceinline__ bool lb_slot(const SceneDev& S, int slot, const Vec3 
         RT_EV(cnt, 3);
         bool go = false;
         if (!PG && act) {
-            const float4* r = S.lb_ent + kLbEnt * (size_t)e;
-            r0 = r[0];
-            r1 = r[1];
+            const float* r = lb_rec(S.lb_ent, e);
+            r0 = lb_a(r);
+            r1 = lb_b(r);
             r2 = lb_tail(r);
         }
         const float4 c0 = r0, c1 = r1;
@@ -728,9 +728,9 @@ __device__ __forceinline__ bool lb_slot(const SceneDev& S, int slot, const Vec3 
                 ++e;
                 have = e < end;
                 if (PG && have) {
-                    const float4* r = S.lb_ent + kLbEnt * (size_t)e;
-                    r0 = r[0];
-                    r1 = r[1];
+                    const float* r = lb_rec(S.lb_ent, e);
+                    r0 = lb_a(r);
+                    r1 = lb_b(r);
                     r2 = lb_tail(r);
                 }
             }
@@ -758,13 +758,13 @@ __device__ __forceinline__ bool lb_slot(const SceneDev& S, int slot, const Vec3 
 #else
     for (unsigned q = 0; q < ndcap; ++q) {
 #endif
-        const float4* r = S.lb_dcap + kLbEnt * (size_t)(dbase + q);
-        const float4 r0 = r[0];
+        const float* r = lb_rec(S.lb_dcap, dbase + q);
+        const float4 r0 = lb_a(r);
         const bool need = use & !occ & (dist > r0.w);
         if (!__any(need)) break;
         ++cnt.tri;
         RT_EV(cnt, 5);
-        const float4 r1 = r[1];
+        const float4 r1 = lb_b(r);
         const float2 r2 = lb_tail(r);
         if (need) {
             const Vec3 e1 = make3(r1.x, r1.y, r1.z), e2 = make3(r1.w, r2.x, r2.y);
