@@ -253,7 +253,14 @@ enum {
                                    lane-refill kernel (persistent waves whose lanes take
                                    a new pixel as soon as their ray tree ends) (1) / one
                                    pixel per lane (0, default: the refill measured no
-                                   gain) */
+                                   gain) */,
+    RT_OPT_LB_COMPACT = 11      /* upload (ABI 5): big lists' light-buffer cell lists
+                                   hold {triangle, key} (8 B) instead of the triangle's
+                                   40-byte record, which the walk reads from the
+                                   L2-resident triangle array: the buffer is 5x
+                                   smaller in HBM and a C3 frame reads 116 instead of
+                                   269 MB, at +8% time (C3) / +2.5% (C5) — 1 / 0
+                                   (default) */
 };
 int rt_set_option(rt_ctx*, int32_t option, double value);
 int rt_get_option(rt_ctx*, int32_t option, double* value);

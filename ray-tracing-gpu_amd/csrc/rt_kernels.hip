@@ -212,7 +212,7 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
 #endif
 constexpr int waves_per_eu(int maxd, int wave)
 {
-    return maxd != 0 ? 1 : (wave == 14 ? RT_WAVES_PER_EU_BIG : RT_WAVES_PER_EU);
+    return maxd != 0 ? 1 : ((wave & 15) == 14 ? RT_WAVES_PER_EU_BIG : RT_WAVES_PER_EU);
 }
 // COUNT: also tally the exact tests executed (the RT_FLAG_STATS launch); in
 // the timed kernels the tallies are dead and compile away.
@@ -746,6 +746,7 @@ struct rt_ctx {
     float4* d_lb_dcap = nullptr;
     float4* d_lb_meta = nullptr;
     bool lb_ready = false;
+    bool lb_idx = false;  // cell lists of {triangle, key} entries (RT_OPT_LB_COMPACT)
     int lb_levels = 0;  // buffers per light: slot = level * n_lights + light
     size_t lb_entries = 0;
     double lb_build_ms = 0.0;
@@ -774,6 +775,7 @@ struct rt_ctx {
     int opt_camera_buffer = 1;  // 0 off, 1 auto, 2 async builds for every frame
     bool opt_union = true;
     double opt_lb_scale = 0.0;
+    bool opt_lb_compact = false;
     double opt_dcov_near = 0.0;
     double opt_cb_inline_mb = 0.0;
     double opt_host_chunk_mb = 8.0;
@@ -964,6 +966,7 @@ RT_EXPORT int rt_set_option(rt_ctx* c, int32_t opt, double v)
         return RT_OK;
     case RT_OPT_ASYNC_RING: c->opt_async_ring = v != 0; return RT_OK;
     case RT_OPT_BOUNCE_REFILL: c->opt_refill = v != 0; return RT_OK;
+    case RT_OPT_LB_COMPACT: c->opt_lb_compact = v != 0; return RT_OK;
     case RT_OPT_CB_CAPACITY:
         if (v < 0 || v > 4e9 || v != std::floor(v)) return RT_E_ARG;
         if (v != c->opt_cb_capacity) c->cb.valid = false;
@@ -987,6 +990,7 @@ RT_EXPORT int rt_get_option(rt_ctx* c, int32_t opt, double* v)
     case RT_OPT_CB_CAPACITY: *v = c->opt_cb_capacity; return RT_OK;
     case RT_OPT_ASYNC_RING: *v = c->opt_async_ring ? 1 : 0; return RT_OK;
     case RT_OPT_BOUNCE_REFILL: *v = c->opt_refill ? 1 : 0; return RT_OK;
+    case RT_OPT_LB_COMPACT: *v = c->opt_lb_compact ? 1 : 0; return RT_OK;
     default: return RT_E_ARG;
     }
 }
@@ -1384,7 +1388,7 @@ static int lb_build(rt_ctx* c, int ntr, int n_opaque, const std::vector<const fl
         for (int j = 0; j < nl; ++j) {
             const Slot& b = B[j];
             hipLaunchKernelGGL(rt_lb_cells, dim3(b.nsup), dim3(256), 0, st, cones[j], ntr, c->d_tri, b.R,
-                               (float)dcov[j], d_soff + b.sob, d_slists, nullptr, c->d_lb_off + b.ob, nullptr);
+                               (float)dcov[j], d_soff + b.sob, d_slists, nullptr, c->d_lb_off + b.ob, nullptr, 0);
             LB_TRY(hipGetLastError());
         }
         LB_TRY(scan_u32(c->d_lb_off, (unsigned)ob, c->d_lb_off, (unsigned long long*)c->d_scan, st, &tot));
@@ -1396,14 +1400,16 @@ static int lb_build(rt_ctx* c, int ntr, int n_opaque, const std::vector<const fl
             c->err = "light buffer too large";
             goto done;
         }
-        LB_TRY(hipMalloc(&c->d_lb_ent, std::max<size_t>(total, 1) * kLbEntF * sizeof(float)));
+        // big lists with RT_OPT_LB_COMPACT: {triangle, key} entries (rt_lightbuf.h)
+        const int idx_mode = c->opt_lb_compact && ntr > kClusterMinTriangles;
+        LB_TRY(hipMalloc(&c->d_lb_ent, std::max<size_t>(total, 1) * (idx_mode ? 8 : kLbEntF * sizeof(float))));
         LB_TRY(hipMalloc(&c->d_lb_dcap, std::max<size_t>(dperm_all.size(), 1) * kLbEntF * sizeof(float)));
         LB_TRY(hipMalloc(&c->d_lb_meta, std::max(nl, 1) * 2 * sizeof(float4)));
         std::vector<float4> meta((size_t)std::max(nl, 1) * 2);
         for (int j = 0; j < nl; ++j) {
             const Slot& b = B[j];
             hipLaunchKernelGGL(rt_lb_cells, dim3(b.nsup), dim3(256), 0, st, cones[j], ntr, c->d_tri, b.R,
-                               (float)dcov[j], d_soff + b.sob, d_slists, c->d_lb_off + b.ob, nullptr, (float*)c->d_lb_ent);
+                               (float)dcov[j], d_soff + b.sob, d_slists, c->d_lb_off + b.ob, nullptr, (float*)c->d_lb_ent, idx_mode);
             LB_TRY(hipGetLastError());
             if (b.ndperm) {
                 hipLaunchKernelGGL(rt_lb_dcap, dim3((unsigned)((b.ndperm + 255) / 256)), dim3(256), 0, st, cones[j],
@@ -1424,6 +1430,7 @@ static int lb_build(rt_ctx* c, int ntr, int n_opaque, const std::vector<const fl
         LB_TRY(hipStreamSynchronize(st));  // meta (host) outlives the copy; the temporaries are freed below
         mark(4);
         c->lb_ready = true;
+        c->lb_idx = idx_mode != 0;
         c->lb_entries = total;
     }
 done:
@@ -1586,6 +1593,7 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
     c->d_lb_off = nullptr;
     c->d_lb_ent = c->d_lb_dcap = c->d_lb_meta = nullptr;
     c->lb_ready = false;
+    c->lb_idx = false;
     c->lb_levels = 0;
     c->lb_entries = 0;
     hipFree(c->d_uni);
@@ -1847,11 +1855,14 @@ typedef void (*kernel_fn)(const SceneDev, const FrameDev, unsigned*, float*, Sta
 #define RT_WAVE_LB 1
 #endif
 template <bool COUNT>
-static kernel_fn pick_kernel(int depth, int n_tri, int n_lights, bool lbuf, bool cbuf, int& cap, int& lb)
+static kernel_fn pick_kernel(int depth, int n_tri, int n_lights, bool lbuf, bool cbuf, int& cap, int& lb,
+                             bool lbidx = false)
 {
     lb = 1;
     if (depth == 0 && n_tri > 0 && lbuf) {  // light-buffer shadows, one light per pass
         cap = 0;
+        if (n_tri > kClusterMinTriangles && lbidx)  // compact cell lists (WAVE bit 16)
+            return cbuf ? (kernel_fn)&rt_trace_kernel<0, 1, 30, COUNT> : (kernel_fn)&rt_trace_kernel<0, 1, 22, COUNT>;
         if (n_tri > kClusterMinTriangles)
             return cbuf ? (kernel_fn)&rt_trace_kernel<0, 1, 14, COUNT> : (kernel_fn)&rt_trace_kernel<0, 1, 6, COUNT>;
         return cbuf ? (kernel_fn)&rt_trace_kernel<0, 1, 13, COUNT> : (kernel_fn)&rt_trace_kernel<0, 1, 5, COUNT>;
@@ -1889,6 +1900,8 @@ static kernel_fn pick_kernel(int depth, int n_tri, int n_lights, bool lbuf, bool
 static void trace_dims(kernel_fn k, int width, int rows, dim3& grid, dim3& block, unsigned& lds)
 {
     const bool big = k == (kernel_fn)&rt_trace_kernel<0, 1, 14, false> || k == (kernel_fn)&rt_trace_kernel<0, 1, 14, true> ||
+                     k == (kernel_fn)&rt_trace_kernel<0, 1, 30, false> || k == (kernel_fn)&rt_trace_kernel<0, 1, 30, true> ||
+                     k == (kernel_fn)&rt_trace_kernel<0, 1, 22, false> || k == (kernel_fn)&rt_trace_kernel<0, 1, 22, true> ||
                      k == (kernel_fn)&rt_trace_kernel<0, 1, 6, false> || k == (kernel_fn)&rt_trace_kernel<0, 1, 6, true> ||
                      k == (kernel_fn)&rt_trace_kernel<0, RT_WAVE_LB, 10, false> ||
                      k == (kernel_fn)&rt_trace_kernel<0, RT_WAVE_LB, 10, true> ||
@@ -2556,8 +2569,9 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
         if (int rc = prepare_state(c, f, st, sync_path, capturing, cb_want)) return rc;
     }
     const bool cbuf = cb_want && (ring ? ring->cs.cb.valid : cb_matches(c->cb, f));
-    kernel_fn k = (f->flags & RT_FLAG_STATS) ? pick_kernel<true>(depth, c->n_tri, c->n_lights, lbuf, cbuf, cap, lb)
-                                              : pick_kernel<false>(depth, c->n_tri, c->n_lights, lbuf, cbuf, cap, lb);
+    kernel_fn k = (f->flags & RT_FLAG_STATS)
+                      ? pick_kernel<true>(depth, c->n_tri, c->n_lights, lbuf, cbuf, cap, lb, lbuf && c->lb_idx)
+                      : pick_kernel<false>(depth, c->n_tri, c->n_lights, lbuf, cbuf, cap, lb, lbuf && c->lb_idx);
     if (!k) {
         c->err = "reachable bounce depth " + std::to_string(depth) + " exceeds the compiled stack (32)";
         return RT_E_UNSUPPORTED;
@@ -2789,7 +2803,7 @@ RT_EXPORT int rt_render_sequence_async(rt_ctx* c, const rt_frame* frames, int32_
             if (int rc = camera_records(c, f->cam_pos, fs, cbuf, q.tricam, q.cone_cam, q.uni, q.clu_cam)) return rc;
         }
         int cap = 0, lb = 1;
-        kernel_fn k = pick_kernel<false>(depth, c->n_tri, c->n_lights, lbuf, cbuf, cap, lb);
+        kernel_fn k = pick_kernel<false>(depth, c->n_tri, c->n_lights, lbuf, cbuf, cap, lb, lbuf && c->lb_idx);
         SceneDev S = scene_dev(c, lbuf, false);
         S.tricam = q.tricam;
         S.cone_cam = q.cone_cam;

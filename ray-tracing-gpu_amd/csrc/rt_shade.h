@@ -452,6 +452,7 @@ __device__ __forceinline__ void shadow_opaque_wave(const SceneDev& S, int l0, in
 #define RT_LB_LDS_UBR 1
 #endif
 constexpr int kLbLdsG = RT_LB_LDS_G;      // most cells a wave stages
+template <bool IDX>
 __device__ __forceinline__ bool lb_walk_lds(const SceneDev& S, bool use, int cell, unsigned e, unsigned end,
                                             const Vec3 P, const Vec3 L, float dist, bool& occ, Counters& cnt)
 {
@@ -527,10 +528,12 @@ __device__ __forceinline__ bool lb_walk_lds(const SceneDev& S, bool use, int cel
                 }
                 const unsigned q = q0 + k + ((unsigned)s & wmask);
                 if (((gact >> gi) & 1u) && q < q1) {
-                    const float* r = lb_rec(S.lb_ent, q);
-                    win.a[s] = lb_a(r);
-                    win.b[s] = lb_b(r);
-                    win.c[s] = lb_tail(r);
+                    float4 a, b;
+                    float2 c;
+                    lb_cell_entry<IDX>(S.lb_ent, S.tri, q, a, b, c);
+                    win.a[s] = a;
+                    win.b[s] = b;
+                    win.c[s] = c;
                 }
             }
 #if RT_LB_LDS_PF
@@ -546,10 +549,7 @@ __device__ __forceinline__ bool lb_walk_lds(const SceneDev& S, bool use, int cel
                     }
                     const unsigned q = q0 + k + (wmask + 1u) + ((unsigned)rk & wmask);
                     if (((gact >> gi) & 1u) && q < q1) {
-                        const float* r = lb_rec(S.lb_ent, q);
-                        pa = lb_a(r);
-                        pb = lb_b(r);
-                        pc = lb_tail(r);
+                        lb_cell_entry<IDX>(S.lb_ent, S.tri, q, pa, pb, pc);
                         pv = true;
                     }
                 }
@@ -608,7 +608,9 @@ __device__ __forceinline__ bool lb_walk_lds(const SceneDev& S, bool use, int cel
 // fewer VGPRs (short lists).
 // pre: the lanes' cell list bounds [pe, pn) were loaded ahead (lb_prefetch:
 // every lane that can use the slot has them).
-template <bool PIPE>
+// IDX: the cell lists hold {triangle, key} entries (RT_OPT_LB_COMPACT,
+// big lists; lb_cell_entry).
+template <bool PIPE, bool IDX>
 __device__ __forceinline__ bool lb_slot(const SceneDev& S, int slot, const Vec3 P, const Vec3 L, float dist, bool cand,
                                         bool& occ, Counters& cnt, bool pre = false, unsigned pe = 0, unsigned pn = 0)
 {
@@ -655,14 +657,22 @@ __device__ __forceinline__ bool lb_slot(const SceneDev& S, int slot, const Vec3 
 #else
         for (unsigned q = q0; q < q1; ++q) {
 #endif
-            const float* r = lb_rec(S.lb_ent, q);
-            const float4 c0 = lb_a(r);
+            float4 c0, c1;
+            float2 c2;
+            if constexpr (IDX) {  // {triangle, key}: the key, then the record
+                const uint2 en = reinterpret_cast<const uint2*>(S.lb_ent)[q];
+                if (!__any(use & !occ & (__uint_as_float(en.y) < dist))) break;
+                lb_cell_entry<IDX>(S.lb_ent, S.tri, q, c0, c1, c2);
+            } else {
+                const float* r = lb_rec(S.lb_ent, q);
+                c0 = lb_a(r);
+                if (!__any(use & !occ & (c0.w < dist))) break;
+                c1 = lb_b(r);
+                c2 = lb_tail(r);
+            }
             const bool act = use & !occ & (c0.w < dist);
-            if (!__any(act)) break;
             ++cnt.tri;
             RT_EV(cnt, 4);
-            const float4 c1 = lb_b(r);
-            const float2 c2 = lb_tail(r);
             if (act) {
                 const Vec3 e1 = make3(c1.x, c1.y, c1.z), e2 = make3(c1.w, c2.x, c2.y);
                 const TriU u = tri_u(make3(c0.x, c0.y, c0.z), e1, e2, P, L);
@@ -684,7 +694,7 @@ __device__ __forceinline__ bool lb_slot(const SceneDev& S, int slot, const Vec3 
         }
     }
 #if RT_LB_LDS
-    if ((RT_LB_LDS & (PIPE ? 1 : 2)) && (!one_cell || lds_one) && bu && lb_walk_lds(S, use, cell, e, end, P, L, dist, occ, cnt))
+    if ((RT_LB_LDS & (PIPE ? 1 : 2)) && (!one_cell || lds_one) && bu && lb_walk_lds<IDX>(S, use, cell, e, end, P, L, dist, occ, cnt))
         end = e;  // walked: skip the global walk below
 #endif
     // The next entry's loads are issued before the current entry's exact
@@ -702,10 +712,7 @@ __device__ __forceinline__ bool lb_slot(const SceneDev& S, int slot, const Vec3 
     bool have = e < end;
 #endif
     if (PG && have) {
-        const float* r = lb_rec(S.lb_ent, e);
-        r0 = lb_a(r);
-        r1 = lb_b(r);
-        r2 = lb_tail(r);
+        lb_cell_entry<IDX>(S.lb_ent, S.tri, e, r0, r1, r2);
     }
     for (;;) {
         const bool act = have & !occ;
@@ -713,10 +720,7 @@ __device__ __forceinline__ bool lb_slot(const SceneDev& S, int slot, const Vec3 
         RT_EV(cnt, 3);
         bool go = false;
         if (!PG && act) {
-            const float* r = lb_rec(S.lb_ent, e);
-            r0 = lb_a(r);
-            r1 = lb_b(r);
-            r2 = lb_tail(r);
+            lb_cell_entry<IDX>(S.lb_ent, S.tri, e, r0, r1, r2);
         }
         const float4 c0 = r0, c1 = r1;
         const float2 c2 = r2;
@@ -728,10 +732,7 @@ __device__ __forceinline__ bool lb_slot(const SceneDev& S, int slot, const Vec3 
                 ++e;
                 have = e < end;
                 if (PG && have) {
-                    const float* r = lb_rec(S.lb_ent, e);
-                    r0 = lb_a(r);
-                    r1 = lb_b(r);
-                    r2 = lb_tail(r);
+                    lb_cell_entry<IDX>(S.lb_ent, S.tri, e, r0, r1, r2);
                 }
             }
         }
@@ -785,7 +786,7 @@ __device__ __forceinline__ bool lb_slot(const SceneDev& S, int slot, const Vec3 
 // within the light's buffer distance walk it (lb_slot); with far buffers
 // (big lists, S.lb_R levels) the lanes beyond walk the next level's; lanes
 // no buffer covers take the per-lane loop over every triangle.
-template <bool PIPE>
+template <bool PIPE, bool IDX>
 __device__ __forceinline__ void shadow_opaque_lb(const SceneDev& S, int l, const Vec3 P, const Vec3 L, float dist,
                                                  bool& occ, Counters& cnt, bool pre = false, unsigned pe = 0,
                                                  unsigned pn = 0)
@@ -798,11 +799,11 @@ __device__ __forceinline__ void shadow_opaque_lb(const SceneDev& S, int l, const
     {
     const float mx = fmaxf(fabsf(L.x), fmaxf(fabsf(L.y), fabsf(L.z)));
     const bool cand = !occ & (mx >= 0.5f);  // a direction the lookup takes
-    bool use = lb_slot<PIPE>(S, l, P, L, dist, cand, occ, cnt, pre, pe, pn);
+    bool use = lb_slot<PIPE, IDX>(S, l, P, L, dist, cand, occ, cnt, pre, pe, pn);
     if constexpr (PIPE) {  // big lists: lanes beyond a buffer take the next
         for (int lv = 1; lv < S.lb_R; ++lv) {
             if (!__any(cand & !use & !occ)) break;
-            use |= lb_slot<PIPE>(S, lv * S.n_lights + l, P, L, dist, cand & !use, occ, cnt);
+            use |= lb_slot<PIPE, IDX>(S, lv * S.n_lights + l, P, L, dist, cand & !use, occ, cnt);
         }
     }
     const float slack = dist * 1e-6f;
@@ -941,7 +942,7 @@ __device__ __forceinline__ Color shade_local(const SceneDev& S, const Mat& m, co
             bool occ = !gate;
             RT_MARK(cnt, 2);
 #ifndef RT_ABLATE_SHADOW
-            shadow_opaque_lb<RT_LB_PIPE(WAVE)>(S, li, P, L, dist, occ, cnt, PF, ce, cn);
+            shadow_opaque_lb<RT_LB_PIPE(WAVE), (WAVE & 16) != 0>(S, li, P, L, dist, occ, cnt, PF, ce, cn);
 #endif
             RT_MARK(cnt, 7);
             if (gate) {
