@@ -44,7 +44,8 @@ def test_compact_far_ladder_and_stats_equal_default(heightfield_path, near, far)
     got = b.render_float(f)
     sb = b.stats()
     assert bits_equal(got, want)
-    assert sa == sb
+    fields = [n for n, _ in type(sa)._fields_ if n != "kernel_ms"]
+    assert [getattr(sa, n) for n in fields] == [getattr(sb, n) for n in fields]
     a.close()
     b.close()
 
