@@ -490,13 +490,11 @@ __device__ double point_triangle_dist(const double* a, const double (*v)[3])
     return sqrt(q);
 }
 
-__global__ void rt_cone_prepass(const float4* __restrict__ tri, const float4* __restrict__ sph,
-                                const float4* __restrict__ nrm, const float4* __restrict__ coef, int n, float ax,
-                                float ay, float az, int camera, float dtarget, float4* __restrict__ out,
-                                float4* __restrict__ tricam)
+__device__ __forceinline__ void cone_record(const float4* __restrict__ tri, const float4* __restrict__ sph,
+                                            const float4* __restrict__ nrm, const float4* __restrict__ coef, int n,
+                                            float ax, float ay, float az, int camera, float dtarget,
+                                            float4* __restrict__ out, float4* __restrict__ tricam, int k)
 {
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n) return;
     // the camera's tricam records in the same launch (one kernel less per
     // camera: ~5 us of a moving frame's chain at C3)
     if (tricam) camera_record(tri, k, ax, ay, az, tricam);
@@ -625,6 +623,14 @@ __global__ void rt_cone_prepass(const float4* __restrict__ tri, const float4* __
     oe[1] = ce[1];
     oe[2] = ce[2];
 }
+__global__ void rt_cone_prepass(const float4* __restrict__ tri, const float4* __restrict__ sph,
+                                const float4* __restrict__ nrm, const float4* __restrict__ coef, int n, float ax,
+                                float ay, float az, int camera, float dtarget, float4* __restrict__ out,
+                                float4* __restrict__ tricam)
+{
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < n) cone_record(tri, sph, nrm, coef, n, ax, ay, az, camera, dtarget, out, tricam, k);
+}
 
 // Cluster records for one apex (one thread per 64-triangle cluster, in
 // double), from the members' [c0 c1] records.  A member's wave test passes
@@ -658,12 +664,10 @@ __device__ __forceinline__ double wave_max_dbl(double v)
     for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
     return v;
 }
-__global__ __launch_bounds__(256) void rt_cluster_prepass(const float4* __restrict__ cone, int n, int nclu,
-                                                          float4* __restrict__ out, int csize = 64)
+__device__ __forceinline__ void cluster_record(const float4* __restrict__ cone, int n, int c, int csize,
+                                               float4* __restrict__ out)
 {
     const int lane = (int)(threadIdx.x & 63);
-    const int c = (int)(blockIdx.x * 4 + (threadIdx.x >> 6));
-    if (c >= nclu) return;  // wave-uniform
     const long long k0 = (long long)csize * c, k1 = min((long long)n, k0 + csize);
     double ax = 0, ay = 0, az = 0, dmin = INFINITY, inv = 0.0, dcap = INFINITY;
     bool always = false;
@@ -713,7 +717,31 @@ __global__ __launch_bounds__(256) void rt_cluster_prepass(const float4* __restri
         out[2 * c + 1] = q1;
     }
 }
+__global__ __launch_bounds__(256) void rt_cluster_prepass(const float4* __restrict__ cone, int n, int nclu,
+                                                          float4* __restrict__ out, int csize = 64)
+{
+    const int c = (int)(blockIdx.x * 4 + (threadIdx.x >> 6));
+    if (c < nclu) cluster_record(cone, n, c, csize, out);  // wave-uniform
+}
 inline unsigned cluster_blocks(int nclu) { return (unsigned)((nclu + 3) / 4); }
+
+// Small lists' per-camera records in ONE launch (one workgroup): every
+// triangle's camera cone record (and tricam record), then — after the
+// barrier, in the same workgroup — the union record over them; the same
+// functions as rt_cone_prepass + rt_cluster_prepass, so the same bits, with
+// one launch (and its dispatch gap) less per moving camera.
+constexpr int kCameraSmallMax = 1024;  // triangles (the small-list bound)
+__global__ __launch_bounds__(256) void rt_camera_small(const float4* __restrict__ tri, const float4* __restrict__ sph,
+                                                       const float4* __restrict__ nrm,
+                                                       const float4* __restrict__ coef, int n, float ax, float ay,
+                                                       float az, float4* __restrict__ cone_out,
+                                                       float4* __restrict__ tricam, float4* __restrict__ uni)
+{
+    for (int k = (int)threadIdx.x; k < n; k += (int)blockDim.x)
+        cone_record(tri, sph, nrm, coef, n, ax, ay, az, 1, 0.0f, cone_out, tricam, k);
+    __syncthreads();
+    if (threadIdx.x < 64) cluster_record(cone_out, n, 0, n, uni);
+}
 
 // Camera cluster records in increasing dmin (rank sort; ties by id), the
 // cluster id in q1.y (unused by camera tests).  One wave per cluster, 64

@@ -2023,6 +2023,12 @@ static int camera_records(rt_ctx* c, const float* cp, hipStream_t st, bool all_t
                           float4* cone_cam, float4* uni, float4* clu_cam)
 {
     float4* tc = (all_tricam || c->n_tri <= kTricamMaxTriangles) ? tricam : nullptr;
+    if (uni && c->n_clu == 0 && c->n_tri <= kCameraSmallMax) {  // small lists: one launch
+        hipLaunchKernelGGL(rt_camera_small, dim3(1), dim3(256), 0, st, c->d_tri, c->d_trisph, c->d_trinrm,
+                           c->d_tricoef, c->n_tri, cp[0], cp[1], cp[2], cone_cam, tc, uni);
+        HIP_TRY(c, hipGetLastError());
+        return RT_OK;
+    }
     hipLaunchKernelGGL(rt_cone_prepass, dim3((c->n_tri + 255) / 256), dim3(256), 0, st, c->d_tri, c->d_trisph,
                        c->d_trinrm, c->d_tricoef, c->n_tri, cp[0], cp[1], cp[2], 1, 0.0f, cone_cam, tc);
     HIP_TRY(c, hipGetLastError());
