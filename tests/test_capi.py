@@ -128,3 +128,28 @@ def test_band_rows_matches_binding():
                 assert tot == -(-h // br) * br  # every band exactly once
     assert L.rt_band_rows(100, 8, 2, 0) == -1    # not a multiple of 16
     assert L.rt_band_rows(100, 16, 2, 2) == -1   # index out of range
+
+
+def test_option_enum_matches_binding_and_round_trips():
+    """Every RT_OPT_* of include/rt.h is in rt_amd.OPTIONS under its lower-case
+    name with the same number, and rt_set_option / rt_get_option round-trip
+    each on a CPU context (the setter is host code: no GPU needed)."""
+    text = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    enum = {m.group(1).lower(): int(m.group(2)) for m in re.finditer(r"\bRT_OPT_([A-Z0-9_]+)\s*=\s*(\d+)", text)}
+    assert enum == rt_amd.OPTIONS
+    L = rt_amd.lib()
+    h = ctypes.c_void_p()
+    assert L.rt_create_cpu(1, ctypes.byref(h)) == 0
+    values = {"light_buffer": 2, "camera_buffer": 2, "union_pretest": 0, "lb_scale": 8, "dcov_near": 1.5,
+              "cb_inline_max_mb": 64, "host_chunk_mb": 4, "cb_capacity": 1000, "async_ring": 1,
+              "bounce_refill": 1, "lb_compact": 1}
+    assert set(values) == set(enum)
+    try:
+        for name, v in values.items():
+            assert L.rt_set_option(h, enum[name], ctypes.c_double(v)) == 0, name
+            got = ctypes.c_double()
+            assert L.rt_get_option(h, enum[name], ctypes.byref(got)) == 0, name
+            assert got.value == v, name
+        assert L.rt_set_option(h, 999, ctypes.c_double(1)) != 0
+    finally:
+        L.rt_destroy(h)
