@@ -118,8 +118,44 @@ __device__ __forceinline__ bool edges_open(const WaveCone& wc, const float4* e, 
     return edge_open(wc, e[0], ang) & edge_open(wc, e[1], ang) & edge_open(wc, e[2], ang);
 }
 
+// Per-wave LDS windows (dynamic LDS, one per wave): the light-buffer walk's
+// staged entries (rt_shade.h lb_walk_lds: kLbLdsCap entries of a, b,
+// c per wave) and the camera-list walk's staged records (a, b:
+// kLbLdsCap / 2 records of 64 B per wave).  The two walks never overlap in a
+// wave.
+#ifndef RT_LB_LDS_CAP
+#define RT_LB_LDS_CAP 64
+#endif
+constexpr int kLbLdsCap = RT_LB_LDS_CAP;  // entries per wave window
+// The wave's window in the launch's dynamic LDS (kLdsWaveBytes per wave of
+// the workgroup, trace_dims on the host): a[cap], b[cap] float4, c[cap] float2.
+constexpr size_t kLdsWaveBytes = (size_t)kLbLdsCap * 40;
+struct LdsWin {
+    float4* a;
+    float4* b;
+    float2* c;
+};
+__device__ __forceinline__ LdsWin lds_window()
+{
+    extern __shared__ float4 rt_lds_dyn[];
+    float4* a = rt_lds_dyn + (threadIdx.x >> 6) * (kLbLdsCap * 5 / 2);
+    return LdsWin{a, a + kLbLdsCap, reinterpret_cast<float2*>(a + 2 * kLbLdsCap)};
+}
+
+__device__ __forceinline__ void wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // One batch of 64 triangles [k0, k0 + 64) for the wave's camera rays: one
 // lane per triangle against the wave cone, exact tests on the survivors.
+// STAGE (big lists: the clustered per-wave path, whose kernels have LDS
+// windows): each survivor's lane loads its tri[] record into the wave's
+// window first — one load round trip for the batch instead of one per
+// survivor — and the wave tests them from LDS in the same (ascending) order.
+template <bool STAGE = false>
 __device__ __forceinline__ void camera_wave_batch(const SceneDev& S, const WaveCone& wc, int k0, const Vec3 O,
                                                   const Vec3 D, float& bt, int& bi, Counters& cnt,
                                                   float far = INFINITY)
@@ -137,6 +173,35 @@ __device__ __forceinline__ void camera_wave_batch(const SceneDev& S, const WaveC
     if (RT_EDGES && S.use_edges && reach) reach = edges_open(wc, S.cone_cam + 2 * S.n_tri + 3 * k, 0.0f);
     RT_EV(cnt, 1);
     unsigned long long m = __ballot(reach);
+    if constexpr (STAGE) {
+        if (!m) return;
+        const LdsWin win = lds_window();
+        const int rk = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        if (reach) {
+            const float4* r = S.tri + 3 * k;
+            const float4 a = r[0], b = r[1], c = r[2];
+            win.a[rk] = a;
+            win.b[rk] = b;
+            win.c[rk] = make_float2(c.x, c.y);
+        }
+        wave_lds_sync();
+        const int n = __popcll(m);
+        for (int j = 0; j < n; ++j) {
+            RT_EV(cnt, 2);
+            const float4 a = win.a[j], b = win.b[j];
+            const float2 c = win.c[j];
+            ++cnt.tri;
+            const Vec3 e1 = make3(a.w, b.x, b.y), e2 = make3(b.z, b.w, c.x);
+            const TriU r = tri_u(make3(a.x, a.y, a.z), e1, e2, O, D);
+            if (!__any(r.ok)) continue;
+            float t;
+            const bool ok = tri_vt(r, e1, e2, D, t);
+            take_min(ok, t, __float_as_int(c.y), bt, bi);
+        }
+        return;
+    }
     while (m) {
         const int kk = k0 + (int)__builtin_ctzll(m);
         m &= m - 1;
@@ -157,6 +222,9 @@ __device__ __forceinline__ void camera_wave_batch(const SceneDev& S, const WaveC
 }
 
 // Closest hit for camera rays, wave-culled (full wave, cone ok).
+#ifndef RT_CAMW_LDS  // the clustered path's member batches staged in LDS
+#define RT_CAMW_LDS 1
+#endif
 template <bool CLU>
 __device__ __forceinline__ int closest_hit_camera_wave(const SceneDev& S, const WaveCone& wc, const Vec3 O,
                                                        const Vec3 D, float& best_t, Counters& cnt)
@@ -194,7 +262,8 @@ __device__ __forceinline__ int closest_hit_camera_wave(const SceneDev& S, const 
                 const int b = (int)__builtin_ctzll(cm);
                 cm &= cm - 1;
                 const int cid = __builtin_amdgcn_readlane(id, b);
-                camera_wave_batch(S, wc, 64 * cid, O, D, bt, bi, cnt, wave_max(bi >= 0 ? bt : INFINITY));
+                camera_wave_batch<RT_CAMW_LDS != 0>(S, wc, 64 * cid, O, D, bt, bi, cnt,
+                                                    wave_max(bi >= 0 ? bt : INFINITY));
             }
         }
     } else {
@@ -234,37 +303,6 @@ __device__ __forceinline__ Vec3 camera_dir(const FrameDev& F, int pxc, int pyc)
     const Vec3 dm = d0 * M;
     const float len = sqrt_w(dm.x * dm.x + dm.y * dm.y + dm.z * dm.z);
     return len > kEps ? dm * recip_w(len) : make3(0.f, 0.f, 0.f);
-}
-
-// Per-wave LDS windows (dynamic LDS, one per wave): the light-buffer walk's
-// staged entries (rt_shade.h lb_walk_lds: kLbLdsCap entries of a, b,
-// c per wave) and the camera-list walk's staged records (a, b:
-// kLbLdsCap / 2 records of 64 B per wave).  The two walks never overlap in a
-// wave.
-#ifndef RT_LB_LDS_CAP
-#define RT_LB_LDS_CAP 64
-#endif
-constexpr int kLbLdsCap = RT_LB_LDS_CAP;  // entries per wave window
-// The wave's window in the launch's dynamic LDS (kLdsWaveBytes per wave of
-// the workgroup, trace_dims on the host): a[cap], b[cap] float4, c[cap] float2.
-constexpr size_t kLdsWaveBytes = (size_t)kLbLdsCap * 40;
-struct LdsWin {
-    float4* a;
-    float4* b;
-    float2* c;
-};
-__device__ __forceinline__ LdsWin lds_window()
-{
-    extern __shared__ float4 rt_lds_dyn[];
-    float4* a = rt_lds_dyn + (threadIdx.x >> 6) * (kLbLdsCap * 5 / 2);
-    return LdsWin{a, a + kLbLdsCap, reinterpret_cast<float2*>(a + 2 * kLbLdsCap)};
-}
-
-__device__ __forceinline__ void wave_lds_sync()
-{
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 // Camera-list walk from LDS (RT_CB_LDS build option; bit 0 the big-list
