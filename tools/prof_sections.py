@@ -34,7 +34,10 @@ def main():
     ap.add_argument("lib")
     ap.add_argument("--config", default="c2")
     ap.add_argument("--frames", type=int, default=20)
+    ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
+                    help="context option (rt_amd.OPTIONS), e.g. --option camera_buffer=0")
     a = ap.parse_args()
+    opts = {k: float(v) for k, v in (o.split("=", 1) for o in a.option)}
     os.environ["RT_AMD_LIB"] = os.path.abspath(a.lib)
     import torch  # noqa: F401  (one HIP runtime)
 
@@ -47,7 +50,7 @@ def main():
     L.rt_debug_lb_info.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
     name, W, H, depth = bench.CONFIGS[a.config]
     s = rt_amd.Scene(bench.scene_path(name), W, H, depth)
-    ctx = rt_amd.Context(0)
+    ctx = rt_amd.Context(0, **opts)
     ctx.upload(s)
     info = (ctypes.c_double * 30)()
     L.rt_debug_lb_info(ctx._h, info, 30)
@@ -64,7 +67,7 @@ def main():
     waves = ((W + 7) // 8) * ((H + 7) // 8) * a.frames
     ev_names = EVENTS_LB if lbinfo else EVENTS
     tot = sum(buf[:8]) or 1
-    print(json.dumps({"config": a.config, "frames": a.frames,
+    print(json.dumps({"config": a.config, "options": opts, "frames": a.frames,
                       "share": {n: round(buf[i] / tot, 4) for i, n in enumerate(NAMES)},
                       "wave_clocks_per_frame": {n: buf[i] // a.frames for i, n in enumerate(NAMES)},
                       "events_per_wave": {n: round(ev[i] / waves, 2) for i, n in enumerate(ev_names) if n},
