@@ -376,7 +376,7 @@ def main():
     ap.add_argument("--frame-sha", action="store_true",
                     help="rank 0 adds the SHA-256 of the last assembled RGBA8 frame (bottom row first)")
     ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
-                    help="context option (rt_amd.OPTIONS) for an A/B run, e.g. --option bounce_refill=1; "
+                    help="context option (rt_amd.OPTIONS) for an A/B run, e.g. --option camera_buffer=2; "
                          "none changes an image")
     args = ap.parse_args()
     ctx_opts = {k: float(v) for k, v in (o.split("=", 1) for o in args.option)}

@@ -237,30 +237,14 @@ enum {
                                    and copy in row chunks of this many MiB of output,
                                    each copy overlapping the next chunk (default 8;
                                    0 = one kernel, then one copy) */
-    RT_OPT_CB_CAPACITY = 8,     /* launch (ABI 5): camera-buffer entries allocated;
+    RT_OPT_CB_CAPACITY = 8      /* launch (ABI 5): camera-buffer entries allocated;
                                    0 (default) = sized from earlier builds' totals.  A
                                    tile whose list does not fit renders by the per-wave
                                    path (tests: a small value exercises that path) */
-    RT_OPT_ASYNC_RING = 9       /* launch (ABI 5): rt_render_async of a new camera
-                                   whose buffer is built (RT_OPT_CAMERA_BUFFER) builds
-                                   its camera state in a ring of two slots on an
-                                   internal stream, overlapping the renders already
-                                   enqueued (1) / in the context's state on the
-                                   caller's stream (0, default: the ring measured no
-                                   gain — the build's waves wait for the trace
-                                   kernel's to retire) */,
-    RT_OPT_BOUNCE_REFILL = 10   /* launch (ABI 5): scenes with bounces render with the
-                                   lane-refill kernel (persistent waves whose lanes take
-                                   a new pixel as soon as their ray tree ends) (1) / one
-                                   pixel per lane (0, default: the refill measured no
-                                   gain) */,
-    RT_OPT_LB_COMPACT = 11      /* upload (ABI 5): big lists' light-buffer cell lists
-                                   hold {triangle, key} (8 B) instead of the triangle's
-                                   40-byte record, which the walk reads from the
-                                   L2-resident triangle array: the buffer is 5x
-                                   smaller in HBM and a C3 frame reads 116 instead of
-                                   269 MB, at +8% time (C3) / +2.5% (C5) — 1 / 0
-                                   (default) */
+    /* 9-11 (ABI 5: the async camera-state ring, the bounce lane-refill kernel,
+       compact light-buffer entries) were measured slower or no faster and are
+       removed in ABI 6: rt_set_option returns RT_E_ARG for them.  Their code
+       and measurements: profiles/r04/set_aside/. */
 };
 int rt_set_option(rt_ctx*, int32_t option, double value);
 int rt_get_option(rt_ctx*, int32_t option, double* value);

@@ -370,6 +370,29 @@ REXPORT int ref_load(const char* path, int w, int h, int max_bounces, void** out
     return 0;
 }
 
+// An explicit camera, as the product's rt_frame carries it (include/rt.h):
+// position, the 4x4 orientation (row-major m[i][j]), the film half extents
+// and the pixel reciprocals — the state Scene.cpp:1538-1561 reads per pixel
+// (Camera.Position, Camera.Orientation, HalfW/HalfH from :676-677,
+// InvW/InvH from :678-679).  What a caller that moves the camera between
+// frames (Main.cpp:229-250, LancerRayons per frame) hands the pixel loop.
+REXPORT int ref_set_camera(void* sp, const float* pos, const float* orient, float half_w, float half_h, float inv_w,
+                           float inv_h, int w, int h)
+{
+    RefScene* S = (RefScene*)sp;
+    S->Camera.Position = CVecteur3(pos[0], pos[1], pos[2]);
+    S->Camera.Orientation = CMatrice4(orient[0], orient[1], orient[2], orient[3], orient[4], orient[5], orient[6],
+                                      orient[7], orient[8], orient[9], orient[10], orient[11], orient[12],
+                                      orient[13], orient[14], orient[15]);
+    S->HalfW = half_w;
+    S->HalfH = half_h;
+    S->InvW = inv_w;
+    S->InvH = inv_h;
+    S->ResLargeur = w;
+    S->ResHauteur = h;
+    return 0;
+}
+
 REXPORT const char* ref_error(void* s) { return ((RefScene*)s)->err.c_str(); }
 REXPORT void ref_free(void* s) { delete (RefScene*)s; }
 

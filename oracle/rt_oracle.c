@@ -792,6 +792,26 @@ OEXPORT void oracle_set_params(oracle_scene* S, int max_bounces, float min_energ
     S->scene_ior = scene_ior;
 }
 
+/* An explicit camera (the product's rt_frame fields): position, orientation
+ * m[i][j] row-major, film half extents, pixel reciprocals and resolution —
+ * the state the pixel loop reads (Scene.cpp:1538-1561 with :676-679), as a
+ * caller moving the camera between frames sets it (Main.cpp:229-250). */
+OEXPORT int oracle_set_camera(oracle_scene* S, const float* pos, const float* orient, float half_w, float half_h,
+                              float inv_w, float inv_h, int w, int h)
+{
+    if (!S || !S->prepared || w <= 0 || h <= 0) return -1;
+    S->cam_pos = v3(pos[0], pos[1], pos[2]);
+    for (int i = 0; i < 4; i++)
+        for (int j = 0; j < 4; j++) S->orient.m[i][j] = orient[4 * i + j];
+    S->half_w = half_w;
+    S->half_h = half_h;
+    S->inv_w = inv_w;
+    S->inv_h = inv_h;
+    S->w = w;
+    S->h = h;
+    return 0;
+}
+
 OEXPORT void oracle_free(oracle_scene* S)
 {
     if (!S) return;

@@ -170,7 +170,7 @@ __device__ __forceinline__ void camera_wave_batch(const SceneDev& S, const WaveC
     // whose hits all lie at t >= dmin > far cannot win
     bool reach = cone_overlap(wc, c0, c1.w, 0.0f) & !(far < c1.x);
     // edge records only for sphere survivors
-    if (RT_EDGES && S.use_edges && reach) reach = edges_open(wc, S.cone_cam + 2 * S.n_tri + 3 * k, 0.0f);
+    if (S.use_edges && reach) reach = edges_open(wc, S.cone_cam + 2 * S.n_tri + 3 * k, 0.0f);
     RT_EV(cnt, 1);
     unsigned long long m = __ballot(reach);
     if constexpr (STAGE) {
@@ -222,9 +222,6 @@ __device__ __forceinline__ void camera_wave_batch(const SceneDev& S, const WaveC
 }
 
 // Closest hit for camera rays, wave-culled (full wave, cone ok).
-#ifndef RT_CAMW_LDS  // the clustered path's member batches staged in LDS
-#define RT_CAMW_LDS 1
-#endif
 template <bool CLU>
 __device__ __forceinline__ int closest_hit_camera_wave(const SceneDev& S, const WaveCone& wc, const Vec3 O,
                                                        const Vec3 D, float& best_t, Counters& cnt)
@@ -262,7 +259,7 @@ __device__ __forceinline__ int closest_hit_camera_wave(const SceneDev& S, const 
                 const int b = (int)__builtin_ctzll(cm);
                 cm &= cm - 1;
                 const int cid = __builtin_amdgcn_readlane(id, b);
-                camera_wave_batch<RT_CAMW_LDS != 0>(S, wc, 64 * cid, O, D, bt, bi, cnt,
+                camera_wave_batch<true>(S, wc, 64 * cid, O, D, bt, bi, cnt,
                                                     wave_max(bi >= 0 ? bt : INFINITY));
             }
         }
@@ -305,18 +302,13 @@ __device__ __forceinline__ Vec3 camera_dir(const FrameDev& F, int pxc, int pyc)
     return len > kEps ? dm * recip_w(len) : make3(0.f, 0.f, 0.f);
 }
 
-// Camera-list walk from LDS (RT_CB_LDS build option; bit 0 the big-list
-// kernel, bit 1 the small-list one): the wave stages the next W records of
+// Camera-list walk from LDS (the big-list kernel; the small-list kernel
+// measured slower with it): the wave stages the next W records of
 // its list with one load per lane (for lists of indices, the index then its
 // record: two latencies per window instead of per entry) and walks them from
 // LDS — same entries, same order, same exit.
-#ifndef RT_CB_LDS
-#define RT_CB_LDS 1
-#endif
-#ifndef RT_CB_LDS_W
-#define RT_CB_LDS_W 32
-#endif
-static_assert(2 * RT_CB_LDS_W <= RT_LB_LDS_CAP, "camera window exceeds the wave's LDS");
+constexpr unsigned kCbLdsW = 32;
+static_assert(2 * kCbLdsW <= kLbLdsCap, "camera window exceeds the wave's LDS");
 
 // Closest hit for camera rays from the tile's camera-buffer list (the wave
 // is the tile: full, rows aligned).  Planes and quadrics first (their hits
@@ -347,9 +339,8 @@ __device__ __forceinline__ int closest_hit_camera_list(const SceneDev& S, int ti
         take_min(ok, t, __float_as_int(c.z), bt, bi);
     }
     const unsigned e1 = S.cb_off[tile + 1];
-#if RT_CB_LDS
-    if constexpr ((RT_CB_LDS & (INLINE ? 1 : 2)) != 0) {
-        constexpr unsigned W = RT_CB_LDS_W;
+    if constexpr (INLINE) {
+        constexpr unsigned W = kCbLdsW;
         const int lane = (int)(threadIdx.x & 63);
         const LdsWin win = lds_window();
         const bool inl = INLINE && S.cb_rec;
@@ -395,7 +386,6 @@ __device__ __forceinline__ int closest_hit_camera_list(const SceneDev& S, int ti
         best_t = bt;
         return bi;
     }
-#endif
     if (INLINE && S.cb_rec) {  // records inline: one scalar load round trip per entry
         for (unsigned e = S.cb_off[tile]; e < e1; ++e) {
             const float4* r = S.cb_rec + 4 * (size_t)e;

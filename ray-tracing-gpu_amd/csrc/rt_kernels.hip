@@ -10,8 +10,7 @@
 //
 // Execution model:
 //  * one wave64 = one 8x8 pixel tile, lane l -> (l&7, l>>3); one wave per
-//    workgroup by default (RT_WG1 3; 0 restores 256-thread workgroups of
-//    2x2 tiles);
+//    workgroup;
 //  * the surface list is walked in FILE ORDER by every lane of the wave in
 //    lockstep, so the surface index, its type switch and its 64-byte record are
 //    wave-uniform: records arrive through the scalar data cache (s_load) into
@@ -68,9 +67,6 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
 {
     const Color bg{F.bg[0], F.bg[1], F.bg[2]};
     if constexpr (MAXD == 0) {
-#ifdef RT_ABLATE_ALL  // timing-only build: ray set-up and store only
-        return Color{D.x, D.y, D.z};
-#endif
         float t;
         RT_MARK(cnt, 0);
         const int idx = closest_hit_primary<(WAVE & 11)>(S, O, D, t, cnt, tile);
@@ -79,9 +75,6 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
         // shading so the wave stays whole for wave-level shadow culling.
         const bool hit = idx >= 0;
         if (!__any(hit & live)) return bg;
-#ifdef RT_ABLATE_SHADE  // timing-only build: primary closest hit only
-        return Color{t, (float)idx, 0.f};
-#endif
         const int sidx = hit ? idx : 0;
         // A tile usually sees one surface: then its normal and material
         // records come by scalar (broadcast) loads instead of a per-lane gather.
@@ -204,9 +197,6 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
 #ifndef RT_WAVES_PER_EU
 #define RT_WAVES_PER_EU 7
 #endif
-#ifndef RT_WG1
-#define RT_WG1 3
-#endif
 #ifndef RT_WAVES_PER_EU_BIG
 #define RT_WAVES_PER_EU_BIG 7
 #endif
@@ -217,22 +207,14 @@ constexpr int waves_per_eu(int maxd, int wave)
 // COUNT: also tally the exact tests executed (the RT_FLAG_STATS launch); in
 // the timed kernels the tallies are dead and compile away.
 template <int MAXD, int LB, int WAVE, bool COUNT>
-// workgroup size the trace kernels are compiled for: one wave with RT_WG1 3
-// (C5 -1.1% against declaring 256; the others flat)
-#ifndef RT_TRACE_LB
-#define RT_TRACE_LB (RT_WG1 == 3 ? 64 : 256)
-#endif
-__global__ __launch_bounds__(RT_TRACE_LB) __attribute__((amdgpu_waves_per_eu(waves_per_eu(MAXD, WAVE)))) void rt_trace_kernel(const SceneDev S, const FrameDev F, unsigned* __restrict__ rgba,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(waves_per_eu(MAXD, WAVE)))) void rt_trace_kernel(const SceneDev S, const FrameDev F, unsigned* __restrict__ rgba,
                                                        float* __restrict__ rgbf, StatsDev* __restrict__ stats)
 {
-    // One wave per workgroup (RT_WG1 3, the default): one 8 x 8 tile each, so
-    // a CU takes a new tile as soon as any wave slot frees instead of four at
-    // once (A/B against 2 x 2 tiles per workgroup: C3 -3.1%, C5 -4.5%, C4
-    // -3.7%, scene7 -3.4%, scene9 -1.4%, C2 -0.8%).  1: only the small-list
-    // camera-buffer kernel, 2: every kernel but the big-list ones, 0: none.
-    constexpr bool kWg1 = RT_WG1 == 1 ? WAVE == 13 : (RT_WG1 == 2 ? !(WAVE & 2) : RT_WG1 == 3);
+    // One wave per workgroup: one 8 x 8 tile each, so a CU takes a new tile
+    // as soon as any wave slot frees instead of four at once (A/B against
+    // 2 x 2 tiles per workgroup: C3 -3.1%, C5 -4.5%, C4 -3.7%, scene7 -3.4%,
+    // scene9 -1.4%, C2 -0.8%; declaring 64 threads: C5 -1.1%).
     const int lane = threadIdx.x & 63;
-    const int wave = kWg1 ? 0 : (int)(threadIdx.x >> 6);
     // XCD-aware block order: the dispatcher deals workgroups round-robin over
     // the 8 XCDs (each with its own L2), so workgroup w runs on XCD w % 8 as
     // that XCD's (w / 8)-th; give every XCD one contiguous run of blocks in
@@ -254,9 +236,9 @@ __global__ __launch_bounds__(RT_TRACE_LB) __attribute__((amdgpu_waves_per_eu(wav
             by = (int)(lw / gridDim.x);
         }
     }
-    const int tile_x = kWg1 ? bx : bx * 2 + (wave & 1);  // 8-pixel column of the wave's tile
+    const int tile_x = bx;  // 8-pixel column of the wave's tile
     const int px = tile_x * 8 + (lane & 7);
-    const int ly0 = kWg1 ? by * 8 : by * 16 + (wave >> 1) * 8;  // the wave's first output row
+    const int ly0 = by * 8;  // the wave's first output row
     const int ly = ly0 + (lane >> 3);
     // frame row of output row r: the slab, or band (r / band_rows) of this
     // rank's cyclic set (a wave's 8 rows never straddle a band: 16 | band_rows)
@@ -304,12 +286,9 @@ __global__ __launch_bounds__(RT_TRACE_LB) __attribute__((amdgpu_waves_per_eu(wav
             // each 128-B line out twice (WRITE_SIZE 134 -> 268 MB per frame:
             // 32-B tile rows evicted before the neighbouring tiles fill the
             // line) for -0.5%.
-#ifndef RT_NT_STORE
-#define RT_NT_STORE 1
-#endif
             if (rgba) {
                 const unsigned px8 = unorm8(c.r) | (unorm8(c.g) << 8) | (unorm8(c.b) << 16) | 0xFF000000u;
-                if constexpr (RT_NT_STORE && !(WAVE & 2)) __builtin_nontemporal_store(px8, rgba + o);
+                if constexpr (!(WAVE & 2)) __builtin_nontemporal_store(px8, rgba + o);
                 else rgba[o] = px8;
             }
         }
@@ -323,8 +302,7 @@ __global__ __launch_bounds__(RT_TRACE_LB) __attribute__((amdgpu_waves_per_eu(wav
             atomicAdd(&rt_prof_ev[i], (unsigned long long)cnt.ev[i]);
             tot += cnt.pt[i];
         }
-        const int tile = kWg1 ? (int)(blockIdx.y * gridDim.x + blockIdx.x)
-                              : (int)((blockIdx.y * 2 + (wave >> 1)) * (gridDim.x * 2) + blockIdx.x * 2 + (wave & 1));
+        const int tile = (int)(blockIdx.y * gridDim.x + blockIdx.x);
         if (rt_prof_tiles && tile < rt_prof_ntiles) {
             unsigned* o = rt_prof_tiles + 16 * (size_t)tile;
             o[0] = (unsigned)tot;
@@ -354,224 +332,6 @@ __global__ __launch_bounds__(RT_TRACE_LB) __attribute__((amdgpu_waves_per_eu(wav
 #pragma unroll
             for (int i = 0; i < 7; ++i)
                 if (i < nv) atomicAdd(dst[i], v[i]);
-        }
-    }
-}
-
-// Lane refill for the bounce kernels (RT_OPT_BOUNCE_REFILL, an A/B switch;
-// off by default).  rt_trace_kernel<MAXD> gives each lane one pixel and walks
-// its ray tree to the end, so a wave runs as long as its deepest tree and the
-// lanes whose trees end early idle.  Here a persistent wave keeps its lanes
-// busy instead: each loop iteration advances every busy lane by one trace of
-// its depth-first walk and the unwinds up to its next trace, so the busy
-// lanes trace together; lanes whose pixel is done
-// take the next items of the wave's pool by ballot + prefix count.  The wave
-// claims pools of kRefillChunk 8 x 8 tiles (tile-major, so lanes start on
-// neighbouring pixels) with one atomic on work[0].  Every lane runs the same
-// per-ray arithmetic as radiance<MAXD>, so the images are the same bits.
-// Camera rays take the per-lane tests of the bounce kernels (WAVE 0); in a
-// scene without triangles the same loop as the bounce rays (closest_hit_camera
-// and closest_hit<false> differ only in the triangle loop).
-#ifndef RT_REFILL_CHUNK
-#define RT_REFILL_CHUNK 4
-#endif
-#ifndef RT_REFILL_PARTS
-#define RT_REFILL_PARTS 8
-#endif
-#ifndef RT_REFILL_STATIC
-#define RT_REFILL_STATIC 0
-#endif
-#ifndef RT_REFILL_STRIDE  // words between the parts' counters
-#define RT_REFILL_STRIDE 1024
-#endif
-constexpr unsigned kRefillChunk = RT_REFILL_CHUNK;
-constexpr unsigned kRefillParts = RT_REFILL_PARTS;
-template <int MAXD>
-__global__ __launch_bounds__(64) void rt_refill_kernel(const SceneDev S, const FrameDev F, unsigned* __restrict__ rgba,
-                                                       float* __restrict__ rgbf, unsigned* __restrict__ work, int gx,
-                                                       int gy)
-{
-    const int lane = threadIdx.x & 63;
-    const unsigned long long below = (1ull << lane) - 1ull;
-    const unsigned total = (unsigned)gx * (unsigned)gy * 64u;
-    const Color bg{F.bg[0], F.bg[1], F.bg[2]};
-    unsigned pool = 0, pool_end = 0;  // wave-uniform: the wave's unclaimed items
-    // The items are split into kRefillParts contiguous parts, one counter
-    // each; a wave starts on the part of its XCD (the workgroups are dealt
-    // round-robin to the XCDs) and moves on to the next part when that one
-    // runs dry.  One counter for the whole grid serialises the atomics.
-    unsigned part = kRefillParts > 1 ? (unsigned)blockIdx.x % kRefillParts : 0u, tries = 0;
-    bool drained = false, has = false;
-    Frame stk[MAXD];
-    Refr rf[MAXD];
-    int sp = 0;
-    float rior = 1.0f, energy = 1.0f;
-    Color ret{0.f, 0.f, 0.f};
-    bool trace = false, camera_ray = false;
-    Vec3 O{0.f, 0.f, 0.f}, D{0.f, 0.f, 0.f};
-    size_t o = 0;
-    Counters cnt;
-    for (;;) {
-        if (!drained) {
-            const unsigned long long need = __ballot(!has);
-            if (need) {
-#if RT_REFILL_STATIC  // A/B: each wave's own contiguous run of tiles, no atomics
-                if (pool == pool_end) {
-                    if (tries++ == 0) {
-                        const unsigned long long nt = total / 64u, g = gridDim.x;
-                        pool = (unsigned)(nt * blockIdx.x / g) * 64u;
-                        pool_end = (unsigned)(nt * (blockIdx.x + 1) / g) * 64u;
-                    }
-                    if (pool == pool_end) drained = true;
-                }
-#endif
-                while (pool == pool_end && !drained) {
-                    const unsigned lo = (unsigned)((unsigned long long)(total / 64u) * part / kRefillParts) * 64u;
-                    const unsigned hi = (unsigned)((unsigned long long)(total / 64u) * (part + 1) / kRefillParts) * 64u;
-                    unsigned b = 0;
-                    if (lane == 0) b = atomicAdd(work + part * RT_REFILL_STRIDE, kRefillChunk * 64u);
-                    b = lo + (unsigned)__builtin_amdgcn_readfirstlane((int)b);
-                    if (b < hi) {
-                        pool = b;
-                        pool_end = b + kRefillChunk * 64u < hi ? b + kRefillChunk * 64u : hi;
-                    } else if (++tries >= kRefillParts) {
-                        drained = true;
-                    } else {
-                        part = part + 1 < kRefillParts ? part + 1 : 0u;
-                    }
-                }
-                if (!drained) {
-                    const unsigned avail = pool_end - pool;
-                    const unsigned take = (unsigned)__popcll(need) < avail ? (unsigned)__popcll(need) : avail;
-                    const unsigned rank = (unsigned)__popcll(need & below);
-                    if (!has && rank < take) {
-                        const unsigned idx = pool + rank;
-                        const unsigned t = idx >> 6, l = idx & 63u;
-                        const int tile_x = (int)(t % (unsigned)gx), ly0 = (int)(t / (unsigned)gx) * 8;
-                        int py0 = F.row_begin + ly0, rend = F.row_end;
-                        if (F.band_rows > 0) {
-                            py0 = ((ly0 / F.band_rows) * F.band_count + F.band_index) * F.band_rows + ly0 % F.band_rows;
-                            rend = F.height;
-                        }
-                        const int px = tile_x * 8 + (int)(l & 7u), py = py0 + (int)(l >> 3);
-                        if (px < F.width && py < rend) {
-                            has = true;
-                            o = (size_t)(ly0 + (int)(l >> 3)) * F.width + px;
-                            D = camera_dir(F, px, py);
-                            O = make3(F.cam[0], F.cam[1], F.cam[2]);
-                            sp = 0;
-                            rior = 1.0f;
-                            energy = 1.0f;
-                            trace = true;
-                            camera_ray = true;
-                        }
-                    }
-                    pool += take;
-                }
-            }
-        }
-        if (!__any(has)) {
-            if (drained) break;
-            continue;
-        }
-        // one trace of radiance<MAXD>'s loop per busy lane, then its unwinds
-        // up to the next trace (the same operations in the same order: a
-        // trace that pushes goes on to its child at the next step, one that
-        // does not unwinds in this one)
-        bool pushed = false;
-        if (has && trace) {
-            float t;
-            int idx;
-            // Without triangles the camera-ray path is the generic one: one
-            // loop for camera and bounce lanes alike (a wave mixes them).
-            if (camera_ray && S.n_tri > 0) idx = closest_hit_primary<0>(S, O, D, t, cnt);
-            else idx = closest_hit<false>(S, O, D, t, cnt);
-            camera_ray = false;
-            ret = bg;
-            if (idx >= 0) {
-                const Vec3 N = hit_normal(S, idx, O, D, t);
-                const Mat m = load_mat(S, idx);
-                const Vec3 P = O + t * D;
-                const Color acc = shade_local<1, 0>(S, m, P, N, D, cnt);
-                const float er = m.kr * energy;
-                const float et = m.kt * energy;
-                const bool can = sp < F.max_bounces && sp < MAXD;
-                const bool doR = er > F.min_energy && can;
-                const bool doT = et > F.min_energy && can;
-                if (doR || doT) {
-                    Frame& fr = stk[sp];
-                    fr.acc = acc;
-                    fr.surf = idx;
-                    Vec3 Dt = D;
-                    float rior_t = rior;
-                    if (doT) {
-                        Vec3 n = N;
-                        float ratio;
-                        if (rior == m.ior) {
-                            rior_t = F.scene_ior;
-                            ratio = m.ior / F.scene_ior;
-                            n = -n;
-                        } else {
-                            rior_t = m.ior;
-                            ratio = F.scene_ior / m.ior;
-                        }
-                        Dt = refract(D, n, ratio);
-                    }
-                    O = P;
-                    if (doR) {
-                        fr.stage = doT ? 2 : 0;
-                        if (doT) rf[sp] = Refr{P, Dt, rior_t, et};
-                        D = reflect(D, N);
-                        rior = 0.0f;
-                        energy = er;
-                    } else {
-                        fr.stage = 1;
-                        D = Dt;
-                        rior = rior_t;
-                        energy = et;
-                    }
-                    ++sp;
-                    pushed = true;
-                } else {
-                    ret = acc;
-                }
-            }
-            if (!pushed) trace = false;
-        }
-        // unwind until the lane's next trace (or its end), so that at the
-        // next step every busy lane traces at once
-        while (has && !trace) {
-            if (sp == 0) {
-                if (rgbf) {
-                    rgbf[3 * o] = ret.r;
-                    rgbf[3 * o + 1] = ret.g;
-                    rgbf[3 * o + 2] = ret.b;
-                }
-                if (rgba) rgba[o] = unorm8(ret.r) | (unorm8(ret.g) << 8) | (unorm8(ret.b) << 16) | 0xFF000000u;
-                has = false;
-            } else {
-                Frame& fr = stk[sp - 1];
-                const Mat m = load_mat(S, fr.surf);
-                if (fr.stage != 1) {
-                    fr.acc += ret * m.kr;
-                    if (fr.stage == 2) {
-                        fr.stage = 1;
-                        const Refr r = rf[sp - 1];
-                        O = r.P;
-                        D = r.D;
-                        rior = r.rior;
-                        energy = r.energy;
-                        trace = true;
-                    } else {
-                        ret = fr.acc;
-                        --sp;
-                    }
-                } else {
-                    fr.acc += ret * m.kt;
-                    ret = fr.acc;
-                    --sp;
-                }
-            }
         }
     }
 }
@@ -632,10 +392,7 @@ using namespace rt;
 #define RT_SEQ_STREAMS 4
 #endif
 constexpr int kSeqSlots = RT_SEQ_STREAMS;
-// camera states of rt_render_async's ring (big lists): frame k+1's built
-// while frame k renders
-constexpr int kAsyncSlots = 2;
-constexpr int kCbWordSets = 16;  // camera buffers per context: 1 + sequence slots + ring slots
+constexpr int kCbWordSets = 16;  // camera buffers per context: 1 + sequence slots (spare sets)
 
 struct rt_ctx {
     int device = 0;
@@ -714,25 +471,6 @@ struct rt_ctx {
     } seq[kSeqSlots];
     hipStream_t seq_streams[kSeqSlots] = {};
     hipEvent_t seq_fork = nullptr, seq_join[kSeqSlots] = {};
-    // rt_render_async's own camera states for big lists (round 3): a ring
-    // of kAsyncSlots slots built on an internal stream, so that frame k+1's
-    // camera records and camera buffer are built while frame k's trace
-    // kernel runs.  A slot is rebuilt only after the renders that read it
-    // (its `done` event: each reader records it, after waiting for the
-    // previous one, so it covers them all); a render waits for its slot's
-    // `ready` event.
-    struct ASlot {
-        CamSlot cs;
-        float key[30] = {};
-        bool valid = false, read = false;
-        hipEvent_t ready = nullptr, done = nullptr;
-        unsigned long long used = 0;
-    } aring[kAsyncSlots];
-    hipStream_t abuild = nullptr;
-    unsigned long long ause = 0;
-    bool opt_async_ring = false;
-    bool opt_refill = false;        // RT_OPT_BOUNCE_REFILL
-    unsigned* d_refill = nullptr;   // the refill kernel's work counters, one per launch of a chunked render
     int n_cu = 0;
     std::vector<void*> deferred;  // replaced buffers an enqueued render may read: freed at the next host sync
     void* d_scan = nullptr;     // u64 scratch of the light-buffer build scans
@@ -746,7 +484,6 @@ struct rt_ctx {
     float4* d_lb_dcap = nullptr;
     float4* d_lb_meta = nullptr;
     bool lb_ready = false;
-    bool lb_idx = false;  // cell lists of {triangle, key} entries (RT_OPT_LB_COMPACT)
     int lb_levels = 0;  // buffers per light: slot = level * n_lights + light
     size_t lb_entries = 0;
     double lb_build_ms = 0.0;
@@ -775,7 +512,6 @@ struct rt_ctx {
     int opt_camera_buffer = 1;  // 0 off, 1 auto, 2 async builds for every frame
     bool opt_union = true;
     double opt_lb_scale = 0.0;
-    bool opt_lb_compact = false;
     double opt_dcov_near = 0.0;
     double opt_cb_inline_mb = 0.0;
     double opt_host_chunk_mb = 8.0;
@@ -835,7 +571,6 @@ RT_EXPORT int rt_create(int32_t dev, rt_ctx** out)
     HIP_TRY(c, hipHostMalloc((void**)&c->h_word, 2 * sizeof(unsigned long long), hipHostMallocDefault));
     HIP_TRY(c, hipHostMalloc((void**)&c->h_cbwords, kCbWordSets * 8 * sizeof(unsigned long long), hipHostMallocDefault));
     HIP_TRY(c, hipMalloc(&c->d_stats, kStatSlots * sizeof(StatsDev)));
-    HIP_TRY(c, hipMalloc(&c->d_refill, 16 * kRefillParts * RT_REFILL_STRIDE * sizeof(unsigned)));
     HIP_TRY(c, hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, dev));
     c->far_ladder = {2.5, 6.0, 16.0, 64.0};
     return RT_OK;
@@ -903,7 +638,6 @@ static int sync_all(rt_ctx* c)
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     if (c->copy_stream) HIP_TRY(c, hipStreamSynchronize(c->copy_stream));
     for (hipStream_t s : c->async_streams) HIP_TRY(c, hipStreamSynchronize(s));
-    if (c->abuild) HIP_TRY(c, hipStreamSynchronize(c->abuild));
     c->async_streams.clear();
     c->state_pending = false;
     c->state_stream = nullptr;
@@ -964,9 +698,6 @@ RT_EXPORT int rt_set_option(rt_ctx* c, int32_t opt, double v)
         if (v < 0) return RT_E_ARG;
         c->opt_host_chunk_mb = v;
         return RT_OK;
-    case RT_OPT_ASYNC_RING: c->opt_async_ring = v != 0; return RT_OK;
-    case RT_OPT_BOUNCE_REFILL: c->opt_refill = v != 0; return RT_OK;
-    case RT_OPT_LB_COMPACT: c->opt_lb_compact = v != 0; return RT_OK;
     case RT_OPT_CB_CAPACITY:
         if (v < 0 || v > 4e9 || v != std::floor(v)) return RT_E_ARG;
         if (v != c->opt_cb_capacity) c->cb.valid = false;
@@ -988,9 +719,6 @@ RT_EXPORT int rt_get_option(rt_ctx* c, int32_t opt, double* v)
     case RT_OPT_CB_INLINE_MAX_MB: *v = c->opt_cb_inline_mb; return RT_OK;
     case RT_OPT_HOST_CHUNK_MB: *v = c->opt_host_chunk_mb; return RT_OK;
     case RT_OPT_CB_CAPACITY: *v = c->opt_cb_capacity; return RT_OK;
-    case RT_OPT_ASYNC_RING: *v = c->opt_async_ring ? 1 : 0; return RT_OK;
-    case RT_OPT_BOUNCE_REFILL: *v = c->opt_refill ? 1 : 0; return RT_OK;
-    case RT_OPT_LB_COMPACT: *v = c->opt_lb_compact ? 1 : 0; return RT_OK;
     default: return RT_E_ARG;
     }
 }
@@ -1069,18 +797,7 @@ RT_EXPORT void rt_destroy(rt_ctx* c)
         hipFree(q.uni);
         cb_free(q.cb);
     }
-    for (auto& a : c->aring) {
-        hipFree(a.cs.tricam);
-        hipFree(a.cs.cone_cam);
-        hipFree(a.cs.clu_cam);
-        hipFree(a.cs.uni);
-        cb_free(a.cs.cb);
-        if (a.ready) hipEventDestroy(a.ready);
-        if (a.done) hipEventDestroy(a.done);
-    }
-    if (c->abuild) hipStreamDestroy(c->abuild);
     hipFree(c->d_stats);
-    hipFree(c->d_refill);
     hipFree(c->d_scratch);
     if (c->ev0) hipEventDestroy(c->ev0);
     if (c->ev1) hipEventDestroy(c->ev1);
@@ -1388,7 +1105,7 @@ static int lb_build(rt_ctx* c, int ntr, int n_opaque, const std::vector<const fl
         for (int j = 0; j < nl; ++j) {
             const Slot& b = B[j];
             hipLaunchKernelGGL(rt_lb_cells, dim3(b.nsup), dim3(256), 0, st, cones[j], ntr, c->d_tri, b.R,
-                               (float)dcov[j], d_soff + b.sob, d_slists, nullptr, c->d_lb_off + b.ob, nullptr, 0);
+                               (float)dcov[j], d_soff + b.sob, d_slists, nullptr, c->d_lb_off + b.ob, nullptr);
             LB_TRY(hipGetLastError());
         }
         LB_TRY(scan_u32(c->d_lb_off, (unsigned)ob, c->d_lb_off, (unsigned long long*)c->d_scan, st, &tot));
@@ -1400,16 +1117,14 @@ static int lb_build(rt_ctx* c, int ntr, int n_opaque, const std::vector<const fl
             c->err = "light buffer too large";
             goto done;
         }
-        // big lists with RT_OPT_LB_COMPACT: {triangle, key} entries (rt_lightbuf.h)
-        const int idx_mode = c->opt_lb_compact && ntr > kClusterMinTriangles;
-        LB_TRY(hipMalloc(&c->d_lb_ent, std::max<size_t>(total, 1) * (idx_mode ? 8 : kLbEntF * sizeof(float))));
+        LB_TRY(hipMalloc(&c->d_lb_ent, std::max<size_t>(total, 1) * kLbEntF * sizeof(float)));
         LB_TRY(hipMalloc(&c->d_lb_dcap, std::max<size_t>(dperm_all.size(), 1) * kLbEntF * sizeof(float)));
         LB_TRY(hipMalloc(&c->d_lb_meta, std::max(nl, 1) * 2 * sizeof(float4)));
         std::vector<float4> meta((size_t)std::max(nl, 1) * 2);
         for (int j = 0; j < nl; ++j) {
             const Slot& b = B[j];
             hipLaunchKernelGGL(rt_lb_cells, dim3(b.nsup), dim3(256), 0, st, cones[j], ntr, c->d_tri, b.R,
-                               (float)dcov[j], d_soff + b.sob, d_slists, c->d_lb_off + b.ob, nullptr, (float*)c->d_lb_ent, idx_mode);
+                               (float)dcov[j], d_soff + b.sob, d_slists, c->d_lb_off + b.ob, nullptr, (float*)c->d_lb_ent);
             LB_TRY(hipGetLastError());
             if (b.ndperm) {
                 hipLaunchKernelGGL(rt_lb_dcap, dim3((unsigned)((b.ndperm + 255) / 256)), dim3(256), 0, st, cones[j],
@@ -1430,7 +1145,6 @@ static int lb_build(rt_ctx* c, int ntr, int n_opaque, const std::vector<const fl
         LB_TRY(hipStreamSynchronize(st));  // meta (host) outlives the copy; the temporaries are freed below
         mark(4);
         c->lb_ready = true;
-        c->lb_idx = idx_mode != 0;
         c->lb_entries = total;
     }
 done:
@@ -1593,7 +1307,6 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
     c->d_lb_off = nullptr;
     c->d_lb_ent = c->d_lb_dcap = c->d_lb_meta = nullptr;
     c->lb_ready = false;
-    c->lb_idx = false;
     c->lb_levels = 0;
     c->lb_entries = 0;
     hipFree(c->d_uni);
@@ -1746,26 +1459,6 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
             HIP_TRY(c, hipMemcpyAsync(q.uni, c->d_uni, (size_t)(nl + 1) * 2 * sizeof(float4), hipMemcpyDeviceToDevice, st));
         }
     }
-    // the async ring's slots (big lists only): records of their own, sized
-    // here; their camera buffers are kept (resized on demand)
-    for (auto& a : c->aring) {
-        hipFree(a.cs.tricam);
-        hipFree(a.cs.cone_cam);
-        hipFree(a.cs.clu_cam);
-        hipFree(a.cs.uni);
-        a.cs.tricam = a.cs.cone_cam = a.cs.clu_cam = a.cs.uni = nullptr;
-        a.cs.cb.valid = false;
-        a.valid = false;
-        a.read = false;
-        if (ntr <= (size_t)kClusterMinTriangles) continue;
-        HIP_TRY(c, hipMalloc((void**)&a.cs.tricam, ntr * 4 * sizeof(float4)));
-        HIP_TRY(c, hipMalloc((void**)&a.cs.cone_cam, ntr * kConeRec * sizeof(float4)));
-        HIP_TRY(c, hipMalloc((void**)&a.cs.clu_cam, (size_t)c->n_clu * 4 * sizeof(float4)));
-        if (!a.ready) HIP_TRY(c, hipEventCreateWithFlags(&a.ready, hipEventDisableTiming));
-        if (!a.done) HIP_TRY(c, hipEventCreateWithFlags(&a.done, hipEventDisableTiming));
-    }
-    if (ntr > (size_t)kClusterMinTriangles && !c->abuild)
-        HIP_TRY(c, hipStreamCreateWithFlags(&c->abuild, hipStreamNonBlocking));
     HIP_TRY(c, hipStreamSynchronize(st));
     c->upload_parts_ms[1] = since(tp0);
     const auto tl0 = std::chrono::steady_clock::now();
@@ -1855,14 +1548,11 @@ typedef void (*kernel_fn)(const SceneDev, const FrameDev, unsigned*, float*, Sta
 #define RT_WAVE_LB 1
 #endif
 template <bool COUNT>
-static kernel_fn pick_kernel(int depth, int n_tri, int n_lights, bool lbuf, bool cbuf, int& cap, int& lb,
-                             bool lbidx = false)
+static kernel_fn pick_kernel(int depth, int n_tri, int n_lights, bool lbuf, bool cbuf, int& cap, int& lb)
 {
     lb = 1;
     if (depth == 0 && n_tri > 0 && lbuf) {  // light-buffer shadows, one light per pass
         cap = 0;
-        if (n_tri > kClusterMinTriangles && lbidx)  // compact cell lists (WAVE bit 16)
-            return cbuf ? (kernel_fn)&rt_trace_kernel<0, 1, 30, COUNT> : (kernel_fn)&rt_trace_kernel<0, 1, 22, COUNT>;
         if (n_tri > kClusterMinTriangles)
             return cbuf ? (kernel_fn)&rt_trace_kernel<0, 1, 14, COUNT> : (kernel_fn)&rt_trace_kernel<0, 1, 6, COUNT>;
         return cbuf ? (kernel_fn)&rt_trace_kernel<0, 1, 13, COUNT> : (kernel_fn)&rt_trace_kernel<0, 1, 5, COUNT>;
@@ -1895,69 +1585,29 @@ static kernel_fn pick_kernel(int depth, int n_tri, int n_lights, bool lbuf, bool
     return nullptr;
 }
 
-// Launch shape of a trace kernel over `rows` output rows: 16 x 16-pixel
-// workgroups of 4 waves, or (RT_WG1) one 8 x 8 tile per workgroup.
+// Launch shape of a trace kernel over `rows` output rows: one 8 x 8 tile per
+// workgroup; the big-list kernels get their waves' LDS windows (the staged
+// light-buffer and camera-list walks).
 static void trace_dims(kernel_fn k, int width, int rows, dim3& grid, dim3& block, unsigned& lds)
 {
     const bool big = k == (kernel_fn)&rt_trace_kernel<0, 1, 14, false> || k == (kernel_fn)&rt_trace_kernel<0, 1, 14, true> ||
-                     k == (kernel_fn)&rt_trace_kernel<0, 1, 30, false> || k == (kernel_fn)&rt_trace_kernel<0, 1, 30, true> ||
-                     k == (kernel_fn)&rt_trace_kernel<0, 1, 22, false> || k == (kernel_fn)&rt_trace_kernel<0, 1, 22, true> ||
                      k == (kernel_fn)&rt_trace_kernel<0, 1, 6, false> || k == (kernel_fn)&rt_trace_kernel<0, 1, 6, true> ||
                      k == (kernel_fn)&rt_trace_kernel<0, RT_WAVE_LB, 10, false> ||
                      k == (kernel_fn)&rt_trace_kernel<0, RT_WAVE_LB, 10, true> ||
                      k == (kernel_fn)&rt_trace_kernel<0, RT_WAVE_LB, 2, false> ||
                      k == (kernel_fn)&rt_trace_kernel<0, RT_WAVE_LB, 2, true>;
-    const bool small13 = k == (kernel_fn)&rt_trace_kernel<0, 1, 13, false> ||
-                         k == (kernel_fn)&rt_trace_kernel<0, 1, 13, true>;
-    // the big-list kernels' LDS windows (RT_LB_LDS, RT_CB_LDS): one per wave
-    if ((RT_WG1 == 1 && small13) || (RT_WG1 == 2 && !big) || RT_WG1 == 3) {
-        grid = dim3((width + 7) / 8, (rows + 7) / 8);
-        block = dim3(64);
-    } else {
-        grid = dim3((width + 15) / 16, (rows + 15) / 16);
-        block = dim3(256);
-    }
-    // (the small-list kernels use them only in the A/B builds RT_LB_LDS /
-    // RT_CB_LDS bit 1)
-    const bool windows = big || ((RT_LB_LDS | RT_CB_LDS) & 2);
-    lds = windows ? (unsigned)(block.x / 64 * kLdsWaveBytes) : 0u;
+    grid = dim3((width + 7) / 8, (rows + 7) / 8);
+    block = dim3(64);
+    lds = big ? (unsigned)kLdsWaveBytes : 0u;
 }
 
-// The lane-refill kernel of a bounce-stack capacity (RT_OPT_BOUNCE_REFILL).
-static kernel_fn refill_kernel(int cap)
-{
-#define RT_REFILL(N) \
-    if (N > 0 && cap == N) return (kernel_fn)&rt_refill_kernel<(N > 0 ? N : 1)>;
-    RT_STACK_DEPTHS(RT_REFILL)
-#undef RT_REFILL
-    return nullptr;
-}
-
-// One trace launch over `rows` output rows: the tile grid, or with the
-// refill kernel persistent waves (as many as are resident at once) over the
-// same tiles, counting on work counter `slot`.
-static int launch_trace(rt_ctx* c, kernel_fn k, int cap, bool stats_on, SceneDev& S, FrameDev& F, int width,
-                        int rows, unsigned* oa, float* ob, StatsDev* stats, int slot, hipStream_t st)
+// One trace launch over `rows` output rows.
+static int launch_trace(rt_ctx* c, kernel_fn k, SceneDev& S, FrameDev& F, int width, int rows, unsigned* oa,
+                        float* ob, StatsDev* stats, hipStream_t st)
 {
     dim3 grid, block;
     unsigned lds = 0;
     trace_dims(k, width, rows, grid, block, lds);
-    kernel_fn rk = (c->opt_refill && cap > 0 && !stats_on) ? refill_kernel(cap) : nullptr;
-    if (rk) {
-        int per_cu = 0;
-        HIP_TRY(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)rk, 64, 0));
-        const long tiles = (long)grid.x * grid.y;
-        #ifndef RT_REFILL_GRID_MUL
-#define RT_REFILL_GRID_MUL 1
-#endif
-        const long waves = std::min(tiles, (long)std::max(1, per_cu) * std::max(1, c->n_cu) * RT_REFILL_GRID_MUL);
-        int gx = (int)grid.x, gy = (int)grid.y;
-        unsigned* work = c->d_refill + (size_t)slot * kRefillParts * RT_REFILL_STRIDE;
-        HIP_TRY(c, hipMemsetAsync(work, 0, kRefillParts * RT_REFILL_STRIDE * sizeof(unsigned), st));
-        void* args[] = {&S, &F, &oa, &ob, &work, &gx, &gy};
-        HIP_TRY(c, hipLaunchKernel((const void*)rk, dim3((unsigned)waves), dim3(64), args, 0, st));
-        return RT_OK;
-    }
     void* args[] = {&S, &F, &oa, &ob, &stats};
     HIP_TRY(c, hipLaunchKernel((const void*)k, grid, block, args, lds, st));
     return RT_OK;
@@ -2424,66 +2074,6 @@ static bool cb_async_pays(const rt_ctx* c, const rt_frame* f)
     return c->n_tri > kClusterMinTriangles && (double)f->width * frame_rows(f) >= 4e6;
 }
 
-// The async ring (rt_render_async, big lists): the slot holding frame f's
-// camera (position, orientation, film and tile rows), or the least recently
-// used one rebuilt for it on c->abuild — after every render that read it —
-// while the renders already enqueued run.  st then waits for the slot.
-static int ring_prepare(rt_ctx* c, const rt_frame* f, hipStream_t st, rt_ctx::ASlot*& out)
-{
-    float key[30];
-    cb_key_of(f, key);
-    rt_ctx::ASlot* hit = nullptr;
-    for (auto& a : c->aring) {
-        cb_harvest(a.cs.cb);
-        if (a.valid && a.cs.cb.valid && std::memcmp(a.key, key, sizeof key) == 0) hit = &a;
-    }
-    if (!hit) {
-        hit = &c->aring[0];
-        for (auto& a : c->aring)
-            if (a.used < hit->used) hit = &a;
-        rt_ctx::ASlot& a = *hit;
-        a.valid = false;
-        if (a.read) HIP_TRY(c, hipStreamWaitEvent(c->abuild, a.done, 0));
-        if (int rc = camera_records(c, f->cam_pos, c->abuild, true, a.cs.tricam, a.cs.cone_cam, a.cs.uni,
-                                    a.cs.clu_cam))
-            return rc;
-        SceneDev S = scene_dev(c, false, false);
-        S.tricam = a.cs.tricam;
-        S.cone_cam = a.cs.cone_cam;
-        S.clu_cam = a.cs.clu_cam;
-        S.uni = nullptr;
-        if (int rc = cb_build(c, a.cs.cb, f, S, c->abuild, false, false, false)) return rc;
-        HIP_TRY(c, hipEventRecord(a.ready, c->abuild));
-        std::memcpy(a.key, key, sizeof key);
-        a.valid = true;
-    }
-    hit->used = ++c->ause;
-    HIP_TRY(c, hipStreamWaitEvent(st, hit->ready, 0));
-    // readers on several streams: the done event this render records must
-    // also cover the previous reader
-    if (hit->read) HIP_TRY(c, hipStreamWaitEvent(st, hit->done, 0));
-    out = hit;
-    return RT_OK;
-}
-
-// The slot's records and camera buffer in a render's scene.
-static void ring_scene(const rt_ctx::ASlot* a, SceneDev& S, bool cbuf)
-{
-    S.tricam = a->cs.tricam;
-    S.cone_cam = a->cs.cone_cam;
-    S.clu_cam = a->cs.clu_cam;
-    S.uni = nullptr;
-    if (cbuf) {
-        S.cb_off = a->cs.cb.off;
-        S.cb_ent = a->cs.cb.ent;
-        S.cb_flag = a->cs.cb.flag;
-        S.cb_tiles_x = a->cs.cb.tiles_x;
-    } else {
-        S.cb_tiles_x = 0;
-    }
-    S.cb_rec = nullptr;
-}
-
 // Make the per-camera state current for frame f, ordered on stream st: the
 // camera prepass when the camera moved, and the camera buffer when the
 // frame's kernel uses one and it is not current.  sync_path: a synchronous
@@ -2564,26 +2154,18 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
     const bool lbuf = c->lb_ready && (mode == 1 || (mode == 2 && c->n_tri > kClusterMinTriangles));
     const bool cb_want = depth == 0 && c->n_tri > 0 && c->opt_camera_buffer && cb_frame_ok(f);
     const int rows = frame_rows(f);
-    // big lists, async, a camera the context's own state does not hold:
-    // the async ring (its state built on c->abuild, overlapping the
-    // renders already enqueued)
-    rt_ctx::ASlot* ring = nullptr;
-    if (rows > 0 && !sync_path && !capturing && cb_want && c->opt_async_ring && c->abuild && cb_async_pays(c, f) &&
-        (camera_needs_prepass(c, f, true) || !cb_matches(c->cb, f))) {
-        if (int rc = ring_prepare(c, f, st, ring)) return rc;
-    } else if (rows > 0) {
+    if (rows > 0) {
         if (int rc = prepare_state(c, f, st, sync_path, capturing, cb_want)) return rc;
     }
-    const bool cbuf = cb_want && (ring ? ring->cs.cb.valid : cb_matches(c->cb, f));
+    const bool cbuf = cb_want && cb_matches(c->cb, f);
     kernel_fn k = (f->flags & RT_FLAG_STATS)
-                      ? pick_kernel<true>(depth, c->n_tri, c->n_lights, lbuf, cbuf, cap, lb, lbuf && c->lb_idx)
-                      : pick_kernel<false>(depth, c->n_tri, c->n_lights, lbuf, cbuf, cap, lb, lbuf && c->lb_idx);
+                      ? pick_kernel<true>(depth, c->n_tri, c->n_lights, lbuf, cbuf, cap, lb)
+                      : pick_kernel<false>(depth, c->n_tri, c->n_lights, lbuf, cbuf, cap, lb);
     if (!k) {
         c->err = "reachable bounce depth " + std::to_string(depth) + " exceeds the compiled stack (32)";
         return RT_E_UNSUPPORTED;
     }
     SceneDev S = scene_dev(c, lbuf, cbuf);
-    if (ring) ring_scene(ring, S, cbuf);
     FrameDev F;
     frame_dev(f, F);
     c->last = rt_stats{};
@@ -2602,9 +2184,8 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
     const int nch = (host_out && f->band_rows == 0 && chunk > 0)
                         ? (int)std::min(8.0, std::floor((double)out_bytes / chunk))
                         : 1;
-    const bool stats_on = (f->flags & RT_FLAG_STATS) != 0;
     if (nch <= 1) {
-        if (int rc = launch_trace(c, k, cap, stats_on, S, F, f->width, rows, rgba_dev, rgb_dev, stats, 0, st)) return rc;
+        if (int rc = launch_trace(c, k, S, F, f->width, rows, rgba_dev, rgb_dev, stats, st)) return rc;
         if (host_out)
             HIP_TRY(c, hipMemcpyAsync(host_out, rgba_dev ? (void*)rgba_dev : (void*)rgb_dev,
                                       (size_t)rows * f->width * px_bytes, hipMemcpyDeviceToHost, st));
@@ -2620,7 +2201,7 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
             Fc.row_end = f->row_begin + r1;
             unsigned* oa = rgba_dev ? rgba_dev + (size_t)r0 * f->width : nullptr;
             float* ob = rgb_dev ? rgb_dev + (size_t)r0 * f->width * 3 : nullptr;
-            if (int rc = launch_trace(c, k, cap, stats_on, S, Fc, f->width, r1 - r0, oa, ob, stats, n, st)) return rc;
+            if (int rc = launch_trace(c, k, S, Fc, f->width, r1 - r0, oa, ob, stats, st)) return rc;
             HIP_TRY(c, hipEventRecord(c->ev_chunk[n], st));
         }
         if (timed) HIP_TRY(c, hipEventRecord(c->ev1, st));
@@ -2640,10 +2221,6 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
         if (cbuf) c->cb.pinned = true;
     } else if (!sync_path) {
         note_async(c, st);
-    }
-    if (ring) {  // this render read the slot: its done event now covers it
-        HIP_TRY(c, hipEventRecord(ring->done, st));
-        ring->read = true;
     }
     return RT_OK;
 }
@@ -2809,7 +2386,7 @@ RT_EXPORT int rt_render_sequence_async(rt_ctx* c, const rt_frame* frames, int32_
             if (int rc = camera_records(c, f->cam_pos, fs, cbuf, q.tricam, q.cone_cam, q.uni, q.clu_cam)) return rc;
         }
         int cap = 0, lb = 1;
-        kernel_fn k = pick_kernel<false>(depth, c->n_tri, c->n_lights, lbuf, cbuf, cap, lb, lbuf && c->lb_idx);
+        kernel_fn k = pick_kernel<false>(depth, c->n_tri, c->n_lights, lbuf, cbuf, cap, lb);
         SceneDev S = scene_dev(c, lbuf, false);
         S.tricam = q.tricam;
         S.cone_cam = q.cone_cam;

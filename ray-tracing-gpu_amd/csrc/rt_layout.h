@@ -35,9 +35,6 @@ namespace rt {
 // Cone records per apex, rt_cone_prepass: kConeRec float4 per triangle, as
 // [2 x n_tri: c0 c1 per triangle][3 x n_tri: the three edge planes].
 constexpr int kConeRec = 5;
-#ifndef RT_EDGES
-#define RT_EDGES 1
-#endif
 
 struct SceneDev {
     const float4* __restrict__ geom;    // file order, 64-byte records (above)

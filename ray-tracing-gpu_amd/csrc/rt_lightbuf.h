@@ -31,11 +31,8 @@ namespace rt {
 // per-lane predicate light_reach, split in two.
 constexpr int kLbGroup = 16;  // cells per supercell edge (two-level build)
 // Light-buffer entry: 10 floats (40 B, 8-byte aligned) — [p0, key] [e1,
-// e2.x] [e2.y, e2.z]; RT_LB_E40 0 pads it to 48 B (the round-2 layout).
-#ifndef RT_LB_E40
-#define RT_LB_E40 1
-#endif
-constexpr int kLbEntF = RT_LB_E40 ? 10 : 12;  // floats per light-buffer entry
+// e2.x] [e2.y, e2.z] (48 B in round 2: C3 313 -> 269 MB per frame).
+constexpr int kLbEntF = 10;  // floats per light-buffer entry
 
 __device__ __forceinline__ int lb_cell(const Vec3 d, int R)
 {
@@ -208,29 +205,13 @@ __device__ __forceinline__ float2 lb_tail(const float* r)
     return make_float2(v.x, v.y);
 }
 
-// Compact cell lists (RT_OPT_LB_COMPACT, big lists): entries are
-// {triangle, key} (8 B) and the walk reads the triangle's tri[] record (48 B
-// per triangle, 2.4 MB for the 50k heightfield: L2-resident) — 8 B per entry
-// from the fabric and in HBM instead of 40.  The dcap lists keep whole
-// entries.
-template <bool IDX>
-__device__ __forceinline__ void lb_cell_entry(const float4* __restrict__ ent, const float4* __restrict__ tri, size_t q,
-                                              float4& a, float4& b, float2& c)
+// A cell-list entry: p0 and the key; e1 and e2.x; e2.yz.
+__device__ __forceinline__ void lb_cell_entry(const float4* __restrict__ ent, size_t q, float4& a, float4& b, float2& c)
 {
-    if constexpr (IDX) {
-        const uint2 en = reinterpret_cast<const uint2*>(ent)[q];
-        const float4* t = tri + 3 * (size_t)en.x;
-        const float4 t0 = t[0], t1 = t[1];
-        const float t2 = reinterpret_cast<const float*>(t + 2)[0];
-        a = make_float4(t0.x, t0.y, t0.z, __uint_as_float(en.y));
-        b = make_float4(t0.w, t1.x, t1.y, t1.z);
-        c = make_float2(t1.w, t2);
-    } else {
-        const float* r = lb_rec(ent, q);
-        a = lb_a(r);
-        b = lb_b(r);
-        c = lb_tail(r);
-    }
+    const float* r = lb_rec(ent, q);
+    a = lb_a(r);
+    b = lb_b(r);
+    c = lb_tail(r);
 }
 
 __device__ __forceinline__ void lb_write(float* o, const float4* __restrict__ tri, int k, float key)
@@ -242,7 +223,6 @@ __device__ __forceinline__ void lb_write(float* o, const float4* __restrict__ tr
     w[2] = lb_v2{a.w, b.x};
     w[3] = lb_v2{b.y, b.z};
     w[4] = lb_v2{b.w, c.x};
-    if (kLbEntF == 12) w[5] = lb_v2{0.0f, 0.0f};
 }
 
 // Build pass 2: one thread per cell of a supercell, over the supercell's
@@ -250,7 +230,7 @@ __device__ __forceinline__ void lb_write(float* o, const float4* __restrict__ tr
 __global__ __launch_bounds__(256) void rt_lb_cells(const float4* __restrict__ cone, int n, const float4* __restrict__ tri,
                                                    int R, float dcov, const unsigned* __restrict__ soffs,
                                                    const int* __restrict__ slists, const unsigned* __restrict__ coffs,
-                                                   unsigned* __restrict__ ccounts, float* __restrict__ ent, int idx)
+                                                   unsigned* __restrict__ ccounts, float* __restrict__ ent)
 {
     const int G = R / kLbGroup;
     const int s = blockIdx.x;
@@ -277,8 +257,7 @@ __global__ __launch_bounds__(256) void rt_lb_cells(const float4* __restrict__ co
         for (int x = 0; x < m; ++x) {
             const float4 c0 = rec[kConeRec * x], c1 = rec[kConeRec * x + 1];
             if (!lb_keep(wc, c0, c1, rec + kConeRec * x + 2, dcov)) continue;
-            if (ent && idx) reinterpret_cast<uint2*>(ent)[out++] = make_uint2((unsigned)kid[x], __float_as_uint(c1.x));
-            else if (ent) lb_write(ent + kLbEntF * (size_t)out++, tri, kid[x], c1.x);
+            if (ent) lb_write(ent + kLbEntF * (size_t)out++, tri, kid[x], c1.x);
             else ++cnt;
         }
     }

@@ -268,7 +268,7 @@ __device__ __forceinline__ void shadow_wave_batch(const SceneDev& S, const float
     const int k = k0 + (int)(threadIdx.x & 63);
     // every record load of the batch first (one wait), then the tests
     float4 c0[kLightBatch], c1[kLightBatch], ed[kLightBatch][3];
-    const bool edges = RT_EDGES && S.use_edges;
+    const bool edges = S.use_edges;
 #pragma unroll
     for (int j = 0; j < kLightBatch; ++j) {
         c0[j] = make_float4(0.f, 0.f, 0.f, 1.f);
@@ -391,11 +391,7 @@ __device__ __forceinline__ void shadow_opaque_wave(const SceneDev& S, int l0, in
         }
     }
     RT_MARK(cnt, 3);
-#ifndef RT_ABLATE_SHADOW_PLANE  // timing-only build: no plane shadow tests
     for (int k = 0; k < S.n_plane_opaque; ++k) {
-#else
-    for (int k = 0; k < 0; ++k) {
-#endif
         const float4 a = S.plane[2 * k];
 #pragma unroll
         for (int j = 0; j < kLightBatch; ++j) {
@@ -422,8 +418,8 @@ __device__ __forceinline__ void shadow_opaque_wave(const SceneDev& S, int l0, in
     }
 }
 
-// LDS-staged per-lane walk (RT_LB_LDS: on for the big-list kernel, C5 -11%,
-// C3 -6.5%; bit 1 would add the small-list kernel, measured slower): when
+// LDS-staged per-lane walk (the big-list kernel: C5 -11%, C3 -6.5%; the
+// small-list kernel measured slower with it): when
 // the wave's lanes fall in a few cells, every still-active lane of one cell is
 // at the same entry of its list (each active lane consumes one entry per
 // iteration), so the wave stages the next W entries of every cell's list in
@@ -431,28 +427,8 @@ __device__ __forceinline__ void shadow_opaque_wave(const SceneDev& S, int l0, in
 // their entries from LDS — one load latency per W entries instead of a
 // dependent gather per entry.  Same tests, same order per lane: the any-hit
 // result is the global walk's.  Returns false (nothing done) for more cells
-// than it stages (RT_LB_LDS_G).
-#ifndef RT_LB_LDS
-#define RT_LB_LDS 1
-#endif
-#if RT_LB_LDS
-#ifndef RT_LB_LDS_G
-#define RT_LB_LDS_G 4
-#endif
-#ifndef RT_LB_LDS_ONE  // also the one-cell walk (window of 1 << RT_LB_LDS_SH1 entries)
-#define RT_LB_LDS_ONE 0
-#endif
-#ifndef RT_LB_LDS_SH1
-#define RT_LB_LDS_SH1 4
-#endif
-#ifndef RT_LB_LDS_PF  // prefetch the next window into registers
-#define RT_LB_LDS_PF 0
-#endif
-#ifndef RT_LB_LDS_UBR  // v and t only where some lane's u is in [0, 1]
-#define RT_LB_LDS_UBR 1
-#endif
-constexpr int kLbLdsG = RT_LB_LDS_G;      // most cells a wave stages
-template <bool IDX>
+// than it stages (kLbLdsG).
+constexpr int kLbLdsG = 4;  // most cells a wave stages
 __device__ __forceinline__ bool lb_walk_lds(const SceneDev& S, bool use, int cell, unsigned e, unsigned end,
                                             const Vec3 P, const Vec3 L, float dist, bool& occ, Counters& cnt)
 {
@@ -477,12 +453,9 @@ __device__ __forceinline__ bool lb_walk_lds(const SceneDev& S, bool use, int cel
         }
     }
     if (rem) return false;
-#ifdef RT_ABLATE_LBMULTI  // timing-only build: no multi-cell walk
-    return true;
-#endif
     // window per cell: the capacity over the cell count rounded up to a power of 2
     const int lg = ng <= 1 ? 0 : 32 - __builtin_clz((unsigned)(ng - 1));
-    const int sh = ng <= 1 ? RT_LB_LDS_SH1 : __builtin_ctz((unsigned)kLbLdsCap) - lg;
+    const int sh = __builtin_ctz((unsigned)kLbLdsCap) - lg;
     const unsigned wmask = (1u << sh) - 1u;
     const LdsWin win = lds_window();
     const unsigned long long ex = __ballot(true);
@@ -491,14 +464,6 @@ __device__ __forceinline__ bool lb_walk_lds(const SceneDev& S, bool use, int cel
     bool have = use & (e < end);
     unsigned k = 0;  // entries each active lane has consumed (wave-uniform)
     const int nslots = ng << sh;
-#if RT_LB_LDS_PF
-    // every slot of a window has its own lane: the next window's entries are
-    // loaded into registers while this one is walked
-    const bool pf = nslots <= nact;
-    float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa;
-    float2 pc = make_float2(0.f, 0.f);
-    bool pv = false;
-#endif
     for (;;) {
         const bool act = have & !occ;
         const unsigned long long ba = __ballot(act);
@@ -509,15 +474,6 @@ __device__ __forceinline__ bool lb_walk_lds(const SceneDev& S, bool use, int cel
             for (int i = 0; i < kLbLdsG; ++i) gact |= (ba & gm[i]) ? (1u << i) : 0u;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
-#if RT_LB_LDS_PF
-            if (pf && k > 0) {
-                if (pv) {
-                    win.a[rk] = pa;
-                    win.b[rk] = pb;
-                    win.c[rk] = pc;
-                }
-            } else
-#endif
             for (int s = rk; s < nslots; s += nact) {
                 const int gi = s >> sh;
                 unsigned q0 = gp[0], q1 = ge[0];
@@ -530,31 +486,12 @@ __device__ __forceinline__ bool lb_walk_lds(const SceneDev& S, bool use, int cel
                 if (((gact >> gi) & 1u) && q < q1) {
                     float4 a, b;
                     float2 c;
-                    lb_cell_entry<IDX>(S.lb_ent, S.tri, q, a, b, c);
+                    lb_cell_entry(S.lb_ent, q, a, b, c);
                     win.a[s] = a;
                     win.b[s] = b;
                     win.c[s] = c;
                 }
             }
-#if RT_LB_LDS_PF
-            if (pf) {  // issue the next window's loads (waited for at the next boundary)
-                pv = false;
-                if (rk < nslots) {
-                    const int gi = rk >> sh;
-                    unsigned q0 = gp[0], q1 = ge[0];
-#pragma unroll
-                    for (int i = 1; i < kLbLdsG; ++i) {
-                        q0 = gi == i ? gp[i] : q0;
-                        q1 = gi == i ? ge[i] : q1;
-                    }
-                    const unsigned q = q0 + k + (wmask + 1u) + ((unsigned)rk & wmask);
-                    if (((gact >> gi) & 1u) && q < q1) {
-                        lb_cell_entry<IDX>(S.lb_ent, S.tri, q, pa, pb, pc);
-                        pv = true;
-                    }
-                }
-            }
-#endif
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -583,10 +520,7 @@ __device__ __forceinline__ bool lb_walk_lds(const SceneDev& S, bool use, int cel
             if (go) {
                 const Vec3 e1 = make3(c1.x, c1.y, c1.z), e2 = make3(c1.w, c2.x, c2.y);
                 const TriU u = tri_u(make3(c0.x, c0.y, c0.z), e1, e2, P, L);
-#if RT_LB_LDS_UBR
-                if (__any(u.ok))
-#endif
-                {
+                if (__any(u.ok)) {  // v and t only where some lane's u is in [0, 1]
                     float t;
                     const bool ok = tri_vt(u, e1, e2, L, t);
                     occ |= ok & (t > kEps) & (t < dist);
@@ -596,23 +530,17 @@ __device__ __forceinline__ bool lb_walk_lds(const SceneDev& S, bool use, int cel
     }
     return true;
 }
-#endif
 
 // One buffer slot's walk for the lanes in `cand` (slot = a light, or
 // n_lights + the light for its far buffer): the lanes whose dist the slot
 // covers (dist <= its dcov) look their cell up, walk its list, then the
 // slot's dcap list while their dist exceeds the entries' caps.  Returns
 // those lanes (the covered ones).
-// PIPE: the per-lane walk issues the next entry's gathers before the
-// current entry's test (long lists: C3, C5); without it the walk holds 12
-// fewer VGPRs (short lists).
-// pre: the lanes' cell list bounds [pe, pn) were loaded ahead (lb_prefetch:
-// every lane that can use the slot has them).
-// IDX: the cell lists hold {triangle, key} entries (RT_OPT_LB_COMPACT,
-// big lists; lb_cell_entry).
-template <bool PIPE, bool IDX>
+// BIG (the big-list kernel): multi-cell waves walk staged in LDS, and lanes
+// beyond a level's dcov take the next level of the ladder.
+template <bool BIG>
 __device__ __forceinline__ bool lb_slot(const SceneDev& S, int slot, const Vec3 P, const Vec3 L, float dist, bool cand,
-                                        bool& occ, Counters& cnt, bool pre = false, unsigned pe = 0, unsigned pn = 0)
+                                        bool& occ, Counters& cnt)
 {
     const float4 m0 = S.lb_meta[2 * slot], m1 = S.lb_meta[2 * slot + 1];
     const unsigned obase = __float_as_uint(m0.x), dbase = __float_as_uint(m0.y), ndcap = __float_as_uint(m0.z);
@@ -636,40 +564,15 @@ __device__ __forceinline__ bool lb_slot(const SceneDev& S, int slot, const Vec3 
         if (one_cell) RT_EV(cnt, 0);
         else RT_EV(cnt, 1);
     }
-#if RT_LB_LDS && RT_LB_LDS_ONE
-    constexpr bool lds_one = (RT_LB_LDS & (PIPE ? 1 : 2)) != 0;
-#else
-    constexpr bool lds_one = false;
-#endif
-    if (one_cell && !lds_one) {
-        unsigned q0, q1;
-        if (pre) {
-            const int fl = (int)__builtin_ctzll(bu);
-            q0 = (unsigned)__builtin_amdgcn_readlane((int)pe, fl);
-            q1 = (unsigned)__builtin_amdgcn_readlane((int)pn, fl);
-        } else {
-            const unsigned* o = S.lb_off + obase + cf;
-            q0 = o[0];
-            q1 = o[1];
-        }
-#ifdef RT_ABLATE_LBCELL  // timing-only build: no cell walk
-        for (unsigned q = q0; q < q0; ++q) {
-#else
+    if (one_cell) {
+        const unsigned* o = S.lb_off + obase + cf;
+        const unsigned q0 = o[0], q1 = o[1];
         for (unsigned q = q0; q < q1; ++q) {
-#endif
-            float4 c0, c1;
-            float2 c2;
-            if constexpr (IDX) {  // {triangle, key}: the key, then the record
-                const uint2 en = reinterpret_cast<const uint2*>(S.lb_ent)[q];
-                if (!__any(use & !occ & (__uint_as_float(en.y) < dist))) break;
-                lb_cell_entry<IDX>(S.lb_ent, S.tri, q, c0, c1, c2);
-            } else {
-                const float* r = lb_rec(S.lb_ent, q);
-                c0 = lb_a(r);
-                if (!__any(use & !occ & (c0.w < dist))) break;
-                c1 = lb_b(r);
-                c2 = lb_tail(r);
-            }
+            const float* r = lb_rec(S.lb_ent, q);
+            const float4 c0 = lb_a(r);
+            if (!__any(use & !occ & (c0.w < dist))) break;
+            const float4 c1 = lb_b(r);
+            const float2 c2 = lb_tail(r);
             const bool act = use & !occ & (c0.w < dist);
             ++cnt.tri;
             RT_EV(cnt, 4);
@@ -684,56 +587,29 @@ __device__ __forceinline__ bool lb_slot(const SceneDev& S, int slot, const Vec3 
             }
         }
     } else if (use) {
-        if (pre) {
-            e = pe;
-            end = pn;
-        } else {
-            const unsigned* o = S.lb_off + obase + cell;
-            e = o[0];
-            end = o[1];
-        }
+        const unsigned* o = S.lb_off + obase + cell;
+        e = o[0];
+        end = o[1];
     }
-#if RT_LB_LDS
-    if ((RT_LB_LDS & (PIPE ? 1 : 2)) && (!one_cell || lds_one) && bu && lb_walk_lds<IDX>(S, use, cell, e, end, P, L, dist, occ, cnt))
+    // big lists: waves over 2-4 cells walk their lists staged in LDS
+    if (BIG && !one_cell && bu && lb_walk_lds(S, use, cell, e, end, P, L, dist, occ, cnt))
         end = e;  // walked: skip the global walk below
-#endif
-    // The next entry's loads are issued before the current entry's exact
-    // test (software pipelining of the per-lane gathers; PG — only waves
-    // over more than the staged cells walk here in the big-list kernel).
-#ifndef RT_LB_PIPE_GLOBAL
-#define RT_LB_PIPE_GLOBAL 0
-#endif
-    constexpr bool PG = PIPE && RT_LB_PIPE_GLOBAL;
-    float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0;
-    float2 r2 = make_float2(0.f, 0.f);
-#ifdef RT_ABLATE_LBCELL  // timing-only build: no cell walk
-    bool have = false;
-#else
     bool have = e < end;
-#endif
-    if (PG && have) {
-        lb_cell_entry<IDX>(S.lb_ent, S.tri, e, r0, r1, r2);
-    }
     for (;;) {
         const bool act = have & !occ;
         if (!__any(act)) break;
         RT_EV(cnt, 3);
         bool go = false;
-        if (!PG && act) {
-            lb_cell_entry<IDX>(S.lb_ent, S.tri, e, r0, r1, r2);
-        }
-        const float4 c0 = r0, c1 = r1;
-        const float2 c2 = r2;
+        float4 c0 = make_float4(0.f, 0.f, 0.f, 0.f), c1 = c0;
+        float2 c2 = make_float2(0.f, 0.f);
         if (act) {
+            lb_cell_entry(S.lb_ent, e, c0, c1, c2);
             if (!(c0.w < dist)) {
                 have = false;  // this and every later entry lie beyond P (dmin)
             } else {
                 go = true;
                 ++e;
                 have = e < end;
-                if (PG && have) {
-                    lb_cell_entry<IDX>(S.lb_ent, S.tri, e, r0, r1, r2);
-                }
             }
         }
         if (__any(go)) {
@@ -754,11 +630,7 @@ __device__ __forceinline__ bool lb_slot(const SceneDev& S, int slot, const Vec3 
     RT_MARK(cnt, 4);
     // pairs not culled up to dcov: sorted by dcap, so once no live lane lies
     // beyond an entry's cap none lies beyond a later one
-#ifdef RT_ABLATE_LBLIST  // timing-only build: no per-light list
-    for (unsigned q = 0; q < 0; ++q) {
-#else
     for (unsigned q = 0; q < ndcap; ++q) {
-#endif
         const float* r = lb_rec(S.lb_dcap, dbase + q);
         const float4 r0 = lb_a(r);
         const bool need = use & !occ & (dist > r0.w);
@@ -786,10 +658,9 @@ __device__ __forceinline__ bool lb_slot(const SceneDev& S, int slot, const Vec3 
 // within the light's buffer distance walk it (lb_slot); with far buffers
 // (big lists, S.lb_R levels) the lanes beyond walk the next level's; lanes
 // no buffer covers take the per-lane loop over every triangle.
-template <bool PIPE, bool IDX>
+template <bool BIG>
 __device__ __forceinline__ void shadow_opaque_lb(const SceneDev& S, int l, const Vec3 P, const Vec3 L, float dist,
-                                                 bool& occ, Counters& cnt, bool pre = false, unsigned pe = 0,
-                                                 unsigned pn = 0)
+                                                 bool& occ, Counters& cnt)
 {
     for (int k = 0; k < S.n_plane_opaque; ++k) {
         if (!__any(!occ)) return;
@@ -799,11 +670,11 @@ __device__ __forceinline__ void shadow_opaque_lb(const SceneDev& S, int l, const
     {
     const float mx = fmaxf(fabsf(L.x), fmaxf(fabsf(L.y), fabsf(L.z)));
     const bool cand = !occ & (mx >= 0.5f);  // a direction the lookup takes
-    bool use = lb_slot<PIPE, IDX>(S, l, P, L, dist, cand, occ, cnt, pre, pe, pn);
-    if constexpr (PIPE) {  // big lists: lanes beyond a buffer take the next
+    bool use = lb_slot<BIG>(S, l, P, L, dist, cand, occ, cnt);
+    if constexpr (BIG) {  // big lists: lanes beyond a buffer take the next
         for (int lv = 1; lv < S.lb_R; ++lv) {
             if (!__any(cand & !use & !occ)) break;
-            use |= lb_slot<PIPE, IDX>(S, lv * S.n_lights + l, P, L, dist, cand & !use, occ, cnt);
+            use |= lb_slot<BIG>(S, lv * S.n_lights + l, P, L, dist, cand & !use, occ, cnt);
         }
     }
     const float slack = dist * 1e-6f;
@@ -866,46 +737,13 @@ __device__ __forceinline__ void add_light(Color& res, const Mat& m, const float4
         // pow(x, 0) == 1 for every x (C99 F.9.4.4, glibc and ocml alike):
         // materials without a shininess never pay for powf.
         float pw = 1.0f;
-#ifdef RT_ABLATE_POWF  // timing-only build: no powf
-        if (m.shin != 0.0f) pw = ps * m.shin;
-#else
         if (m.shin != 0.0f) pw = powf(ps, m.shin);
-#endif
         const float pf = l0.w * m.ks * pw;
         res += LC * pf;
     }
 }
 
-#ifndef RT_LB_PIPE
-#define RT_LB_PIPE(WAVE) (((WAVE) & 2) != 0)
-#endif
 
-// Light li's level-0 cell list bounds for every lane that can use its
-// buffer (gate, a direction the lookup takes, within dcov): the same light
-// vector, distance and cell lb_slot computes, loaded one light ahead so the
-// gathers overlap the previous light's walk instead of heading its own
-// dependent chain (cell -> bounds -> entries).
-__device__ __forceinline__ void lb_prefetch(const SceneDev& S, int li, const Vec3 P, const Vec3 N, bool active,
-                                            unsigned& e, unsigned& n)
-{
-    const float4 l0 = S.lights[2 * li];
-    const Vec3 Lr = make3(l0.x, l0.y, l0.z) - P;
-    const bool gate = active & (dot(Lr, N) > 0);
-    const float dist = sqrt_w(Lr.x * Lr.x + Lr.y * Lr.y + Lr.z * Lr.z);
-    const Vec3 L = Lr * recip_w(dist);
-    const float4 m0 = S.lb_meta[2 * li], m1 = S.lb_meta[2 * li + 1];
-    const int R = __float_as_int(m0.w);
-    const float mx = fmaxf(fabsf(L.x), fmaxf(fabsf(L.y), fabsf(L.z)));
-    e = n = 0;
-    if (gate & (mx >= 0.5f) & (dist <= m1.x) & (R > 0)) {
-        const unsigned* o = S.lb_off + __float_as_uint(m0.x) + lb_cell(-L, R);
-        e = o[0];
-        n = o[1];
-    }
-}
-#ifndef RT_LB_PREFETCH
-#define RT_LB_PREFETCH 0
-#endif
 template <int kLightBatch, int WAVE>
 __device__ __forceinline__ Color shade_local(const SceneDev& S, const Mat& m, const Vec3 P, const Vec3 N,
                                              const Vec3 D, Counters& cnt, bool active = true)
@@ -926,13 +764,7 @@ __device__ __forceinline__ Color shade_local(const SceneDev& S, const Mat& m, co
         return res;
     }
     if constexpr ((WAVE & 4) != 0) {  // light buffer: one light at a time, file order
-        // small lists: the next light's cell bounds are loaded a light ahead
-        constexpr bool PF = RT_LB_PREFETCH && !RT_LB_PIPE(WAVE);
-        unsigned ne = 0, nn = 0;
-        if (PF && S.n_lights > 0) lb_prefetch(S, 0, P, N, active, ne, nn);
         for (int li = 0; li < S.n_lights; ++li) {
-            const unsigned ce = ne, cn = nn;
-            if (PF && li + 1 < S.n_lights) lb_prefetch(S, li + 1, P, N, active, ne, nn);
             const float4 l0 = S.lights[2 * li], l1 = S.lights[2 * li + 1];
             const Vec3 Lr = make3(l0.x, l0.y, l0.z) - P;
             const bool gate = active & (dot(Lr, N) > 0);  // Scene.cpp:1756, unnormalised
@@ -941,9 +773,7 @@ __device__ __forceinline__ Color shade_local(const SceneDev& S, const Mat& m, co
             cnt.shadow += gate;
             bool occ = !gate;
             RT_MARK(cnt, 2);
-#ifndef RT_ABLATE_SHADOW
-            shadow_opaque_lb<RT_LB_PIPE(WAVE), (WAVE & 16) != 0>(S, li, P, L, dist, occ, cnt, PF, ce, cn);
-#endif
+            shadow_opaque_lb<((WAVE) & 2) != 0>(S, li, P, L, dist, occ, cnt);
             RT_MARK(cnt, 7);
             if (gate) {
                 Color F{0.0f, 0.0f, 0.0f};
@@ -987,9 +817,6 @@ __device__ __forceinline__ Color shade_local(const SceneDev& S, const Mat& m, co
         WaveCone wc[kLightBatch];
         float dmax[kLightBatch];
         unsigned tmask = (1u << nl) - 1u;  // lights whose triangles the wave must walk
-#ifdef RT_ABLATE_SHADOW_TRI  // timing-only build: no triangle shadow tests
-        tmask = 0;
-#endif
         if (use_wave) {
 #pragma unroll
             for (int j = 0; j < kLightBatch; ++j) {
@@ -1007,11 +834,9 @@ __device__ __forceinline__ Color shade_local(const SceneDev& S, const Mat& m, co
                 }
             }
         }
-#ifndef RT_ABLATE_SHADOW  // timing-only build: no shadow rays
         RT_MARK(cnt, 3);
         if (use_wave) shadow_opaque_wave<kLightBatch, (WAVE & 3) == 2>(S, lb, nl, tmask, P, L, dist, occ, wc, dmax, cnt);
         else shadow_opaque_batch<kLightBatch>(S, lb, nl, P, L, dist, occ, cnt);
-#endif
         RT_MARK(cnt, 4);
 #pragma unroll
         for (int j = 0; j < kLightBatch; ++j) {

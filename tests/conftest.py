@@ -154,3 +154,56 @@ def ulp_diff(a: np.ndarray, b: np.ndarray) -> int:
     if a.size == 0:
         return 0
     return int(np.abs(key(a) - key(b)).max())
+
+
+# ---- moved cameras and big bounce frames pinned to oracle/_ref
+# (tests/golden/make_camera_golden.py, cameras.json): per frame the SHA-256
+# of its camera words and of the reference's float32 RGB / RGBA8 frame.
+def _sha(a: np.ndarray) -> str:
+    import hashlib
+
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+_CAM_GOLDEN = None
+
+
+def cam_golden() -> dict:
+    global _CAM_GOLDEN
+    if _CAM_GOLDEN is None:
+        with open(os.path.join(GOLDEN, "cameras.json")) as f:
+            _CAM_GOLDEN = json.load(f)
+    return _CAM_GOLDEN
+
+
+def cam_scene_path(which: str, hf_path: str) -> str:
+    return hf_path if which == "hf" else scene(int(which[-1]))
+
+
+class CamRef:
+    """The reference frames of one fixture set of tests/cameras.py: its Scene,
+    its frames of each kind, and the check of an image against _ref."""
+
+    def __init__(self, which: str, hf_path: str):
+        import cameras
+        import rt_amd
+
+        self.which = which
+        _, name, self.w, self.h, self.depth = next(s for s in cameras.SETS if s[0] == which)
+        self.path = cam_scene_path(which, hf_path)
+        self.scene = rt_amd.Scene(self.path, self.w, self.h, self.depth)
+        self.frames = {kind: fn(self.scene.frame) for kind, fn in cameras.KINDS.items()}
+        for kind, frames in self.frames.items():  # the generator's camera words
+            for i, f in enumerate(frames):
+                assert cam_golden()[cameras.key(which, kind, i)]["camera_words_sha256"] == cameras.words_sha(f)
+
+    def entry(self, kind: str, i: int) -> dict:
+        import cameras
+
+        return cam_golden()[cameras.key(self.which, kind, i)]
+
+    def matches(self, img: np.ndarray, kind: str, i: int) -> bool:
+        """float32 RGB (rows, W, 3) or RGBA8 (rows, W, 4) against the reference frame."""
+        e = self.entry(kind, i)
+        want = e["rgba8_sha256"] if img.dtype == np.uint8 else e["rgb_f32_sha256"]
+        return _sha(img) == want

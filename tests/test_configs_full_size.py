@@ -70,3 +70,20 @@ def test_c4_scene2_hip_reference_digest(config_golden):
     q = _render(ctx, scene(2), 3840, 2160, 5, as_float=False)
     assert _sha(q) == config_golden["scene2_3840x2160_d5_rgba8_sha256"]
     ctx.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("which", ["scene7", "scene9"])
+def test_c4_bounce_scenes_full_frame_reference_digest(which):
+    """C4's reflect / refract stress scenes at 3840x2160,
+    depth 5, whole frame: float32 RGB and RGBA8 digests of oracle/_ref's
+    frame (tests/golden/make_camera_golden.py)."""
+    from conftest import cam_golden
+
+    e = cam_golden()[f"{which}_3840x2160_d5_full"]
+    ctx = rt_amd.Context(0)
+    got = _render(ctx, scene(int(which[-1])), 3840, 2160, 5)
+    assert _sha(got) == e["rgb_f32_sha256"], abs(float(got.astype(np.float64).sum()) - e["rgb_sum"])
+    q = _render(ctx, scene(int(which[-1])), 3840, 2160, 5, as_float=False)
+    assert _sha(q) == e["rgba8_sha256"]
+    ctx.close()

@@ -7,18 +7,18 @@ stream, async renders on the caller's: every write of that state must come
 after every render already enqueued that may read it, and every render after
 the write it needs — with no host sync by the caller.  Each test interleaves
 cameras and streams without a single synchronize between calls and compares
-every output, bit for bit, with a cold context that renders each camera
-alone (the reference's bits are pinned for those by test_gpu_parity.py)."""
+every output, bit for bit, with the reference's frame of its camera
+(oracle/_ref with the frame's explicit camera words, tests/golden/cameras.json:
+the moved cameras of tests/cameras.py at 480 x 270)."""
 from __future__ import annotations
 
 import contextlib
 import gc
 
-import numpy as np
 import pytest
 
 import rt_amd
-from conftest import bits_equal, scene
+from conftest import CamRef, scene
 
 pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
@@ -48,28 +48,15 @@ def _cameras(s, moves):
     return out
 
 
-def _cold(path, w, h, frames):
-    """Each camera rendered by a fresh context (no state carried over)."""
-    s = rt_amd.Scene(path, w, h, 0)
-    want = []
-    for f in frames:
-        c = rt_amd.Context(0)
-        c.upload(s)
-        want.append(c.render_float(f))
-        c.close()
-    return want
-
-
-@pytest.mark.parametrize("which", ["scene2", "heightfield"])
+@pytest.mark.parametrize("which", ["scene2", "hf"])
 def test_async_sync_interleaved_without_host_sync(which, heightfield_path):
     """async(A) on s1, sync(B), async(B) on s1, async(A) on s2, ... in a loop,
-    never synchronising: every image equals the cold context's."""
-    path, w, h = (scene(2), 1920, 1080) if which == "scene2" else (heightfield_path, 960, 540)
-    s = rt_amd.Scene(path, w, h, 0)
-    cams = _cameras(s, [(0.0, 0.0), (9.5, -4.0), (-14.25, 6.5)])
-    want = _cold(path, w, h, cams)
+    never synchronising: every image is the reference's."""
+    r = CamRef(which, heightfield_path)
+    w, h = r.w, r.h
+    cams = r.frames["cams"][:3]
     ctx = rt_amd.Context(0)
-    ctx.upload(s)
+    ctx.upload(r.scene)
     s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
     torch.cuda.synchronize()
     outs, host = [], []
@@ -90,20 +77,19 @@ def test_async_sync_interleaved_without_host_sync(which, heightfield_path):
     ctx.sync()
     torch.cuda.synchronize()
     for i, (cam, o) in enumerate(outs):
-        assert bits_equal(o.cpu().numpy(), want[cam]), f"async render {i} (camera {cam})"
+        assert r.matches(o.cpu().numpy(), "cams", cam), f"async render {i} (camera {cam})"
     for i, (cam, img) in enumerate(host):
-        assert bits_equal(img, want[cam]), f"sync render {i} (camera {cam})"
+        assert r.matches(img, "cams", cam), f"sync render {i} (camera {cam})"
 
 
-def test_async_prepass_seen_by_other_stream():
+def test_async_prepass_seen_by_other_stream(heightfield_path):
     """A camera first met by an async render is prepared on that stream; a
     render of the same camera on another stream right after must wait for it."""
-    w, h = 640, 480
-    s = rt_amd.Scene(scene(2), w, h, 0)
-    cams = _cameras(s, [(3.0, 1.0), (-6.0, 2.0)])
-    want = _cold(scene(2), w, h, cams)
+    r = CamRef("scene2", heightfield_path)
+    w, h = r.w, r.h
+    cams = r.frames["cams"][1:3]
     ctx = rt_amd.Context(0)
-    ctx.upload(s)
+    ctx.upload(r.scene)
     s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
     torch.cuda.synchronize()
     outs = []
@@ -116,20 +102,19 @@ def test_async_prepass_seen_by_other_stream():
                 outs.append((cam, o))
     ctx.sync()
     for i, (cam, o) in enumerate(outs):
-        assert bits_equal(o.cpu().numpy(), want[cam]), i
+        assert r.matches(o.cpu().numpy(), "cams", cam + 1), i
 
 
-def test_prepare_camera_makes_async_fast():
+def test_prepare_camera_makes_async_fast(heightfield_path):
     """rt_prepare_camera builds the camera buffer without rendering; the
     async render after it uses it (and renders the reference's bits)."""
     import ctypes
 
-    w, h = 320, 240
-    s = rt_amd.Scene(scene(2), w, h, 0)
-    f = _cameras(s, [(2.5, 0.0)])[0]
-    want = _cold(scene(2), w, h, [f])[0]
+    r = CamRef("scene2", heightfield_path)
+    w, h = r.w, r.h
+    f = r.frames["cams"][1]
     ctx = rt_amd.Context(0)
-    ctx.upload(s)
+    ctx.upload(r.scene)
     ctx.prepare_camera(f)
     L = rt_amd.lib()
     L.rt_debug_cb_info.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
@@ -139,22 +124,21 @@ def test_prepare_camera_makes_async_fast():
     o = torch.empty((h, w, 3), dtype=torch.float32, device="cuda")
     ctx.render_async(f, 0, o.data_ptr(), torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
-    assert bits_equal(o.cpu().numpy(), want)
+    assert r.matches(o.cpu().numpy(), "cams", 1)
 
 
 # the refused capture leaves its graph empty, which torch warns about
 @pytest.mark.filterwarnings("ignore:The CUDA Graph is empty")
-def test_graph_capture_and_replay():
+def test_graph_capture_and_replay(heightfield_path):
     """rt_render_async captured in a hipGraph (torch.cuda.CUDAGraph) replays
     the reference's image; capture of an unprepared camera is RT_E_STATE;
     a replay after other cameras were rendered and the captured one was
     prepared again is still exact (captured buffers are never freed)."""
-    w, h = 480, 320
-    s = rt_amd.Scene(scene(2), w, h, 0)
-    cams = _cameras(s, [(0.0, 0.0), (11.0, -3.0), (-20.0, 9.0)])
-    want = _cold(scene(2), w, h, cams)
+    r = CamRef("scene2", heightfield_path)
+    w, h = r.w, r.h
+    cams = r.frames["cams"][:3]
     ctx = rt_amd.Context(0)
-    ctx.upload(s)
+    ctx.upload(r.scene)
     out = torch.zeros((h, w, 3), dtype=torch.float32, device="cuda")
     ctx.render_float(cams[0])  # prepares camera 0
     torch.cuda.synchronize()
@@ -165,7 +149,7 @@ def test_graph_capture_and_replay():
         out.zero_()
         g.replay()
         torch.cuda.synchronize()
-        assert bits_equal(out.cpu().numpy(), want[0])
+        assert r.matches(out.cpu().numpy(), "cams", 0)
     # an unprepared camera cannot be captured
     g2 = torch.cuda.CUDAGraph()
     with capture(g2):
@@ -175,12 +159,12 @@ def test_graph_capture_and_replay():
     # bigger frames of other cameras (buffers grow), then camera 0 again
     big = rt_amd.Scene(scene(2), 1280, 960, 0)
     ctx.render_float(_cameras(big, [(11.0, -3.0)])[0])
-    assert bits_equal(ctx.render_float(cams[2]), want[2])
+    assert r.matches(ctx.render_float(cams[2]), "cams", 2)
     ctx.prepare_camera(cams[0])
     out.zero_()
     g.replay()
     torch.cuda.synchronize()
-    assert bits_equal(out.cpu().numpy(), want[0])
+    assert r.matches(out.cpu().numpy(), "cams", 0)
 
 
 def test_options_round_trip_and_validation():
@@ -202,47 +186,41 @@ def test_options_round_trip_and_validation():
     ctx.set_far_ladder(None)
 
 
-@pytest.mark.parametrize("which,w,h,depth", [("scene2", 320, 240, 0), ("heightfield", 480, 320, 1),
-                                             ("scene7", 200, 150, 3), ("scene9", 160, 120, 5)])
-def test_sequence_matches_cold_renders(which, w, h, depth, heightfield_path):
+@pytest.mark.parametrize("which", ["scene2", "hf", "scene7", "scene9"])
+@pytest.mark.parametrize("kind", ["path", "cams"])
+def test_sequence_matches_reference(which, kind, heightfield_path):
     """rt_render_sequence_async over a camera path (yaw + translation per
-    frame): every frame equals a fresh context's synchronous render."""
-    path = heightfield_path if which == "heightfield" else scene(int(which[-1]))
-    s = rt_amd.Scene(path, w, h, depth)
-    frames = rt_amd.camera_path(s.frame, 5, yaw_deg=1.5, step=(2.0, 0.5, -1.0))
-    cold = rt_amd.Context(0)
-    cold.upload(s)
-    want = [cold.render_float(f) for f in frames]
+    frame) or the turned / moved / widened cameras: every frame is the
+    reference's (scene7 at depth 3, scene9 at depth 5: the bounce kernels)."""
+    r = CamRef(which, heightfield_path)
+    w, h = r.w, r.h
+    frames = r.frames[kind]
     ctx = rt_amd.Context(0)
-    ctx.upload(s)
+    ctx.upload(r.scene)
     out = torch.zeros((len(frames), h, w, 3), dtype=torch.float32, device="cuda")
     ctx.render_sequence_async(frames, 0, 0, out.data_ptr(), h * w * 12, torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
-    for i, f in enumerate(want):
-        assert bits_equal(out[i].cpu().numpy(), f), i
+    for i in range(len(frames)):
+        assert r.matches(out[i].cpu().numpy(), kind, i), i
     # the camera of the last frame is not left "current" by a sequence: a
     # synchronous render of it afterwards prepares it and is exact too
-    assert bits_equal(ctx.render_float(frames[-1]), want[-1])
+    assert r.matches(ctx.render_float(frames[-1]), kind, len(frames) - 1)
 
 
-def test_sequences_on_two_streams_share_the_slots_safely():
-    """Sequences of 7 frames (more than the 4 camera slots and internal
+def test_sequences_on_two_streams_share_the_slots_safely(heightfield_path):
+    """Sequences of 6 frames (more than the 4 camera slots and internal
     streams a sequence keeps in flight) on two caller streams, back to back
-    with no host sync: the second waits for the first's slots; every frame
-    equals a fresh context's render."""
-    w, h = 256, 192
-    s = rt_amd.Scene(scene(2), w, h, 0)
-    a = rt_amd.camera_path(s.frame, 7, yaw_deg=2.0, step=(1.5, 0.0, -2.0))
-    b = rt_amd.camera_path(s.frame, 7, yaw_deg=-2.5, step=(-3.0, 0.5, 1.0))
-    cold = rt_amd.Context(0)
-    cold.upload(s)
-    want_a = [cold.render(f) for f in a]
-    want_b = [cold.render(f) for f in b]
+    with no host sync: the second waits for the first's slots; every RGBA8
+    frame is the reference's."""
+    r = CamRef("scene2", heightfield_path)
+    w, h = r.w, r.h
+    a, b = r.frames["path"], r.frames["cams"]
+    n = len(a)
+    oa = torch.zeros((n, h, w, 4), dtype=torch.uint8, device="cuda")
+    ob = torch.zeros((len(b), h, w, 4), dtype=torch.uint8, device="cuda")
+    oc = torch.zeros((n, h, w, 4), dtype=torch.uint8, device="cuda")
     ctx = rt_amd.Context(0)
-    ctx.upload(s)
-    oa = torch.zeros((7, h, w, 4), dtype=torch.uint8, device="cuda")
-    ob = torch.zeros((7, h, w, 4), dtype=torch.uint8, device="cuda")
-    oc = torch.zeros((7, h, w, 4), dtype=torch.uint8, device="cuda")
+    ctx.upload(r.scene)
     s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
     torch.cuda.synchronize()
     for rep in range(3):
@@ -250,26 +228,23 @@ def test_sequences_on_two_streams_share_the_slots_safely():
         ctx.render_sequence_async(b, ob.data_ptr(), h * w * 4, 0, 0, s2.cuda_stream)
         ctx.render_sequence_async(a[::-1], oc.data_ptr(), h * w * 4, 0, 0, s1.cuda_stream)
         torch.cuda.synchronize()
-        for i in range(7):
-            assert np.array_equal(oa[i].cpu().numpy(), want_a[i]), (rep, "a", i)
-            assert np.array_equal(ob[i].cpu().numpy(), want_b[i]), (rep, "b", i)
-            assert np.array_equal(oc[i].cpu().numpy(), want_a[6 - i]), (rep, "c", i)
+        for i in range(n):
+            assert r.matches(oa[i].cpu().numpy(), "path", i), (rep, "a", i)
+            assert r.matches(oc[i].cpu().numpy(), "path", n - 1 - i), (rep, "c", i)
+        for i in range(len(b)):
+            assert r.matches(ob[i].cpu().numpy(), "cams", i), (rep, "b", i)
         oa.zero_(), ob.zero_(), oc.zero_()
 
 
-def test_sequence_graph_replay_is_self_contained():
+def test_sequence_graph_replay_is_self_contained(heightfield_path):
     """A camera path captured into a hipGraph replays the reference's frames
     even after other cameras and sequences were rendered on the context."""
-    w, h = 320, 240
-    s = rt_amd.Scene(scene(2), w, h, 0)
-    frames = rt_amd.camera_path(s.frame, 6, yaw_deg=2.0, step=(1.5, 0.0, -2.0))
-    other = rt_amd.camera_path(s.frame, 3, yaw_deg=-3.0, step=(-4.0, 1.0, 3.0))
-    cold = rt_amd.Context(0)
-    cold.upload(s)
-    want = [cold.render(f) for f in frames]
-    want_other = [cold.render(f) for f in other]
+    r = CamRef("scene2", heightfield_path)
+    w, h = r.w, r.h
+    frames = r.frames["path"]
+    other = r.frames["cams"][1:4]
     ctx = rt_amd.Context(0)
-    ctx.upload(s)
+    ctx.upload(r.scene)
     out = torch.zeros((len(frames), h, w, 4), dtype=torch.uint8, device="cuda")
     tmp = torch.zeros((len(other), h, w, 4), dtype=torch.uint8, device="cuda")
     torch.cuda.synchronize()
@@ -283,26 +258,25 @@ def test_sequence_graph_replay_is_self_contained():
         ctx.render_async(other[rep], tmp[rep].data_ptr(), 0, torch.cuda.current_stream().cuda_stream)
         ctx.render_sequence_async(other, tmp.data_ptr(), h * w * 4, 0, 0, torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()
-        for i, f in enumerate(want):
-            assert np.array_equal(out[i].cpu().numpy(), f), (rep, i)
-        for i, f in enumerate(want_other):
-            assert np.array_equal(tmp[i].cpu().numpy(), f), (rep, i)
-        assert np.array_equal(ctx.render(other[rep]), want_other[rep])
+        for i in range(len(frames)):
+            assert r.matches(out[i].cpu().numpy(), "path", i), (rep, i)
+        for i in range(len(other)):
+            assert r.matches(tmp[i].cpu().numpy(), "cams", i + 1), (rep, i)
+        assert r.matches(ctx.render(other[rep]), "cams", rep + 1)
 
 
 # the refused capture leaves its graph empty, which torch warns about
 @pytest.mark.filterwarnings("ignore:The CUDA Graph is empty")
-def test_capture_after_async_prepass_on_another_stream():
+def test_capture_after_async_prepass_on_another_stream(heightfield_path):
     """A camera first prepared by an async render on stream s1 (its state
     write pending there) cannot be captured on another stream — that would
     need a wait on an event outside the capture — until rt_sync; then it can,
     and the replay is exact."""
-    w, h = 320, 240
-    s = rt_amd.Scene(scene(2), w, h, 0)
-    f = _cameras(s, [(5.0, -2.0)])[0]
-    want = _cold(scene(2), w, h, [f])[0]
+    r = CamRef("scene2", heightfield_path)
+    w, h = r.w, r.h
+    f = r.frames["cams"][2]
     ctx = rt_amd.Context(0)
-    ctx.upload(s)
+    ctx.upload(r.scene)
     s1 = torch.cuda.Stream()
     out = torch.zeros((h, w, 3), dtype=torch.float32, device="cuda")
     ctx.render_async(f, 0, out.data_ptr(), s1.cuda_stream)  # prepass on s1
@@ -319,4 +293,4 @@ def test_capture_after_async_prepass_on_another_stream():
     out.zero_()
     g2.replay()
     torch.cuda.synchronize()
-    assert bits_equal(out.cpu().numpy(), want)
+    assert r.matches(out.cpu().numpy(), "cams", 2)

@@ -25,7 +25,6 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c3", choices=sorted(bench.CONFIGS))
     ap.add_argument("--frames", type=int, default=20)
-    ap.add_argument("--ring", type=int, default=1, help="RT_OPT_ASYNC_RING")
     ap.add_argument("--cb", type=int, default=1, help="RT_OPT_CAMERA_BUFFER")
     args = ap.parse_args()
     import torch
@@ -34,7 +33,7 @@ def main():
 
     name, W, H, depth = bench.CONFIGS[args.config]
     scene = rt_amd.Scene(bench.scene_path(name), W, H, depth)
-    ctx = rt_amd.Context(0, async_ring=args.ring, camera_buffer=args.cb)
+    ctx = rt_amd.Context(0, camera_buffer=args.cb)
     ctx.upload(scene)
     dev = torch.empty((H, W, 4), dtype=torch.uint8, device="cuda")
     stream = torch.cuda.current_stream().cuda_stream
@@ -49,7 +48,7 @@ def main():
             out.append(f)
         return out
 
-    res = {"config": args.config, "ring": args.ring, "cb": args.cb}
+    res = {"config": args.config, "cb": args.cb}
     fr = cams(0.37, -0.21)
     ctx.render_async(scene.frame, dev.data_ptr(), 0, stream)
     torch.cuda.synchronize()

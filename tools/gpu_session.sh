@@ -51,7 +51,7 @@ for s in $STEPS; do
     fastmath) run fastmath_check 600 tools/fastmath_check ;;
     camprobe)
       for c in ${CONFIGS:-c2 c3}; do
-        for r in 1 0; do run camprobe_${c}_ring$r 300 python tools/camera_probe.py --config $c --ring $r; done
+        run camprobe_${c} 300 python tools/camera_probe.py --config $c
         run camprobe_${c}_nocb 300 python tools/camera_probe.py --config $c --cb 0
       done ;;
     camprof)
