@@ -49,8 +49,23 @@ def test_every_export_is_declared():
     assert dbg_plain <= exported, dbg_plain - exported
 
 
+def test_gather_library_exports_its_header():
+    """librt_gather.so (the frame's RCCL gather, include/rt_gather.h) exports
+    exactly the functions its header declares, and links RCCL."""
+    hdr = re.sub(r"/\*.*?\*/", "", open(os.path.join(REPO, "include", "rt_gather.h")).read(), flags=re.S)
+    declared = set(re.findall(r"\b(rt_gather_[a-z_0-9]*)\s*\(", hdr))
+    lib = os.path.join(REPO, "ray-tracing-gpu_amd", "lib", "librt_gather.so")
+    out = subprocess.run(["nm", "-D", "--defined-only", lib], capture_output=True, text=True).stdout
+    exported = set(re.findall(r"\bT (rt_[a-z_0-9]+)\b", out))
+    assert exported == declared, (exported ^ declared)
+    deps = subprocess.run(["objdump", "-p", lib], capture_output=True, text=True).stdout
+    assert "librccl.so" in deps
+    # the renderer itself never links RCCL (PyTorch brings its own)
+    assert "librccl" not in subprocess.run(["objdump", "-p", rt_amd.LIB_PATH], capture_output=True, text=True).stdout
+
+
 def test_abi_version():
-    assert rt_amd.lib().rt_abi_version() == 5
+    assert rt_amd.lib().rt_abi_version() == 6
 
 
 def test_struct_layouts_match_header():

@@ -47,6 +47,36 @@ def test_scene2_1080p_matches_reference_digest(tmp_path, digests, extra):
     assert hashlib.sha256(tex.tobytes()).hexdigest() == digests["scene2_1920x1080_d0_rgba8_sha256"]
 
 
+@pytest.mark.parametrize("extra", [["-g", "1", "--gather", "rccl"], ["-g", "1", "--gather", "rccl", "-n", "3"]])
+def test_rccl_gather_matches_reference_digest(tmp_path, digests, extra):
+    """rt_render's native RCCL path (librt_gather.so): the rank renders into
+    device memory and ONE RCCL group (ncclSend / ncclRecv, here the root to
+    itself) gathers the slab into the root GPU's frame; the PPM is the
+    reference's frame bit for bit.  On the 8-GPU node -g 8 takes this path
+    by default (one rank per GPU, each peer on its own xGMI link)."""
+    out = tmp_path / "scene2.ppm"
+    r = subprocess.run([EXE, scene(2), "-x", "1920", "-y", "1080", "-o", str(out)] + extra, capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert "[ETAT]: gather: RCCL" in r.stdout and "send/recv pair(s)" in r.stdout, r.stdout
+    tex = as_texture(read_ppm(out))
+    assert hashlib.sha256(tex.tobytes()).hexdigest() == digests["scene2_1920x1080_d0_rgba8_sha256"]
+
+
+def test_rccl_gather_refuses_shared_gpus():
+    """RCCL needs one rank per GPU: more contexts than GPUs with --gather rccl
+    is an argument error; without it they share GPUs and assemble on the host."""
+    import torch
+
+    n = torch.cuda.device_count() + 1
+    r = subprocess.run([EXE, scene(2), "-x", "64", "-y", "32", "-g", str(n), "--gather", "rccl"], capture_output=True,
+                       text=True, timeout=60)
+    assert r.returncode == 1 and "--gather rccl needs one GPU per context" in r.stderr
+    r = subprocess.run([EXE, scene(2), "-x", "64", "-y", "32", "-g", str(n)], capture_output=True, text=True,
+                       timeout=60)
+    assert r.returncode == 0 and "gather: host" in r.stdout, r.stderr
+
+
 def test_bounce_scene_matches_oracle(tmp_path, oracle):
     out = tmp_path / "scene7.ppm"
     r = subprocess.run([EXE, scene(7), "-x", "96", "-y", "64", "-d", "3", "-s", "-o", str(out)], capture_output=True,
