@@ -26,7 +26,9 @@ int rt_debug_lb_info(rt_ctx*, double* out, int n);
  * out[2] device ms of the last synchronous build's kernels, out[3] tiles, out[4] inline
  * records (0/1), out[5] host wall ms of the build's enqueue; out[6..9]
  * binning counters: candidate (triangle, tile) pairs tested, lists longer
- * than 256, the longest of them, the entry capacity. */
+ * than 256, the longest of them, the entry capacity; out[10] 1 when the
+ * candidate pairs passed 2^32 - 1 (no pair tested, every tile flagged to the
+ * per-wave path). */
 int rt_debug_cb_info(rt_ctx*, double* out, int n);
 
 /* The current camera buffer checked against brute force (every tile with

@@ -47,7 +47,8 @@ __device__ __forceinline__ bool cb_tile_row_needed(const FrameDev& F, int ty)
 // Per-build device state (one per camera buffer: the context's, and one per
 // sequence slot).  stat words: [1] candidate pairs, [3] lists longer than RT_CB_SORT (their tiles in
 // lng[]), [4] the longest of them, [5] lists of 33..RT_CB_SORT entries
-// (their tiles in mid[]).
+// (their tiles in mid[]), [6] 1: more than 2^32 - 1 candidate pairs (every
+// tile flagged: the per-wave path).
 struct CbDev {
     float4* __restrict__ tcone;   // 2 per tile: [w cosW] [sinW chord 0 0]
     unsigned* __restrict__ off;   // nt + 1: counts, scanned in place into offsets
@@ -123,7 +124,7 @@ __device__ __forceinline__ void cb_tiles_block(const FrameDev& F, const CbDev& B
 struct CbBox {
     int tx0, ty0, nx, ny;
 };
-__device__ __forceinline__ bool cb_span(double cx, double cz, double rho, double& lo, double& hi)
+__host__ __device__ inline bool cb_span(double cx, double cz, double rho, double& lo, double& hi)
 {
     const double d2 = cx * cx + cz * cz;
     if (!(d2 > rho * rho * (1.0 + 1e-9) + 1e-18)) return false;
@@ -139,7 +140,7 @@ __device__ __forceinline__ bool cb_span(double cx, double cz, double rho, double
 }
 // tile range [t0, t1] of the pixels whose slope (X or Y) lies in [lo, hi]
 // (the inverse of X = (2 px inv - 1) half, 2 pixels of slack each side).
-__device__ __forceinline__ void cb_tiles_of(double lo, double hi, float half, float inv, int npx, int ntiles,
+__host__ __device__ inline void cb_tiles_of(double lo, double hi, float half, float inv, int npx, int ntiles,
                                             int& t0, int& t1)
 {
     const double s = 1.0 / (2.0 * (double)inv);
@@ -152,10 +153,11 @@ __device__ __forceinline__ void cb_tiles_of(double lo, double hi, float half, fl
         return;
     }
     t0 = (int)(p0 / 8.0);
-    t1 = min(ntiles - 1, (int)(p1 / 8.0));
+    const int t1p = (int)(p1 / 8.0);
+    t1 = ntiles - 1 < t1p ? ntiles - 1 : t1p;
 }
 // Clip the convex polygon (x[i], y[i]), i < n, to a X + b Y >= c.
-__device__ __forceinline__ int cb_clip(double* x, double* y, int n, double a, double b, double c)
+__host__ __device__ inline int cb_clip(double* x, double* y, int n, double a, double b, double c)
 {
     double ox[8], oy[8];
     int m = 0;
@@ -187,7 +189,7 @@ __device__ __forceinline__ int cb_clip(double* x, double* y, int n, double a, do
 // Dm (the film's corner) satisfies d0 . n_c >= c |d0| >= (c < 0 ? c Dm :
 // c): a half-plane of the film.  The box is that of the film rectangle
 // (within the cone's span) clipped by the three half-planes.
-__device__ __forceinline__ CbBox cb_box(const float4 c0, const float4* e, const FrameDev& F, const CbDev& B)
+__host__ __device__ inline CbBox cb_box(const float4 c0, const float4* e, const FrameDev& F, float wbound)
 {
     const double hw = (double)F.half_w * (1.0 + 1e-6) + 1e-9, hh = (double)F.half_h * (1.0 + 1e-6) + 1e-9;
     double xlo = -hw, xhi = hw, ylo = -hh, yhi = hh;
@@ -195,7 +197,7 @@ __device__ __forceinline__ CbBox cb_box(const float4 c0, const float4* e, const 
                             {F.orient[4], F.orient[5], F.orient[6]},
                             {F.orient[8], F.orient[9], F.orient[10]}};
     if (c0.w > 0.0f) {
-        const double X = acos(fmin(1.0, (double)c0.w)) + (double)B.wbound;
+        const double X = acos(fmin(1.0, (double)c0.w)) + (double)wbound;
         const double an = sqrt((double)c0.x * c0.x + (double)c0.y * c0.y + (double)c0.z * c0.z);
         if (X < 1.39 && an > 0.5 && isfinite(an)) {
             const double Th = acos(fmax(-1.0, cos(X) - 4.4e-6)) + 3e-5;  // + the orientation's 2e-5
@@ -227,7 +229,7 @@ __device__ __forceinline__ CbBox cb_box(const float4 c0, const float4* e, const 
         const double nx = (E.x * r[0][0] + E.y * r[0][1] + E.z * r[0][2]) / nn;
         const double ny = (E.x * r[1][0] + E.y * r[1][1] + E.z * r[1][2]) / nn;
         const double nz = (E.x * r[2][0] + E.y * r[2][1] + E.z * r[2][2]) / nn;
-        const double c = (double)E.w - (double)B.wbound - 3.5e-5;
+        const double c = (double)E.w - (double)wbound - 3.5e-5;
         const double k = c < 0.0 ? c * Dm : c;
         n = cb_clip(px, py, n, nx, ny, k + nz);  // nx X + ny Y - nz >= k
     }
@@ -240,8 +242,8 @@ __device__ __forceinline__ CbBox cb_box(const float4 c0, const float4* e, const 
         ay1 = fmax(ay1, py[i]);
     }
     int x0, x1, y0, y1;
-    cb_tiles_of(ax0, ax1, F.half_w, F.inv_w, F.width, B.tiles_x, x0, x1);
-    cb_tiles_of(ay0, ay1, F.half_h, F.inv_h, F.height, B.tiles_y, y0, y1);
+    cb_tiles_of(ax0, ax1, F.half_w, F.inv_w, F.width, (F.width + 7) / 8, x0, x1);
+    cb_tiles_of(ay0, ay1, F.half_h, F.inv_h, F.height, (F.height + 7) / 8, y0, y1);
     if (x1 < x0 || y1 < y0) return CbBox{0, 0, 0, 0};
     return CbBox{x0, y0, x1 - x0 + 1, y1 - y0 + 1};
 }
@@ -326,7 +328,7 @@ __device__ __forceinline__ void cb_boxes_block(const SceneDev& S, const FrameDev
     if (k >= S.n_tri) return;
     const float4* e = S.cone_cam + 2 * (size_t)S.n_tri + 3 * (size_t)k;
     const float4 e3[3] = {e[0], e[1], e[2]};
-    const CbBox b = cb_box(S.cone_cam[2 * k], e3, F, B);
+    const CbBox b = cb_box(S.cone_cam[2 * k], e3, F, B.wbound);
     const unsigned n = (unsigned)(b.nx * b.ny);
     B.box[k] = make_int4(b.tx0, b.ty0, b.nx, (int)n);
     B.tcnt[k] = n;
@@ -399,13 +401,28 @@ __device__ __forceinline__ bool cb_run(const SceneDev& S, const CbDev& B, unsign
 // next slot of its tile (a tile whose list would end past the capacity is
 // flagged instead: the per-wave path).  Only per-tile counters are atomic:
 // no global counter to serialise on.
+// total (count pass): the box-size scan's 64-bit total (the fill pass, after
+// the offsets' scan reused the scratch, reads the count pass's stat[6]).  The
+// pair offsets are 32-bit: a
+// camera with more than 2^32 - 1 candidate pairs (whole-film boxes of many
+// "always test" triangles at a high tile count) would wrap them, so then no
+// pair is tested — every tile is flagged (the per-wave path: the same image)
+// and stat[6] tells the host.
 template <bool FILL>
-__global__ __launch_bounds__(256) void rt_cb_pairs(const SceneDev S, CbDev B)
+__global__ __launch_bounds__(256) void rt_cb_pairs(const SceneDev S, CbDev B, const unsigned long long* __restrict__ total)
 {
     const int lane = (int)(threadIdx.x & 63);
-    const unsigned np = B.tcnt[S.n_tri];  // total candidate pairs (the scan's last word)
     const unsigned nw = gridDim.x * (blockDim.x >> 6);
     const unsigned w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (FILL ? B.stat[6] != 0u : *total > 0xFFFFFFFFull) {
+        if (!FILL) {
+            const unsigned nt = (unsigned)(B.tiles_x * B.tiles_y);
+            for (unsigned t = w * 64 + (unsigned)lane; t < nt; t += nw * 64) B.flag[t] = 1u;
+            if (w == 0 && lane == 0) B.stat[6] = 1u;
+        }
+        return;
+    }
+    const unsigned np = B.tcnt[S.n_tri];  // total candidate pairs (the scan's last word)
     const unsigned nruns = (np + 63) / 64, per = (nruns + nw - 1) / nw;
     const unsigned r0 = w * per, r1 = min(nruns, r0 + per);
     if (r0 >= r1) return;  // wave-uniform

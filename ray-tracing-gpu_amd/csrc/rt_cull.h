@@ -188,7 +188,14 @@ __device__ __forceinline__ void camera_wave_batch(const SceneDev& S, const WaveC
         }
         wave_lds_sync();
         const int n = __popcll(m);
+        unsigned long long mm = m;
         for (int j = 0; j < n; ++j) {
+            // survivor j's dmin (its lane's record): when every lane already
+            // holds a hit nearer than it, none of its hits (t >= dmin > best)
+            // can win or tie — the camera-list walk's exit, as a skip
+            const int lj = (int)__builtin_ctzll(mm);
+            mm &= mm - 1;
+            if (!__any((bi < 0) | !(bt < readlanef(c1.x, lj)))) continue;
             RT_EV(cnt, 2);
             const float4 a = win.a[j], b = win.b[j];
             const float2 c = win.c[j];
@@ -203,8 +210,10 @@ __device__ __forceinline__ void camera_wave_batch(const SceneDev& S, const WaveC
         return;
     }
     while (m) {
-        const int kk = k0 + (int)__builtin_ctzll(m);
+        const int lk = (int)__builtin_ctzll(m);
+        const int kk = k0 + lk;
         m &= m - 1;
+        if (!__any((bi < 0) | !(bt < readlanef(c1.x, lk)))) continue;  // (as above)
         RT_EV(cnt, 2);
         if (S.use_tricam) {
             const float4* r = S.tricam + 4 * kk;
@@ -407,14 +416,104 @@ __device__ __forceinline__ int closest_hit_camera_list(const SceneDev& S, int ti
     return bi;
 }
 
+// Camera records in the launch (tiny scenes, WAVE bit 32).  For a scene of
+// at most kTinyMax triangles the host computes, per camera, every triangle's
+// camera cone and edge records (cone_record, in double), its tricam record
+// (the values Triangle.cpp:139-160 computes for a ray from the camera) and
+// its dmin (no reported hit nearer), sorted nearest first, and passes them BY
+// VALUE with the kernel launches — no camera prepass, no per-camera arrays:
+// the records arrive by scalar loads from the kernel-argument segment.
+// A tile's triangles are a bit mask (rt_tiny_masks, one thread per 8x8
+// tile, a few us): triangle j is kept iff the camera wave test passes for a
+// cone that holds every ray of the tile — axis = the tile's reference ray
+// (lane 36, pixel (8tx + 4, 8ty + 4) clamped), half-angle = wbound, the
+// analytic bound on every tile's spread (the host's tile_wbound).  That is
+// the camera buffer's test with the tile's measured cone replaced by a
+// provably wider one, so the kept set holds every triangle any of the
+// tile's rays can be reported hitting.  Static cameras reuse the masks.
+constexpr int kTinyMax = 20;
+struct TinyCam {
+    int n;       // listed triangles (never-hit ones left out)
+    int masked;  // 1: mask[] holds the tiles' bits (rows aligned to the tile grid); 0: test all
+    int tiles_x, tiles_y;
+    float cosW, sinW, chord, pad;  // the tile cone's width (wbound), as wave_cone would hold it
+    const unsigned* mask;          // per tile of the full frame: bit j = keep triangle j
+    // per triangle, nearest first: [c0 = axis, cosT] [edge 0] [edge 1] [edge 2]
+    // [tricam 0] [1] [2] [3 = tq, file index, dmin, sinT]
+    float4 rec[8 * kTinyMax];
+};
+
+// rt_tiny_masks: one thread per tile of the rows the frame renders.
+__global__ __launch_bounds__(256) void rt_tiny_masks(const FrameDev F, const TinyCam T, unsigned* __restrict__ mask)
+{
+    const int t = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (t >= T.tiles_x * T.tiles_y) return;
+    const int tx = t % T.tiles_x, ty = t / T.tiles_x;
+    const int rb = F.band_rows > 0 ? 0 : F.row_begin, re = F.band_rows > 0 ? F.height : F.row_end;
+    if (ty * 8 >= re || ty * 8 + 8 <= rb) return;  // rows this frame does not render
+    const int px = min(tx * 8 + 4, F.width - 1), py = min(ty * 8 + 4, F.height - 1);
+    WaveCone wc;
+    wc.w = camera_dir(F, px, py);
+    wc.cosW = T.cosW;
+    wc.sinW = T.sinW;
+    wc.chord = T.chord;
+    wc.ok = true;
+    unsigned m = 0;
+    for (int j = 0; j < T.n; ++j) {
+        const float4* r = T.rec + 8 * j;
+        if (cone_overlap(wc, r[0], r[7].w, 0.0f) && edges_open(wc, r + 1, 0.0f)) m |= 1u << j;
+    }
+    mask[t] = m;
+}
+
+// Closest hit for camera rays from the launch's records: planes and quadrics
+// first, then the tile's kept triangles nearest first (tile < 0 or no masks:
+// every listed triangle), leaving once every lane holds a hit nearer than
+// the next dmin (t >= dmin > best: no later triangle can win or tie).
+__device__ __forceinline__ int closest_hit_camera_tiny(const SceneDev& S, const TinyCam& T, int tile, const Vec3 O,
+                                                       const Vec3 D, float& best_t, Counters& cnt)
+{
+    float bt = -1.0f;
+    int bi = -1;
+    for (int k = 0; k < S.n_plane; ++k) {
+        const float4 a = S.plane[2 * k], b = S.plane[2 * k + 1];
+        float t;
+        ++cnt.pla;
+        const bool ok = hit_plane(make_float4(0.f, a.x, a.y, a.z), make_float4(a.w, 0.f, 0.f, 0.f), O, D, t);
+        take_min(ok, t, __float_as_int(b.x), bt, bi);
+    }
+    for (int k = 0; k < S.n_quad; ++k) {
+        const float4* r = S.quad + 3 * k;
+        const float4 a = r[0], b = r[1], c = r[2];
+        float t;
+        ++cnt.qua;
+        const bool ok = hit_quadric(make_float4(0.f, a.x, a.y, a.z), make_float4(a.w, b.x, b.y, b.z),
+                                    make_float4(b.w, c.x, c.y, 0.f), O, D, t);
+        take_min(ok, t, __float_as_int(c.z), bt, bi);
+    }
+    unsigned m = T.n >= 32 ? ~0u : (1u << T.n) - 1u;
+    if (T.masked && tile >= 0) m = T.mask[tile];  // wave-uniform (scalar) load
+    while (m) {
+        const int j = (int)__builtin_ctz(m);
+        m &= m - 1u;
+        const float4* r = T.rec + 8 * j + 4;
+        const float4 d = r[3];
+        if (!__any((bi < 0) | !(bt < d.z))) break;
+        camera_tri(r[0], r[1], r[2], d, D, bt, bi, cnt);
+    }
+    best_t = bt;
+    return bi;
+}
+
 // Primary rays: wave-culled when the whole wave is here, else per lane.
 // WAVE: 0 per lane only, 1 wave-level culling, 2 wave-level two-level
 // (clustered) culling.
 // tile >= 0: the wave is that camera-buffer tile (WAVE bit 8).
 template <int WAVE>
 __device__ __forceinline__ int closest_hit_primary(const SceneDev& S, const Vec3 O, const Vec3 D, float& t,
-                                                   Counters& cnt, int tile = -1)
+                                                   Counters& cnt, int tile = -1, const TinyCam* T = nullptr)
 {
+    if constexpr ((WAVE & 32) != 0) return closest_hit_camera_tiny(S, *T, tile, O, D, t, cnt);
     if ((WAVE & 8) && tile >= 0 && wave_full())
         return closest_hit_camera_list<(WAVE & 2) != 0>(S, tile, O, D, t, cnt);
     if ((WAVE & 3) > 0 && wave_full()) {
@@ -426,7 +525,7 @@ __device__ __forceinline__ int closest_hit_primary(const SceneDev& S, const Vec3
 
 // tricam[k] for camera position C: the camera-ray triangle values that
 // depend only on the origin (written by rt_cone_prepass's camera launch).
-__device__ __forceinline__ void camera_record(const float4* __restrict__ tri, int k, float cx, float cy, float cz,
+__host__ __device__ inline void camera_record(const float4* __restrict__ tri, int k, float cx, float cy, float cz,
                                               float4* __restrict__ tricam)
 {
     const float4 a = tri[3 * k], b = tri[3 * k + 1], c = tri[3 * k + 2];
@@ -481,7 +580,7 @@ __device__ __forceinline__ void camera_record(const float4* __restrict__ tri, in
 // has max d . n_e < lim for some edge reaches no point of the triangle.
 // Distance from point a to the triangle (v0, v1, v2), in double (closest
 // point by the triangle's Voronoi regions).
-__device__ double point_triangle_dist(const double* a, const double (*v)[3])
+__host__ __device__ inline double point_triangle_dist(const double* a, const double (*v)[3])
 {
     double ab[3], ac[3], ap[3], cl[3];
     for (int i = 0; i < 3; ++i) {
@@ -518,7 +617,7 @@ __device__ double point_triangle_dist(const double* a, const double (*v)[3])
     return sqrt(q);
 }
 
-__device__ __forceinline__ void cone_record(const float4* __restrict__ tri, const float4* __restrict__ sph,
+__host__ __device__ inline void cone_record(const float4* __restrict__ tri, const float4* __restrict__ sph,
                                             const float4* __restrict__ nrm, const float4* __restrict__ coef, int n,
                                             float ax, float ay, float az, int camera, float dtarget,
                                             float4* __restrict__ out, float4* __restrict__ tricam, int k)

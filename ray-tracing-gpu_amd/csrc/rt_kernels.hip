@@ -63,13 +63,14 @@ struct Refr {
 };
 
 template <int MAXD, int LB, int WAVE>
-__device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, Counters& cnt, bool live, int tile)
+__device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, Counters& cnt, bool live, int tile,
+                          const TinyCam* T)
 {
     const Color bg{F.bg[0], F.bg[1], F.bg[2]};
     if constexpr (MAXD == 0) {
         float t;
         RT_MARK(cnt, 0);
-        const int idx = closest_hit_primary<(WAVE & 11)>(S, O, D, t, cnt, tile);
+        const int idx = closest_hit_primary<(WAVE & 43)>(S, O, D, t, cnt, tile, T);
         RT_MARK(cnt, 1);
         // Lanes that miss (or lie outside the frame) stay in step through the
         // shading so the wave stays whole for wave-level shadow culling.
@@ -101,7 +102,7 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
         for (;;) {
             if (trace) {
                 float t;
-                const int idx = camera_ray ? closest_hit_primary<(WAVE & 11)>(S, O, D, t, cnt, tile)
+                const int idx = camera_ray ? closest_hit_primary<(WAVE & 43)>(S, O, D, t, cnt, tile, T)
                                            : closest_hit<false>(S, O, D, t, cnt);
                 camera_ray = false;
                 ret = bg;
@@ -204,11 +205,13 @@ constexpr int waves_per_eu(int maxd, int wave)
 {
     return maxd != 0 ? 1 : ((wave & 15) == 14 ? RT_WAVES_PER_EU_BIG : RT_WAVES_PER_EU);
 }
+// One 8 x 8 tile (the body of both trace kernels below).
 // COUNT: also tally the exact tests executed (the RT_FLAG_STATS launch); in
 // the timed kernels the tallies are dead and compile away.
+// T: the launch's camera records (WAVE bit 32, rt_trace_tiny), else nullptr.
 template <int MAXD, int LB, int WAVE, bool COUNT>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(waves_per_eu(MAXD, WAVE)))) void rt_trace_kernel(const SceneDev S, const FrameDev F, unsigned* __restrict__ rgba,
-                                                       float* __restrict__ rgbf, StatsDev* __restrict__ stats)
+__device__ __forceinline__ void trace_tile(const SceneDev& S, const FrameDev& F, unsigned* __restrict__ rgba,
+                                           float* __restrict__ rgbf, StatsDev* __restrict__ stats, const TinyCam* T)
 {
     // One wave per workgroup: one 8 x 8 tile each, so a CU takes a new tile
     // as soon as any wave slot frees instead of four at once (A/B against
@@ -264,14 +267,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(waves_per_eu
         const Vec3 D = camera_dir(F, pxc, pyc);
         const Vec3 O = make3(F.cam[0], F.cam[1], F.cam[2]);
         cnt.primary = valid ? 1u : 0u;
-        // camera-buffer tile: this wave's 8 rows must be one tile row of the
-        // full frame (the buffer's lists hold for its lanes' clamped pixels)
+        // camera-buffer tile (or the launch records' tile): this wave's 8
+        // rows must be one tile row of the full frame (the lists and boxes
+        // hold for its lanes' clamped pixels, a superset of the wave's)
         int tile = -1;
         if ((WAVE & 8) && S.cb_tiles_x > 0 && (py0 & 7) == 0) {
             tile = (py0 >> 3) * S.cb_tiles_x + tile_x;
             if (S.cb_flag[tile]) tile = -1;
         }
-        c = radiance<MAXD, LB, WAVE>(S, F, O, D, cnt, valid, tile);
+        if ((WAVE & 32) && (py0 & 7) == 0) tile = (py0 >> 3) * T->tiles_x + tile_x;
+        c = radiance<MAXD, LB, WAVE>(S, F, O, D, cnt, valid, tile, T);
         if (valid) {
             const size_t o = (size_t)ly * F.width + px;
             if (rgbf) {
@@ -334,6 +339,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(waves_per_eu
                 if (i < nv) atomicAdd(dst[i], v[i]);
         }
     }
+}
+
+template <int MAXD, int LB, int WAVE, bool COUNT>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(waves_per_eu(MAXD, WAVE)))) void rt_trace_kernel(
+    const SceneDev S, const FrameDev F, unsigned* __restrict__ rgba, float* __restrict__ rgbf,
+    StatsDev* __restrict__ stats)
+{
+    trace_tile<MAXD, LB, WAVE, COUNT>(S, F, rgba, rgbf, stats, nullptr);
+}
+
+// Tiny scenes (WAVE bit 32): the camera records come with the launch
+// (TinyCam by value, read from the kernel-argument segment by scalar loads).
+template <int MAXD, int LB, int WAVE, bool COUNT>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(waves_per_eu(MAXD, WAVE)))) void rt_trace_tiny(
+    const SceneDev S, const FrameDev F, const TinyCam T, unsigned* __restrict__ rgba, float* __restrict__ rgbf,
+    StatsDev* __restrict__ stats)
+{
+    trace_tile<MAXD, LB, WAVE, COUNT>(S, F, rgba, rgbf, stats, &T);
 }
 
 // Compiled bounce-stack capacities.  The host picks the smallest one that
@@ -489,6 +512,24 @@ struct rt_ctx {
     double lb_build_ms = 0.0;
     float cam_key[3] = {0.f, 0.f, 0.f};
     bool cam_valid = false;
+    // Tiny scenes (<= kTinyMax triangles, depth 0, light buffer): the camera
+    // records are computed on the host per camera and passed with the launch
+    // (rt_cull.h TinyCam) — host copies of the triangle records for that.
+    std::vector<float4> h_tri, h_sph, h_nrm, h_coef;
+    TinyCam tiny{};
+    float tiny_key[30] = {};
+    bool tiny_valid = false;
+    bool opt_launch_camera = true;  // RT_OPT_LAUNCH_CAMERA
+    struct MaskBuf {
+        hipStream_t stream = nullptr;
+        unsigned* d = nullptr;
+        size_t cap = 0;
+        float key[30] = {};
+        bool valid = false;
+    };
+    std::vector<MaskBuf> tiny_masks;  // per stream
+    std::vector<unsigned*> mask_pool;  // spare mask buffers for hipGraph captures
+    size_t mask_pool_nt = 0;
     bool tricam_all = false;  // tricam holds every triangle for cam_key
     StatsDev* d_stats = nullptr;
     void* d_scratch = nullptr;  // staging for host outputs
@@ -698,6 +739,7 @@ RT_EXPORT int rt_set_option(rt_ctx* c, int32_t opt, double v)
         if (v < 0) return RT_E_ARG;
         c->opt_host_chunk_mb = v;
         return RT_OK;
+    case RT_OPT_LAUNCH_CAMERA: c->opt_launch_camera = v != 0; return RT_OK;
     case RT_OPT_CB_CAPACITY:
         if (v < 0 || v > 4e9 || v != std::floor(v)) return RT_E_ARG;
         if (v != c->opt_cb_capacity) c->cb.valid = false;
@@ -719,6 +761,7 @@ RT_EXPORT int rt_get_option(rt_ctx* c, int32_t opt, double* v)
     case RT_OPT_CB_INLINE_MAX_MB: *v = c->opt_cb_inline_mb; return RT_OK;
     case RT_OPT_HOST_CHUNK_MB: *v = c->opt_host_chunk_mb; return RT_OK;
     case RT_OPT_CB_CAPACITY: *v = c->opt_cb_capacity; return RT_OK;
+    case RT_OPT_LAUNCH_CAMERA: *v = c->opt_launch_camera ? 1 : 0; return RT_OK;
     default: return RT_E_ARG;
     }
 }
@@ -789,6 +832,8 @@ RT_EXPORT void rt_destroy(rt_ctx* c)
     hipFree(c->d_lb_dcap);
     hipFree(c->d_lb_meta);
     hipFree(c->d_uni);
+    for (auto& q : c->tiny_masks) hipFree(q.d);
+    for (unsigned* d : c->mask_pool) hipFree(d);
     cb_free(c->cb);
     for (auto& q : c->seq) {
         hipFree(q.tricam);
@@ -1381,6 +1426,24 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
     sph.resize(std::max<size_t>(sph.size(), 4));
     nrm.resize(std::max<size_t>(nrm.size(), 4));
     coef.resize(std::max<size_t>(coef.size(), 4));
+    c->tiny_valid = false;
+    for (auto& q : c->tiny_masks) q.valid = false;  // the masks of the old scene's triangles
+    if (ntr > 0 && ntr <= (size_t)kTinyMax) {  // the launch-camera path's host records
+        auto f4 = [](const std::vector<float>& v, size_t n) {
+            std::vector<float4> o(n);
+            std::memcpy(o.data(), v.data(), n * sizeof(float4));
+            return o;
+        };
+        c->h_tri = f4(tri, 3 * ntr);
+        c->h_sph = f4(sph, ntr);
+        c->h_nrm = f4(nrm, ntr);
+        c->h_coef = f4(coef, ntr);
+    } else {
+        c->h_tri.clear();
+        c->h_sph.clear();
+        c->h_nrm.clear();
+        c->h_coef.clear();
+    }
     HIP_TRY(c, up((void**)&c->d_trisph, sph.data(), sph.size() * sizeof(float)));
     HIP_TRY(c, up((void**)&c->d_trinrm, nrm.data(), nrm.size() * sizeof(float)));
     HIP_TRY(c, up((void**)&c->d_tricoef, coef.data(), coef.size() * sizeof(float)));
@@ -1601,13 +1664,28 @@ static void trace_dims(kernel_fn k, int width, int rows, dim3& grid, dim3& block
     lds = big ? (unsigned)kLdsWaveBytes : 0u;
 }
 
-// One trace launch over `rows` output rows.
-static int launch_trace(rt_ctx* c, kernel_fn k, SceneDev& S, FrameDev& F, int width, int rows, unsigned* oa,
-                        float* ob, StatsDev* stats, hipStream_t st)
+// The launch-camera kernel (tiny scenes: camera buffer replaced by the
+// launch's records, light-buffer shadows, one light per pass).
+template <bool COUNT>
+static const void* tiny_kernel()
+{
+    return (const void*)&rt_trace_tiny<0, 1, 37, COUNT>;
+}
+
+// One trace launch over `rows` output rows (T: the launch-camera kernel with
+// its records, else kernel k).
+static int launch_trace(rt_ctx* c, kernel_fn k, const TinyCam* T, bool count, SceneDev& S, FrameDev& F, int width,
+                        int rows, unsigned* oa, float* ob, StatsDev* stats, hipStream_t st)
 {
     dim3 grid, block;
     unsigned lds = 0;
     trace_dims(k, width, rows, grid, block, lds);
+    if (T) {
+        TinyCam Tv = *T;
+        void* args[] = {&S, &F, &Tv, &oa, &ob, &stats};
+        HIP_TRY(c, hipLaunchKernel(count ? tiny_kernel<true>() : tiny_kernel<false>(), grid, block, args, 0, st));
+        return RT_OK;
+    }
     void* args[] = {&S, &F, &oa, &ob, &stats};
     HIP_TRY(c, hipLaunchKernel((const void*)k, grid, block, args, lds, st));
     return RT_OK;
@@ -1790,10 +1868,11 @@ static void cb_harvest(rt_ctx::CamBuf& B)
     B.entries = (size_t)B.h_tot[0];
     B.observed = std::max(B.observed, B.entries);
     std::memcpy(B.hstat, B.h_tot + 1, sizeof B.hstat);
-    B.observed_pairs = std::max(B.observed_pairs, (size_t)B.hstat[1]);
+    if (!B.hstat[6]) B.observed_pairs = std::max(B.observed_pairs, (size_t)B.hstat[1]);
     // a build that did not fit (tiles sent down the per-wave path) is
     // rebuilt at its camera's next render, now that the sizes are known
-    if (B.entries > B.built_cap || ((size_t)B.hstat[1] + 63) / 64 > B.built_rcap) B.valid = false;
+    // (a build past 2^32 - 1 candidate pairs stays valid: every tile flagged)
+    if (B.entries > B.built_cap || (!B.hstat[6] && ((size_t)B.hstat[1] + 63) / 64 > B.built_rcap)) B.valid = false;
 }
 
 // Per-tile arrays for nt tiles, the per-build words, the deferred-triangle
@@ -1877,6 +1956,176 @@ static size_t cb_want_cap(const rt_ctx::CamBuf& B, int nt)
     return B.observed + B.observed / 4 + 4096;
 }
 
+// The widest tile cone: lanes lie within 4 pixels of the reference lane in
+// each axis, and on the film plane z = -1 (|d0| >= 1) an angle is at most the
+// distance; wave_cone lowers the cosine by 1e-6 (plus < 5e-7 of rounding).
+// rt_cb_tiles_boxes checks every tile against it (a wider tile gets no list);
+// the launch-camera boxes rely on it analytically, so they are used only
+// while the 4-pixel distance itself stays below the 1-radian cap (*uncapped).
+static float tile_wbound(const rt_frame* f, float& cos_wbound, bool* uncapped = nullptr)
+{
+    const double px = 2.0 * f->half_w * (double)f->inv_w, py = 2.0 * f->half_h * (double)f->inv_h;
+    const double a = std::sqrt(16.0 * px * px + 16.0 * py * py) * 1.001;
+    if (uncapped) *uncapped = a < 1.0;
+    const double amax = std::min(1.0, a);
+    const double wb = std::acos(std::max(-1.0, std::cos(amax) - 2e-6)) + 1e-6;
+    float w = (float)wb;
+    if ((double)w < wb) w = std::nextafter(w, INFINITY);
+    float cw = (float)std::cos((double)w);
+    if ((double)cw < std::cos((double)w)) cw = std::nextafter(cw, INFINITY);
+    cos_wbound = cw;
+    return w;
+}
+
+// ---- camera records in the launch (tiny scenes; rt_cull.h TinyCam)
+// Used for depth-0 frames of scenes of 1..kTinyMax triangles whose shadow
+// rays go through the light buffer (RT_OPT_LAUNCH_CAMERA, on by default):
+// then nothing per camera lives on the device.
+static bool tiny_ok(const rt_ctx* c, int depth, bool lbuf)
+{
+    return c->opt_launch_camera && depth == 0 && lbuf && c->n_tri > 0 && c->n_tri <= kTinyMax &&
+           (int)c->h_tri.size() == 3 * c->n_tri;
+}
+
+// The frame's camera records (rt_cull.h TinyCam): per triangle the camera
+// cone and edge records and the tricam record — the device prepass's own
+// functions, in double / float on the host — sorted by (dmin, triangle);
+// pairs never reported from this camera (cosT 2) are left out.  Tile masks
+// are usable when the orientation is a rotation and the tiles' spread bound
+// holds analytically (tile_wbound); the mask pointer is set by tiny_masks.
+static void tiny_build(const rt_ctx* c, const rt_frame* f, TinyCam& T)
+{
+    const int n = c->n_tri;
+    float4 cone[kTinyMax * kConeRec], tc[kTinyMax * 4];
+    for (int k = 0; k < n; ++k)
+        cone_record(c->h_tri.data(), c->h_sph.data(), c->h_nrm.data(), c->h_coef.data(), n, f->cam_pos[0],
+                    f->cam_pos[1], f->cam_pos[2], 1, 0.0f, cone, tc, k);
+    float cwb = 0.f;
+    bool uncapped = false;
+    const float wb = tile_wbound(f, cwb, &uncapped);
+    int ord[kTinyMax], m = 0;
+    float key[kTinyMax];
+    for (int k = 0; k < n; ++k) {
+        if (cone[2 * k].w > 1.0f) continue;  // never reported from this camera
+        key[k] = cone[2 * k + 1].x == cone[2 * k + 1].x ? cone[2 * k + 1].x : -INFINITY;
+        ord[m++] = k;
+    }
+    std::sort(ord, ord + m, [&](int a, int b) { return key[a] < key[b] || (key[a] == key[b] && a < b); });
+    T = TinyCam{};
+    T.n = m;
+    T.masked = cb_frame_ok(f) && uncapped ? 1 : 0;
+    T.tiles_x = (f->width + 7) / 8;
+    T.tiles_y = (f->height + 7) / 8;
+    // the tile cone of half-angle wbound as wave_cone holds a cone: cos
+    // rounded down, sin and chord (+1e-6 like wave_cone) rounded up
+    const double cw = std::cos((double)wb);
+    float cwf = (float)cw;
+    if ((double)cwf > cw) cwf = std::nextafter(cwf, -INFINITY);
+    const double sw = std::sqrt(std::max(0.0, 1.0 - (double)cwf * cwf)) + 1e-6, ch = std::sqrt(2.0 * (1.0 - cwf)) + 1e-6;
+    float swf = (float)sw, chf = (float)ch;
+    if ((double)swf < sw) swf = std::nextafter(swf, INFINITY);
+    if ((double)chf < ch) chf = std::nextafter(chf, INFINITY);
+    T.cosW = cwf;
+    T.sinW = swf;
+    T.chord = chf;
+    for (int j = 0; j < m; ++j) {
+        const int k = ord[j];
+        float4* r = T.rec + 8 * j;
+        r[0] = cone[2 * k];
+        for (int e = 0; e < 3; ++e) r[1 + e] = cone[2 * n + 3 * k + e];
+        for (int q = 0; q < 4; ++q) r[4 + q] = tc[4 * k + q];
+        r[7].z = key[k];
+        r[7].w = cone[2 * k + 1].w;  // sinT
+    }
+}
+
+// The frame's records, cached per camera (the host's part of a moving frame).
+static const TinyCam& tiny_prepare(rt_ctx* c, const rt_frame* f)
+{
+    float key[30];
+    cb_key_of(f, key);
+    if (!c->tiny_valid || std::memcmp(key, c->tiny_key, sizeof key) != 0) {
+        tiny_build(c, f, c->tiny);
+        std::memcpy(c->tiny_key, key, sizeof key);
+        c->tiny_valid = true;
+    }
+    return c->tiny;
+}
+
+// Tile masks of the launch-camera path, one buffer per stream (launches on
+// one stream run in order, so a stream's masks are rewritten only after its
+// earlier renders read them).  A hipGraph capture cannot allocate: it takes
+// a buffer of its own from a pool kept filled by uncaptured calls (the graph
+// recomputes its masks at every replay; the buffer is retired, freed at the
+// next upload) — or, with the pool empty, renders its launch unmasked (the
+// same image).  *cap_buf: a capture's buffer shared by the frames of one
+// sequence call on one internal stream (nullptr: take one per launch).
+// Sets T.mask; launches rt_tiny_masks when the masks are not the frame's.
+constexpr int kMaskPool = 8;
+static int tiny_masks(rt_ctx* c, const rt_frame* f, hipStream_t st, bool capturing, TinyCam& T,
+                      unsigned** cap_buf = nullptr)
+{
+    if (!T.masked) return RT_OK;
+    const size_t nt = (size_t)T.tiles_x * T.tiles_y;
+    FrameDev F;
+    frame_dev(f, F);
+    const unsigned blocks = (unsigned)((nt + 255) / 256);
+    if (capturing) {
+        unsigned* d = cap_buf ? *cap_buf : nullptr;
+        if (!d) {
+            if (c->mask_pool.empty() || c->mask_pool_nt < nt) {
+                T.masked = 0;  // no buffer to spare inside a capture: every listed triangle
+                return RT_OK;
+            }
+            d = c->mask_pool.back();
+            c->mask_pool.pop_back();
+            c->retired.push_back(d);
+            if (cap_buf) *cap_buf = d;
+        }
+        T.mask = d;
+        hipLaunchKernelGGL(rt_tiny_masks, dim3(blocks), dim3(256), 0, st, F, T, d);
+        HIP_TRY(c, hipGetLastError());
+        return RT_OK;
+    }
+    rt_ctx::MaskBuf* b = nullptr;
+    for (auto& q : c->tiny_masks)
+        if (q.stream == st) b = &q;
+    if (!b) {
+        c->tiny_masks.push_back(rt_ctx::MaskBuf{});
+        b = &c->tiny_masks.back();
+        b->stream = st;
+    }
+    float key[30];
+    cb_key_of(f, key);
+    if (b->cap < nt) {
+        if (b->d) free_later(c, b->d);
+        b->d = nullptr;
+        b->cap = 0;
+        b->valid = false;
+        HIP_TRY(c, hipMalloc((void**)&b->d, nt * sizeof(unsigned)));
+        b->cap = nt;
+    }
+    T.mask = b->d;
+    if (!b->valid || std::memcmp(key, b->key, sizeof key) != 0) {
+        hipLaunchKernelGGL(rt_tiny_masks, dim3(blocks), dim3(256), 0, st, F, T, b->d);
+        HIP_TRY(c, hipGetLastError());
+        std::memcpy(b->key, key, sizeof key);
+        b->valid = true;
+    }
+    // the capture pool, sized for this frame
+    if (c->mask_pool_nt < nt) {
+        for (unsigned* d : c->mask_pool) free_later(c, d);
+        c->mask_pool.clear();
+        c->mask_pool_nt = nt;
+    }
+    while ((int)c->mask_pool.size() < kMaskPool) {
+        unsigned* d = nullptr;
+        HIP_TRY(c, hipMalloc((void**)&d, nt * sizeof(unsigned)));
+        c->mask_pool.push_back(d);
+    }
+    return RT_OK;
+}
+
 static CbDev cb_dev(const rt_ctx::CamBuf& B, const rt_frame* f)
 {
     CbDev d;
@@ -1895,19 +2144,7 @@ static CbDev cb_dev(const rt_ctx::CamBuf& B, const rt_frame* f)
     d.cap = (unsigned)B.cap;
     d.tiles_x = (f->width + 7) / 8;
     d.tiles_y = (f->height + 7) / 8;
-    // the widest tile cone: lanes lie within 4 pixels of the reference lane
-    // in each axis, and on the film plane z = -1 (|d0| >= 1) an angle is at
-    // most the distance; wave_cone lowers the cosine by 1e-6 (plus < 5e-7
-    // of rounding).  rt_cb_tiles_boxes checks every tile against it: a wider tile
-    // gets no list, so the bound is an efficiency matter, not a correctness one.
-    const double px = 2.0 * f->half_w * (double)f->inv_w, py = 2.0 * f->half_h * (double)f->inv_h;
-    const double amax = std::min(1.0, std::sqrt(16.0 * px * px + 16.0 * py * py) * 1.001);
-    const double wb = std::acos(std::max(-1.0, std::cos(amax) - 2e-6)) + 1e-6;
-    d.wbound = (float)wb;
-    if ((double)d.wbound < wb) d.wbound = std::nextafter(d.wbound, INFINITY);
-    float cw = (float)std::cos((double)d.wbound);
-    if ((double)cw < std::cos((double)d.wbound)) cw = std::nextafter(cw, INFINITY);
-    d.cos_wbound = cw;
+    d.wbound = tile_wbound(f, d.cos_wbound);
     return d;
 }
 
@@ -1978,11 +2215,12 @@ static int cb_build(rt_ctx* c, rt_ctx::CamBuf& B, const rt_frame* f, const Scene
     const unsigned nbb = (unsigned)((c->n_tri + 255) / 256);
     hipLaunchKernelGGL(rt_cb_tiles_boxes, dim3(nbb + tb), dim3(256), 0, st, S, F, D, nbb);
     HIP_TRY(c, hipGetLastError());
-    HIP_TRY(c, scan_u32(B.tcnt, (unsigned)c->n_tri, B.tcnt, (unsigned long long*)B.scan, st, nullptr));
+    unsigned long long* ptot = nullptr;  // the candidate pairs' 64-bit total
+    HIP_TRY(c, scan_u32(B.tcnt, (unsigned)c->n_tri, B.tcnt, (unsigned long long*)B.scan, st, &ptot));
     if (exact_first) {  // the pass masks sized to the candidate pairs (one read back)
-        HIP_TRY(c, hipMemcpyAsync(B.h_tot, B.tcnt + c->n_tri, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+        HIP_TRY(c, hipMemcpyAsync(B.h_tot, ptot, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
         HIP_TRY(c, hipStreamSynchronize(st));
-        const size_t pairs = (size_t)*(const unsigned*)B.h_tot;
+        const size_t pairs = (size_t)std::min<unsigned long long>(B.h_tot[0], 0xFFFFFFFFull);
         B.observed_pairs = std::max(B.observed_pairs, pairs);
         const size_t runs = (pairs + 63) / 64 + 1024;
         if (runs > B.rcap) {
@@ -1995,7 +2233,7 @@ static int cb_build(rt_ctx* c, rt_ctx::CamBuf& B, const rt_frame* f, const Scene
         D.rmask = B.rmask;
         D.rcap = (unsigned)std::min<size_t>(B.rcap, 0xFFFFFFF0u);
     }
-    hipLaunchKernelGGL(rt_cb_pairs<false>, dim3(kPairGrid), dim3(256), 0, st, S, D);
+    hipLaunchKernelGGL(rt_cb_pairs<false>, dim3(kPairGrid), dim3(256), 0, st, S, D, (const unsigned long long*)ptot);
     HIP_TRY(c, hipGetLastError());
     HIP_TRY(c, scan_u32(B.off, (unsigned)nt, B.off, (unsigned long long*)B.scan, st, &tot));
     if (exact_first) {  // size the entries to the count (the fill is the only reader of the capacity)
@@ -2007,7 +2245,7 @@ static int cb_build(rt_ctx* c, rt_ctx::CamBuf& B, const rt_frame* f, const Scene
         D.ent = B.ent;
         D.cap = (unsigned)B.cap;
     }
-    hipLaunchKernelGGL(rt_cb_pairs<true>, dim3(kPairGrid), dim3(256), 0, st, S, D);
+    hipLaunchKernelGGL(rt_cb_pairs<true>, dim3(kPairGrid), dim3(256), 0, st, S, D, (const unsigned long long*)nullptr);
     }
     hipLaunchKernelGGL(rt_cb_keys_small, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, st, D, nt);
     hipLaunchKernelGGL(rt_cb_keys_rest, dim3(kMidGrid), dim3(256), 0, st, D, (const unsigned long long*)tot,
@@ -2154,10 +2392,19 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
     const bool lbuf = c->lb_ready && (mode == 1 || (mode == 2 && c->n_tri > kClusterMinTriangles));
     const bool cb_want = depth == 0 && c->n_tri > 0 && c->opt_camera_buffer && cb_frame_ok(f);
     const int rows = frame_rows(f);
-    if (rows > 0) {
+    // tiny scenes: the camera records travel with the launch (no device state)
+    TinyCam Tl;
+    const TinyCam* tiny = nullptr;
+    if (tiny_ok(c, depth, lbuf)) {
+        Tl = tiny_prepare(c, f);
+        if (rows > 0)
+            if (int rc = tiny_masks(c, f, st, capturing, Tl)) return rc;
+        tiny = &Tl;
+    }
+    if (rows > 0 && !tiny) {
         if (int rc = prepare_state(c, f, st, sync_path, capturing, cb_want)) return rc;
     }
-    const bool cbuf = cb_want && cb_matches(c->cb, f);
+    const bool cbuf = !tiny && cb_want && cb_matches(c->cb, f);
     kernel_fn k = (f->flags & RT_FLAG_STATS)
                       ? pick_kernel<true>(depth, c->n_tri, c->n_lights, lbuf, cbuf, cap, lb)
                       : pick_kernel<false>(depth, c->n_tri, c->n_lights, lbuf, cbuf, cap, lb);
@@ -2185,7 +2432,9 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
                         ? (int)std::min(8.0, std::floor((double)out_bytes / chunk))
                         : 1;
     if (nch <= 1) {
-        if (int rc = launch_trace(c, k, S, F, f->width, rows, rgba_dev, rgb_dev, stats, st)) return rc;
+        if (int rc = launch_trace(c, k, tiny, f->flags & RT_FLAG_STATS, S, F, f->width, rows, rgba_dev, rgb_dev, stats,
+                                  st))
+            return rc;
         if (host_out)
             HIP_TRY(c, hipMemcpyAsync(host_out, rgba_dev ? (void*)rgba_dev : (void*)rgb_dev,
                                       (size_t)rows * f->width * px_bytes, hipMemcpyDeviceToHost, st));
@@ -2201,7 +2450,8 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
             Fc.row_end = f->row_begin + r1;
             unsigned* oa = rgba_dev ? rgba_dev + (size_t)r0 * f->width : nullptr;
             float* ob = rgb_dev ? rgb_dev + (size_t)r0 * f->width * 3 : nullptr;
-            if (int rc = launch_trace(c, k, S, Fc, f->width, r1 - r0, oa, ob, stats, st)) return rc;
+            if (int rc = launch_trace(c, k, tiny, f->flags & RT_FLAG_STATS, S, Fc, f->width, r1 - r0, oa, ob, stats, st))
+                return rc;
             HIP_TRY(c, hipEventRecord(c->ev_chunk[n], st));
         }
         if (timed) HIP_TRY(c, hipEventRecord(c->ev1, st));
@@ -2219,7 +2469,7 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
     if (capturing) {
         c->captured = true;
         if (cbuf) c->cb.pinned = true;
-    } else if (!sync_path) {
+    } else if (!sync_path) {  // (uploads and rt_destroy sync every such stream)
         note_async(c, st);
     }
     return RT_OK;
@@ -2368,6 +2618,7 @@ RT_EXPORT int rt_render_sequence_async(rt_ctx* c, const rt_frame* frames, int32_
         HIP_TRY(c, hipEventRecord(c->seq_fork, st));
         for (int j = 0; j < nstreams; ++j) HIP_TRY(c, hipStreamWaitEvent(c->seq_streams[j], c->seq_fork, 0));
     }
+    unsigned* seq_cap[kSeqSlots] = {};  // a capture's mask buffer per internal stream
     for (int i = 0; i < n; ++i) {
         const rt_frame* f = frames + i;
         rt_ctx::CamSlot& q = c->seq[i % kSeqSlots];
@@ -2380,9 +2631,16 @@ RT_EXPORT int rt_render_sequence_async(rt_ctx* c, const rt_frame* frames, int32_
         // into buffers already sized (a first capture renders without it —
         // the same image)
         const int nt = ((f->width + 7) / 8) * ((f->height + 7) / 8);
-        const bool cbuf = depth == 0 && c->n_tri > 0 && c->opt_camera_buffer && cb_frame_ok(f) && cb_async_pays(c, f) &&
+        TinyCam T;
+        const bool tiny = tiny_ok(c, depth, lbuf);
+        if (tiny) {
+            tiny_build(c, f, T);
+            if (int rc = tiny_masks(c, f, fs, capturing, T, &seq_cap[i % kSeqSlots])) return rc;
+        }
+        const bool cbuf = !tiny && depth == 0 && c->n_tri > 0 && c->opt_camera_buffer && cb_frame_ok(f) &&
+                          cb_async_pays(c, f) &&
                           (!capturing || (q.cb.cap > 0 && q.cb.rcap > 0 && q.cb.nt_alloc >= nt && q.cb.big_alloc >= c->n_tri));
-        if (c->n_tri > 0) {
+        if (c->n_tri > 0 && !tiny) {
             if (int rc = camera_records(c, f->cam_pos, fs, cbuf, q.tricam, q.cone_cam, q.uni, q.clu_cam)) return rc;
         }
         int cap = 0, lb = 1;
@@ -2404,12 +2662,8 @@ RT_EXPORT int rt_render_sequence_async(rt_ctx* c, const rt_frame* frames, int32_
         frame_dev(f, F);
         unsigned* rgba = rgba8_dev ? (unsigned*)(rgba8_dev + (size_t)i * rgba8_stride) : nullptr;
         float* rgb = rgb_dev ? (float*)((char*)rgb_dev + (size_t)i * rgb_stride) : nullptr;
-        StatsDev* stats = c->d_stats;
-        void* args[] = {&S, &F, &rgba, &rgb, &stats};
-        dim3 grid, block;
-        unsigned lds = 0;
-        trace_dims(k, f->width, rows, grid, block, lds);
-        HIP_TRY(c, hipLaunchKernel((const void*)k, grid, block, args, lds, fs));
+        if (int rc = launch_trace(c, k, tiny ? &T : nullptr, false, S, F, f->width, rows, rgba, rgb, c->d_stats, fs))
+            return rc;
     }
     // Join: st continues after every frame.
     if (nstreams > 1) {
@@ -2578,6 +2832,7 @@ RT_EXPORT int rt_debug_cb_info(rt_ctx* c, double* out, int n)
     if (n > 7) out[7] = B.hstat[3];
     if (n > 8) out[8] = B.hstat[4];
     if (n > 9) out[9] = (double)B.cap;
+    if (n > 10) out[10] = B.hstat[6];  // 1: candidate pairs past 2^32 - 1 (every tile flagged)
     return RT_OK;
 }
 

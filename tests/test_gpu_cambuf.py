@@ -79,13 +79,14 @@ def test_partial_frame_lists_equal_brute_force(heightfield_path, rows, bands):
     ctx.close()
 
 
-@pytest.mark.parametrize("which", ["scene2", "scene7", "scene9", "hf"])
+@pytest.mark.parametrize("which,lc", [("scene2", 1), ("scene2", 0), ("scene7", 1), ("scene9", 1), ("hf", 1)])
 @pytest.mark.parametrize("kind", ["cams", "path"])
-def test_moved_cameras_equal_reference(heightfield_path, which, kind):
+def test_moved_cameras_equal_reference(heightfield_path, which, lc, kind):
     """Synchronous renders (float32 RGB and RGBA8) of every moved camera of
-    the set, one context for all of them, against _ref's frames."""
+    the set, one context for all of them, against _ref's frames (scene2 with
+    the launch-camera records and with the device camera buffer)."""
     r = CamRef(which, heightfield_path)
-    ctx = rt_amd.Context(0)
+    ctx = rt_amd.Context(0, launch_camera=lc)
     ctx.upload(r.scene)
     for i, f in enumerate(r.frames[kind]):
         assert r.matches(ctx.render_float(f), kind, i), (which, kind, i)
@@ -93,14 +94,16 @@ def test_moved_cameras_equal_reference(heightfield_path, which, kind):
     ctx.close()
 
 
-@pytest.mark.parametrize("which,cbopt", [("scene2", 1), ("scene2", 2), ("hf", 2), ("hf", 1), ("scene7", 1)])
-def test_async_moving_camera_matches_reference(heightfield_path, which, cbopt):
+@pytest.mark.parametrize("which,cbopt,lc", [("scene2", 1, 1), ("scene2", 1, 0), ("scene2", 2, 0), ("hf", 2, 1),
+                                           ("hf", 1, 1), ("scene7", 1, 1), ("scene9", 1, 1)])
+def test_async_moving_camera_matches_reference(heightfield_path, which, cbopt, lc):
     """rt_render_async of a camera path, no host sync between frames: each
-    new camera's state (and, with camera_buffer 2 or where it pays, its camera
-    buffer) is built on the caller's stream; every frame is the reference's."""
+    new camera's records travel with the launch (scene2, lc 1), or its device
+    state (and, with camera_buffer 2 or where it pays, its camera buffer) is
+    built on the caller's stream; every frame is the reference's."""
     r = CamRef(which, heightfield_path)
     frames = r.frames["path"]
-    ctx = rt_amd.Context(0, camera_buffer=cbopt)
+    ctx = rt_amd.Context(0, camera_buffer=cbopt, launch_camera=lc)
     ctx.upload(r.scene)
     st = torch.cuda.current_stream()
     outs = []
@@ -109,7 +112,7 @@ def test_async_moving_camera_matches_reference(heightfield_path, which, cbopt):
         ctx.render_async(f, 0, o.data_ptr(), st.cuda_stream)
         outs.append(o)
     torch.cuda.synchronize()
-    if cbopt == 2 and r.depth == 0:
+    if cbopt == 2 and r.depth == 0 and not (lc and which == "scene2"):
         info = _cb_info(ctx)
         assert info[1] > 0  # the last camera's buffer, built by the async render
         if info[0] == 1.0:
@@ -154,11 +157,11 @@ def test_non_rotation_orientation_renders_without_buffer():
     b.close()
 
 
-@pytest.mark.parametrize("which,cbopt", [("hf", 1), ("hf", 2), ("scene2", 2)])
-def test_sequence_slots_build_camera_buffers(heightfield_path, which, cbopt):
+@pytest.mark.parametrize("which,cbopt,lc", [("hf", 1, 1), ("hf", 2, 1), ("scene2", 2, 0), ("scene2", 1, 1)])
+def test_sequence_slots_build_camera_buffers(heightfield_path, which, cbopt, lc):
     r = CamRef(which, heightfield_path)
     frames = r.frames["path"]
-    ctx = rt_amd.Context(0, camera_buffer=cbopt)
+    ctx = rt_amd.Context(0, camera_buffer=cbopt, launch_camera=lc)
     ctx.upload(r.scene)
     ring = torch.empty((len(frames), r.h, r.w, 3), dtype=torch.float32, device="cuda")
     for rep in range(2):  # the second call reuses the slots' buffers
@@ -236,3 +239,40 @@ def test_sequence_capture_builds_buffers_inside_the_graph(heightfield_path):
         for i in range(len(frames)):
             assert r.matches(out[len(frames) - 1 - i].cpu().numpy(), "path", i), (rep, "uncaptured", i)
     ctx.close()
+
+
+def test_candidate_pairs_past_32_bits(tmp_path):
+    """the pair offsets are 32-bit.  10,000 triangles that are
+    never culled (edges > 110 units: the reference's det can be too inexact at
+    its 0.01 gate, so no cone record) have whole-film boxes; at 7680 x 4320
+    (518,400 tiles) that is 5.2 G candidate pairs > 2^32 - 1.  The build must
+    flag every tile (per-wave path)
+    instead of wrapping the offsets, and a slab of the frame must render
+    like a context without the camera buffer."""
+    import numpy as np
+
+    rng = np.random.default_rng(7)
+    lines = ["background: 10 20 30", "origin: 0 0 400", "eye: 0 0 0", "up: 0 1 0",
+             "Lumiere:", "position: 0 300 300", "intens: 1", "color: 255 255 255"]
+    for k in range(10000):
+        c = rng.uniform(-60, 60, 3)
+        lines += ["Poly:", "color: 200 100 50"]
+        for i, d in enumerate(([-120, -5, -900], [120, -5, -900], [0, 80, -900])):
+            p = c + np.array(d) + rng.uniform(-1, 1, 3)
+            lines.append(f"point: {i} {p[0]:.2f} {p[1]:.2f} {p[2]:.2f}")
+    path = tmp_path / "big_tris.dat"
+    path.write_text("\n".join(lines) + "\n")
+    s = rt_amd.Scene(str(path), 7680, 4320, 0)
+    ctx = rt_amd.Context(0)
+    ctx.upload(s)
+    ctx.prepare_camera(s.frame)
+    info = _cb_info(ctx, 11)
+    assert info[10] == 1.0, info  # past 2^32 - 1: every tile flagged
+    assert _verify(ctx)[2] == 0   # no tile has a list
+    f = s.frame.copy()
+    f.row_begin, f.row_end = 2160, 2168
+    ref = rt_amd.Context(0, camera_buffer=0)
+    ref.upload(s)
+    assert bits_equal(ctx.render_float(f), ref.render_float(f))
+    ctx.close()
+    ref.close()

@@ -239,10 +239,10 @@ def test_camera_buffer_follows_the_camera():
         f = s.frame.copy()
         f.cam_pos[0] += dx
         frames.append(f)
-    ref = rt_amd.Context(0, camera_buffer=0)
+    ref = rt_amd.Context(0, camera_buffer=0, launch_camera=0)
     ref.upload(s)
     want = [ref.render_float(f) for f in frames]
-    c = rt_amd.Context(0)
+    c = rt_amd.Context(0, launch_camera=0)  # the device camera buffer (launch records: no state to go stale)
     c.upload(s)
     out = torch.zeros((120, 160, 3), dtype=torch.float32, device="cuda")
     stream = torch.cuda.current_stream().cuda_stream
@@ -254,6 +254,42 @@ def test_camera_buffer_follows_the_camera():
         c.render_async(f, 0, out.data_ptr(), stream)  # current: used
         torch.cuda.synchronize()
         assert bits_equal(out.cpu().numpy(), w), k
+
+
+@pytest.mark.parametrize("w,h", [(1920, 1080), (333, 197), (8, 8), (1, 1), (640, 17)])
+@pytest.mark.parametrize("i", [1, 2, 3, 4, 5, 6])
+def test_launch_camera_equals_device_camera_state(i, w, h):
+    """Tiny scenes' launch-camera records (RT_OPT_LAUNCH_CAMERA) against the
+    device camera buffer and the per-wave path: the same float32 bits — at
+    the reference camera, slabs off the 8-row grid, bands, a wide-angle film
+    (the boxes' tile bound above one radian: no boxes) and a scaled, non
+    rotation orientation (no boxes)."""
+    s = rt_amd.Scene(scene(i), w, h, 0)
+    a = rt_amd.Context(0)
+    b = rt_amd.Context(0, launch_camera=0)
+    p = rt_amd.Context(0, launch_camera=0, camera_buffer=0)
+    for c in (a, b, p):
+        c.upload(s)
+    frames = [s.frame]
+    if h >= 20:
+        f = s.frame.copy()
+        f.row_begin, f.row_end = 3, h - 5
+        frames.append(f)
+        f = s.frame.copy()
+        f.band_rows, f.band_count, f.band_index = 16, 3, 1
+        frames.append(f)
+    f = s.frame.copy()
+    f.half_w *= 40.0
+    f.half_h *= 40.0
+    frames.append(f)
+    f = s.frame.copy()
+    for q in range(12):
+        f.orient[q] *= 1.25
+    frames.append(f)
+    for k, f in enumerate(frames):
+        want = p.render_float(f)
+        assert bits_equal(a.render_float(f), want), (i, w, h, k)
+        assert bits_equal(b.render_float(f), want), (i, w, h, k)
 
 
 def test_camera_buffer_after_bounce_frame(tmp_path):
@@ -338,7 +374,7 @@ def test_camera_buffer_covers_only_the_ranks_rows(which, heightfield_path):
 
     path = scene(2) if which == "scene2" else heightfield_path
     s = rt_amd.Scene(path, 1920, 1080, 0)
-    c = rt_amd.Context(0)
+    c = rt_amd.Context(0, launch_camera=0)  # scene2's device camera buffer
     c.upload(s)
     L = rt_amd.lib()
     L.rt_debug_cb_info.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]

@@ -48,14 +48,15 @@ def _cameras(s, moves):
     return out
 
 
-@pytest.mark.parametrize("which", ["scene2", "hf"])
-def test_async_sync_interleaved_without_host_sync(which, heightfield_path):
+@pytest.mark.parametrize("which,lc", [("scene2", 1), ("scene2", 0), ("hf", 1)])
+def test_async_sync_interleaved_without_host_sync(which, lc, heightfield_path):
     """async(A) on s1, sync(B), async(B) on s1, async(A) on s2, ... in a loop,
-    never synchronising: every image is the reference's."""
+    never synchronising: every image is the reference's (scene2: with the
+    launch-camera records, and with the device camera state, lc 0)."""
     r = CamRef(which, heightfield_path)
     w, h = r.w, r.h
     cams = r.frames["cams"][:3]
-    ctx = rt_amd.Context(0)
+    ctx = rt_amd.Context(0, launch_camera=lc)
     ctx.upload(r.scene)
     s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
     torch.cuda.synchronize()
@@ -84,11 +85,12 @@ def test_async_sync_interleaved_without_host_sync(which, heightfield_path):
 
 def test_async_prepass_seen_by_other_stream(heightfield_path):
     """A camera first met by an async render is prepared on that stream; a
-    render of the same camera on another stream right after must wait for it."""
+    render of the same camera on another stream right after must wait for it
+    (the device camera state: launch_camera 0)."""
     r = CamRef("scene2", heightfield_path)
     w, h = r.w, r.h
     cams = r.frames["cams"][1:3]
-    ctx = rt_amd.Context(0)
+    ctx = rt_amd.Context(0, launch_camera=0)
     ctx.upload(r.scene)
     s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
     torch.cuda.synchronize()
@@ -131,13 +133,14 @@ def test_prepare_camera_makes_async_fast(heightfield_path):
 @pytest.mark.filterwarnings("ignore:The CUDA Graph is empty")
 def test_graph_capture_and_replay(heightfield_path):
     """rt_render_async captured in a hipGraph (torch.cuda.CUDAGraph) replays
-    the reference's image; capture of an unprepared camera is RT_E_STATE;
-    a replay after other cameras were rendered and the captured one was
-    prepared again is still exact (captured buffers are never freed)."""
+    the reference's image; capture of an unprepared camera is RT_E_STATE
+    (device camera state: launch_camera 0); a replay after other cameras were
+    rendered and the captured one was prepared again is still exact (captured
+    buffers are never freed)."""
     r = CamRef("scene2", heightfield_path)
     w, h = r.w, r.h
     cams = r.frames["cams"][:3]
-    ctx = rt_amd.Context(0)
+    ctx = rt_amd.Context(0, launch_camera=0)
     ctx.upload(r.scene)
     out = torch.zeros((h, w, 3), dtype=torch.float32, device="cuda")
     ctx.render_float(cams[0])  # prepares camera 0
@@ -267,6 +270,34 @@ def test_sequence_graph_replay_is_self_contained(heightfield_path):
 
 # the refused capture leaves its graph empty, which torch warns about
 @pytest.mark.filterwarnings("ignore:The CUDA Graph is empty")
+def test_launch_camera_captures_any_camera(heightfield_path):
+    """With the camera records in the launch (tiny scenes) there is no
+    per-camera device state: a never-rendered camera is captured directly
+    and every replay — after other cameras on other streams — is exact."""
+    r = CamRef("scene2", heightfield_path)
+    w, h = r.w, r.h
+    cams = r.frames["cams"]
+    ctx = rt_amd.Context(0)
+    ctx.upload(r.scene)
+    outs = [torch.zeros((h, w, 3), dtype=torch.float32, device="cuda") for _ in cams]
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with capture(g):
+        for f, o in zip(cams, outs):
+            ctx.render_async(f, 0, o.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    s1 = torch.cuda.Stream()
+    tmp = torch.zeros((h, w, 3), dtype=torch.float32, device="cuda")
+    for rep in range(2):
+        for o in outs:
+            o.zero_()
+        g.replay()
+        ctx.render_async(r.frames["path"][rep + 1], 0, tmp.data_ptr(), s1.cuda_stream)
+        torch.cuda.synchronize()
+        for i, o in enumerate(outs):
+            assert r.matches(o.cpu().numpy(), "cams", i), (rep, i)
+        assert r.matches(tmp.cpu().numpy(), "path", rep + 1)
+
+
 def test_capture_after_async_prepass_on_another_stream(heightfield_path):
     """A camera first prepared by an async render on stream s1 (its state
     write pending there) cannot be captured on another stream — that would
@@ -275,7 +306,7 @@ def test_capture_after_async_prepass_on_another_stream(heightfield_path):
     r = CamRef("scene2", heightfield_path)
     w, h = r.w, r.h
     f = r.frames["cams"][2]
-    ctx = rt_amd.Context(0)
+    ctx = rt_amd.Context(0, launch_camera=0)
     ctx.upload(r.scene)
     s1 = torch.cuda.Stream()
     out = torch.zeros((h, w, 3), dtype=torch.float32, device="cuda")
