@@ -188,14 +188,7 @@ __device__ __forceinline__ void camera_wave_batch(const SceneDev& S, const WaveC
         }
         wave_lds_sync();
         const int n = __popcll(m);
-        unsigned long long mm = m;
         for (int j = 0; j < n; ++j) {
-            // survivor j's dmin (its lane's record): when every lane already
-            // holds a hit nearer than it, none of its hits (t >= dmin > best)
-            // can win or tie — the camera-list walk's exit, as a skip
-            const int lj = (int)__builtin_ctzll(mm);
-            mm &= mm - 1;
-            if (!__any((bi < 0) | !(bt < readlanef(c1.x, lj)))) continue;
             RT_EV(cnt, 2);
             const float4 a = win.a[j], b = win.b[j];
             const float2 c = win.c[j];
@@ -210,10 +203,8 @@ __device__ __forceinline__ void camera_wave_batch(const SceneDev& S, const WaveC
         return;
     }
     while (m) {
-        const int lk = (int)__builtin_ctzll(m);
-        const int kk = k0 + lk;
+        const int kk = k0 + (int)__builtin_ctzll(m);
         m &= m - 1;
-        if (!__any((bi < 0) | !(bt < readlanef(c1.x, lk)))) continue;  // (as above)
         RT_EV(cnt, 2);
         if (S.use_tricam) {
             const float4* r = S.tricam + 4 * kk;
@@ -436,34 +427,41 @@ struct TinyCam {
     int n;       // listed triangles (never-hit ones left out)
     int masked;  // 1: mask[] holds the tiles' bits (rows aligned to the tile grid); 0: test all
     int tiles_x, tiles_y;
-    float cosW, sinW, chord, pad;  // the tile cone's width (wbound), as wave_cone would hold it
+    float cosW, sinW, chord;  // the tile cone's width (wbound), as wave_cone would hold it
+    int grid_x, grid_y;       // (the persistent-wave A/B build: the launch's tile grid)
     const unsigned* mask;          // per tile of the full frame: bit j = keep triangle j
     // per triangle, nearest first: [c0 = axis, cosT] [edge 0] [edge 1] [edge 2]
     // [tricam 0] [1] [2] [3 = tq, file index, dmin, sinT]
     float4 rec[8 * kTinyMax];
 };
 
-// rt_tiny_masks: one thread per tile of the rows the frame renders.
+// rt_tiny_masks: 32 lanes per tile (lane & 31 = triangle j), two tiles per
+// wave, only the tiles of the rows the frame renders; each half-wave's
+// ballot is its tile's mask.  (One thread per tile walking the triangles
+// took 7 us at C2: 127 workgroups, a serial chain per thread.)
+static_assert(kTinyMax <= 32, "one half-wave per tile");
 __global__ __launch_bounds__(256) void rt_tiny_masks(const FrameDev F, const TinyCam T, unsigned* __restrict__ mask)
 {
-    const int t = (int)(blockIdx.x * blockDim.x + threadIdx.x);
-    if (t >= T.tiles_x * T.tiles_y) return;
-    const int tx = t % T.tiles_x, ty = t / T.tiles_x;
+    const int lane = (int)(threadIdx.x & 63), j = lane & 31;
+    const int t = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 5);
+    const bool in = t < T.tiles_x * T.tiles_y;
+    const int tx = in ? t % T.tiles_x : 0, ty = in ? t / T.tiles_x : 0;
     const int rb = F.band_rows > 0 ? 0 : F.row_begin, re = F.band_rows > 0 ? F.height : F.row_end;
-    if (ty * 8 >= re || ty * 8 + 8 <= rb) return;  // rows this frame does not render
-    const int px = min(tx * 8 + 4, F.width - 1), py = min(ty * 8 + 4, F.height - 1);
-    WaveCone wc;
-    wc.w = camera_dir(F, px, py);
-    wc.cosW = T.cosW;
-    wc.sinW = T.sinW;
-    wc.chord = T.chord;
-    wc.ok = true;
-    unsigned m = 0;
-    for (int j = 0; j < T.n; ++j) {
+    const bool rows = in && ty * 8 < re && ty * 8 + 8 > rb;  // rows this frame renders
+    bool keep = false;
+    if (rows && j < T.n) {
+        const int px = min(tx * 8 + 4, F.width - 1), py = min(ty * 8 + 4, F.height - 1);
+        WaveCone wc;
+        wc.w = camera_dir(F, px, py);
+        wc.cosW = T.cosW;
+        wc.sinW = T.sinW;
+        wc.chord = T.chord;
+        wc.ok = true;
         const float4* r = T.rec + 8 * j;
-        if (cone_overlap(wc, r[0], r[7].w, 0.0f) && edges_open(wc, r + 1, 0.0f)) m |= 1u << j;
+        keep = cone_overlap(wc, r[0], r[7].w, 0.0f) && edges_open(wc, r + 1, 0.0f);
     }
-    mask[t] = m;
+    const unsigned long long b = __ballot(keep);
+    if (rows && j == 0) mask[t] = (unsigned)(lane < 32 ? b : b >> 32);
 }
 
 // Closest hit for camera rays from the launch's records: planes and quadrics

@@ -211,34 +211,15 @@ constexpr int waves_per_eu(int maxd, int wave)
 // T: the launch's camera records (WAVE bit 32, rt_trace_tiny), else nullptr.
 template <int MAXD, int LB, int WAVE, bool COUNT>
 __device__ __forceinline__ void trace_tile(const SceneDev& S, const FrameDev& F, unsigned* __restrict__ rgba,
-                                           float* __restrict__ rgbf, StatsDev* __restrict__ stats, const TinyCam* T)
+                                           float* __restrict__ rgbf, StatsDev* __restrict__ stats, const TinyCam* T,
+                                           int bx, int by)
 {
-    // One wave per workgroup: one 8 x 8 tile each, so a CU takes a new tile
-    // as soon as any wave slot frees instead of four at once (A/B against
-    // 2 x 2 tiles per workgroup: C3 -3.1%, C5 -4.5%, C4 -3.7%, scene7 -3.4%,
-    // scene9 -1.4%, C2 -0.8%; declaring 64 threads: C5 -1.1%).
     const int lane = threadIdx.x & 63;
     // XCD-aware block order: the dispatcher deals workgroups round-robin over
     // the 8 XCDs (each with its own L2), so workgroup w runs on XCD w % 8 as
     // that XCD's (w / 8)-th; give every XCD one contiguous run of blocks in
     // row-major order, so neighbouring tiles — which read the same cells,
     // tile lists and records — share an L2.  A bijection for any grid size.
-    int bx = (int)blockIdx.x, by = (int)blockIdx.y;
-    // Chunks of K consecutive blocks dealt round-robin to the XCDs, when the
-    // grid divides evenly (whole-region runs per XCD were 1.8x slower on C3:
-    // the mesh rows then pile onto a few XCDs).  Per kernel (A/B): the
-    // big-list kernel K = 8 (C5 -1.4% against 4), the small-list kernel
-    // none (C2 -2.5% against 4; the remap's code alone costs it).
-    constexpr unsigned K = (WAVE & 2) ? RT_XCD_CHUNK_BIG : RT_XCD_CHUNK_SMALL;
-    if constexpr (K > 0) {
-        const unsigned nb = gridDim.x * gridDim.y, w = blockIdx.y * gridDim.x + blockIdx.x;
-        const unsigned x = w % kXcds, i = w / kXcds;
-        const unsigned lw = ((i / K) * kXcds + x) * K + i % K;
-        if (lw < nb && (nb % (kXcds * K)) == 0) {
-            bx = (int)(lw % gridDim.x);
-            by = (int)(lw / gridDim.x);
-        }
-    }
     const int tile_x = bx;  // 8-pixel column of the wave's tile
     const int px = tile_x * 8 + (lane & 7);
     const int ly0 = by * 8;  // the wave's first output row
@@ -341,22 +322,64 @@ __device__ __forceinline__ void trace_tile(const SceneDev& S, const FrameDev& F,
     }
 }
 
+// One wave per workgroup: one 8 x 8 tile each, so a CU takes a new tile as
+// soon as any wave slot frees instead of four at once (A/B against 2 x 2
+// tiles per workgroup: C3 -3.1%, C5 -4.5%, C4 -3.7%, scene7 -3.4%, scene9
+// -1.4%, C2 -0.8%; declaring 64 threads: C5 -1.1%).
+// XCD-aware block order: the dispatcher deals workgroups round-robin over
+// the 8 XCDs (each with its own L2), so workgroup w runs on XCD w % 8 as
+// that XCD's (w / 8)-th; chunks of K consecutive blocks go to one XCD, when
+// the grid divides evenly, so neighbouring tiles — which read the same
+// cells, tile lists and records — share an L2 (whole-region runs per XCD
+// were 1.8x slower on C3: the mesh rows then pile onto a few XCDs).  Per
+// kernel (A/B): the big-list kernel K = 8 (C5 -1.4% against 4), the
+// small-list kernels none (C2 -2.5% against 4; the remap's code alone costs it).
+template <int WAVE>
+__device__ __forceinline__ void tile_of_block(int& bx, int& by)
+{
+    bx = (int)blockIdx.x;
+    by = (int)blockIdx.y;
+    constexpr unsigned K = (WAVE & 2) ? RT_XCD_CHUNK_BIG : RT_XCD_CHUNK_SMALL;
+    if constexpr (K > 0) {
+        const unsigned nb = gridDim.x * gridDim.y, w = blockIdx.y * gridDim.x + blockIdx.x;
+        const unsigned x = w % kXcds, i = w / kXcds;
+        const unsigned lw = ((i / K) * kXcds + x) * K + i % K;
+        if (lw < nb && (nb % (kXcds * K)) == 0) {
+            bx = (int)(lw % gridDim.x);
+            by = (int)(lw / gridDim.x);
+        }
+    }
+}
+
 template <int MAXD, int LB, int WAVE, bool COUNT>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(waves_per_eu(MAXD, WAVE)))) void rt_trace_kernel(
     const SceneDev S, const FrameDev F, unsigned* __restrict__ rgba, float* __restrict__ rgbf,
     StatsDev* __restrict__ stats)
 {
-    trace_tile<MAXD, LB, WAVE, COUNT>(S, F, rgba, rgbf, stats, nullptr);
+    int bx, by;
+    tile_of_block<WAVE>(bx, by);
+    trace_tile<MAXD, LB, WAVE, COUNT>(S, F, rgba, rgbf, stats, nullptr, bx, by);
 }
 
 // Tiny scenes (WAVE bit 32): the camera records come with the launch
 // (TinyCam by value, read from the kernel-argument segment by scalar loads).
+#ifndef RT_PERSIST
+#define RT_PERSIST 0
+#endif
 template <int MAXD, int LB, int WAVE, bool COUNT>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(waves_per_eu(MAXD, WAVE)))) void rt_trace_tiny(
     const SceneDev S, const FrameDev F, const TinyCam T, unsigned* __restrict__ rgba, float* __restrict__ rgbf,
     StatsDev* __restrict__ stats)
 {
-    trace_tile<MAXD, LB, WAVE, COUNT>(S, F, rgba, rgbf, stats, &T);
+#if RT_PERSIST  // A/B: persistent waves over the launch's tile grid (T.grid_x x T.grid_y)
+    const int gx = T.grid_x, nt = gx * T.grid_y;
+    for (int w = (int)blockIdx.x; w < nt; w += (int)gridDim.x)
+        trace_tile<MAXD, LB, WAVE, COUNT>(S, F, rgba, rgbf, stats, &T, w % gx, w / gx);
+#else
+    int bx, by;
+    tile_of_block<WAVE>(bx, by);
+    trace_tile<MAXD, LB, WAVE, COUNT>(S, F, rgba, rgbf, stats, &T, bx, by);
+#endif
 }
 
 // Compiled bounce-stack capacities.  The host picks the smallest one that
@@ -1682,6 +1705,11 @@ static int launch_trace(rt_ctx* c, kernel_fn k, const TinyCam* T, bool count, Sc
     trace_dims(k, width, rows, grid, block, lds);
     if (T) {
         TinyCam Tv = *T;
+#if RT_PERSIST
+        Tv.grid_x = (int)grid.x;
+        Tv.grid_y = (int)grid.y;
+        grid = dim3(std::min(grid.x * grid.y, (unsigned)c->n_cu * 4u * RT_WAVES_PER_EU), 1);  // resident waves
+#endif
         void* args[] = {&S, &F, &Tv, &oa, &ob, &stats};
         HIP_TRY(c, hipLaunchKernel(count ? tiny_kernel<true>() : tiny_kernel<false>(), grid, block, args, 0, st));
         return RT_OK;
@@ -1803,514 +1831,7 @@ static SceneDev scene_dev(rt_ctx* c, bool lbuf, bool cbuf)
                     c->cb.inline_rec ? c->cb.rec : nullptr};
 }
 
-// ---- the camera buffer (rt_cambuf.h), host side
-// A replaced buffer that an enqueued render or build may still read: freed
-// at the next host sync of the context (or kept for a captured graph).
-static void free_later(rt_ctx* c, void* p)
-{
-    if (!p) return;
-    if (c->captured)
-        c->retired.push_back(p);
-    else
-        c->deferred.push_back(p);
-}
-
-static void cb_free(rt_ctx::CamBuf& B)
-{
-    hipFree(B.tcone);
-    hipFree(B.off);
-    hipFree(B.cur);
-    hipFree(B.flag);
-    hipFree(B.box);
-    hipFree(B.tcnt);
-    hipFree(B.rmask);
-    hipFree(B.lng);
-    hipFree(B.mid);
-    hipFree(B.stat);
-    hipFree(B.scan);
-    hipFree(B.ent);
-    hipFree(B.rec);
-    if (B.ev_tot) hipEventDestroy(B.ev_tot);
-    if (B.ev0) hipEventDestroy(B.ev0);
-    if (B.ev1) hipEventDestroy(B.ev1);
-    B = rt_ctx::CamBuf{};
-}
-
-// The camera buffer needs the frame's orientation to be a rotation (rows
-// 0-2 orthonormal to 1e-5, no translation row: cb_box reads directions in
-// camera coordinates through it) and a sane film; other frames render
-// without one (the per-wave path: the same image).
-static bool cb_frame_ok(const rt_frame* f)
-{
-    const float* m = f->orient;
-    if (m[12] != 0.0f || m[13] != 0.0f || m[14] != 0.0f) return false;
-    for (int i = 0; i < 3; ++i)
-        for (int j = 0; j < 3; ++j) {
-            const double d = (double)m[4 * i] * m[4 * j] + (double)m[4 * i + 1] * m[4 * j + 1] +
-                             (double)m[4 * i + 2] * m[4 * j + 2];
-            if (!(std::fabs(d - (i == j ? 1.0 : 0.0)) <= 1e-5)) return false;
-        }
-    const float v[4] = {f->half_w, f->half_h, f->inv_w, f->inv_h};
-    for (float x : v)
-        if (!(x > 0.0f) || !std::isfinite(x)) return false;
-    return true;
-}
-
-// Read back the last build's total and counters if its copy has landed
-// (no wait).
-static void cb_harvest(rt_ctx::CamBuf& B)
-{
-    if (!B.tot_pending || hipEventQuery(B.ev_tot) != hipSuccess) {
-        (void)hipGetLastError();
-        return;
-    }
-    B.tot_pending = false;
-    B.entries = (size_t)B.h_tot[0];
-    B.observed = std::max(B.observed, B.entries);
-    std::memcpy(B.hstat, B.h_tot + 1, sizeof B.hstat);
-    if (!B.hstat[6]) B.observed_pairs = std::max(B.observed_pairs, (size_t)B.hstat[1]);
-    // a build that did not fit (tiles sent down the per-wave path) is
-    // rebuilt at its camera's next render, now that the sizes are known
-    // (a build past 2^32 - 1 candidate pairs stays valid: every tile flagged)
-    if (B.entries > B.built_cap || (!B.hstat[6] && ((size_t)B.hstat[1] + 63) / 64 > B.built_rcap)) B.valid = false;
-}
-
-// Per-tile arrays for nt tiles, the per-build words, the deferred-triangle
-// list for the scene's triangles.
-static int cb_ensure(rt_ctx* c, rt_ctx::CamBuf& B, int nt, bool capturing)
-{
-    if (!B.ev_tot) {
-        HIP_TRY(c, hipEventCreateWithFlags(&B.ev_tot, hipEventDisableTiming));
-        HIP_TRY(c, hipEventCreate(&B.ev0));
-        HIP_TRY(c, hipEventCreate(&B.ev1));
-        B.h_tot = c->h_cbwords + 8 * (c->n_cbwords++ % kCbWordSets);  // pinned words from rt_create
-        HIP_TRY(c, hipMalloc((void**)&B.stat, 8 * sizeof(unsigned)));
-    }
-    if (nt > B.nt_alloc || c->n_tri > B.big_alloc) {
-        free_later(c, B.tcone);
-        free_later(c, B.off);
-        free_later(c, B.cur);
-        free_later(c, B.flag);
-        free_later(c, B.lng);
-        free_later(c, B.mid);
-        free_later(c, B.scan);
-        B.tcone = nullptr;
-        B.off = B.cur = B.flag = nullptr;
-        B.lng = B.mid = nullptr;
-        B.scan = nullptr;
-        B.nt_alloc = 0;
-        HIP_TRY(c, hipMalloc((void**)&B.tcone, (size_t)nt * 2 * sizeof(float4)));
-        HIP_TRY(c, hipMalloc((void**)&B.off, (size_t)(nt + 1) * sizeof(unsigned)));
-        HIP_TRY(c, hipMalloc((void**)&B.cur, (size_t)nt * sizeof(unsigned)));
-        HIP_TRY(c, hipMalloc((void**)&B.flag, (size_t)nt * sizeof(unsigned)));
-        HIP_TRY(c, hipMalloc((void**)&B.lng, (size_t)nt * sizeof(int)));
-        HIP_TRY(c, hipMalloc((void**)&B.mid, (size_t)nt * sizeof(int)));
-        B.scan_words = scan_scratch((size_t)std::max(nt, c->n_tri));
-        HIP_TRY(c, hipMalloc(&B.scan, B.scan_words * sizeof(unsigned long long)));
-        B.nt_alloc = nt;
-    }
-    if (c->n_tri > B.big_alloc) {
-        free_later(c, B.box);
-        free_later(c, B.tcnt);
-        B.box = nullptr;
-        B.tcnt = nullptr;
-        B.big_alloc = 0;
-        HIP_TRY(c, hipMalloc((void**)&B.box, (size_t)c->n_tri * sizeof(int4)));
-        HIP_TRY(c, hipMalloc((void**)&B.tcnt, (size_t)(c->n_tri + 1) * sizeof(unsigned)));
-        B.big_alloc = c->n_tri;
-    }
-    // pass masks: 1.25 x the largest candidate count read back, or a first
-    // guess of 64 candidates per triangle
-    const size_t runs = B.observed_pairs ? (B.observed_pairs / 64) * 5 / 4 + 1024
-                                         : std::max<size_t>(16384, (size_t)c->n_tri);
-    if (runs > B.rcap && !capturing) {  // a capture keeps the masks it has (the runs past them: per-wave)
-        free_later(c, B.rmask);
-        B.rmask = nullptr;
-        B.rcap = 0;
-        HIP_TRY(c, hipMalloc((void**)&B.rmask, runs * sizeof(unsigned long long)));
-        B.rcap = runs;
-    }
-    return RT_OK;
-}
-
-static int cb_grow(rt_ctx* c, rt_ctx::CamBuf& B, size_t want)
-{
-    if (want <= B.cap && B.ent) return RT_OK;
-    if (want > 0xFFFFFFF0ull) {
-        c->err = "camera buffer too large";
-        return RT_E_UNSUPPORTED;
-    }
-    free_later(c, B.ent);
-    B.ent = nullptr;
-    B.cap = 0;
-    HIP_TRY(c, hipMalloc((void**)&B.ent, std::max<size_t>(want, 1) * sizeof(int2)));
-    B.cap = std::max<size_t>(want, 1);
-    return RT_OK;
-}
-
-// Entries a build should have room for: 1.25 x the largest total read back
-// (plus slack), or a first guess of 16 per tile.
-static size_t cb_want_cap(const rt_ctx::CamBuf& B, int nt)
-{
-    if (B.observed == 0) return std::max<size_t>(65536, (size_t)nt * 16);
-    return B.observed + B.observed / 4 + 4096;
-}
-
-// The widest tile cone: lanes lie within 4 pixels of the reference lane in
-// each axis, and on the film plane z = -1 (|d0| >= 1) an angle is at most the
-// distance; wave_cone lowers the cosine by 1e-6 (plus < 5e-7 of rounding).
-// rt_cb_tiles_boxes checks every tile against it (a wider tile gets no list);
-// the launch-camera boxes rely on it analytically, so they are used only
-// while the 4-pixel distance itself stays below the 1-radian cap (*uncapped).
-static float tile_wbound(const rt_frame* f, float& cos_wbound, bool* uncapped = nullptr)
-{
-    const double px = 2.0 * f->half_w * (double)f->inv_w, py = 2.0 * f->half_h * (double)f->inv_h;
-    const double a = std::sqrt(16.0 * px * px + 16.0 * py * py) * 1.001;
-    if (uncapped) *uncapped = a < 1.0;
-    const double amax = std::min(1.0, a);
-    const double wb = std::acos(std::max(-1.0, std::cos(amax) - 2e-6)) + 1e-6;
-    float w = (float)wb;
-    if ((double)w < wb) w = std::nextafter(w, INFINITY);
-    float cw = (float)std::cos((double)w);
-    if ((double)cw < std::cos((double)w)) cw = std::nextafter(cw, INFINITY);
-    cos_wbound = cw;
-    return w;
-}
-
-// ---- camera records in the launch (tiny scenes; rt_cull.h TinyCam)
-// Used for depth-0 frames of scenes of 1..kTinyMax triangles whose shadow
-// rays go through the light buffer (RT_OPT_LAUNCH_CAMERA, on by default):
-// then nothing per camera lives on the device.
-static bool tiny_ok(const rt_ctx* c, int depth, bool lbuf)
-{
-    return c->opt_launch_camera && depth == 0 && lbuf && c->n_tri > 0 && c->n_tri <= kTinyMax &&
-           (int)c->h_tri.size() == 3 * c->n_tri;
-}
-
-// The frame's camera records (rt_cull.h TinyCam): per triangle the camera
-// cone and edge records and the tricam record — the device prepass's own
-// functions, in double / float on the host — sorted by (dmin, triangle);
-// pairs never reported from this camera (cosT 2) are left out.  Tile masks
-// are usable when the orientation is a rotation and the tiles' spread bound
-// holds analytically (tile_wbound); the mask pointer is set by tiny_masks.
-static void tiny_build(const rt_ctx* c, const rt_frame* f, TinyCam& T)
-{
-    const int n = c->n_tri;
-    float4 cone[kTinyMax * kConeRec], tc[kTinyMax * 4];
-    for (int k = 0; k < n; ++k)
-        cone_record(c->h_tri.data(), c->h_sph.data(), c->h_nrm.data(), c->h_coef.data(), n, f->cam_pos[0],
-                    f->cam_pos[1], f->cam_pos[2], 1, 0.0f, cone, tc, k);
-    float cwb = 0.f;
-    bool uncapped = false;
-    const float wb = tile_wbound(f, cwb, &uncapped);
-    int ord[kTinyMax], m = 0;
-    float key[kTinyMax];
-    for (int k = 0; k < n; ++k) {
-        if (cone[2 * k].w > 1.0f) continue;  // never reported from this camera
-        key[k] = cone[2 * k + 1].x == cone[2 * k + 1].x ? cone[2 * k + 1].x : -INFINITY;
-        ord[m++] = k;
-    }
-    std::sort(ord, ord + m, [&](int a, int b) { return key[a] < key[b] || (key[a] == key[b] && a < b); });
-    T = TinyCam{};
-    T.n = m;
-    T.masked = cb_frame_ok(f) && uncapped ? 1 : 0;
-    T.tiles_x = (f->width + 7) / 8;
-    T.tiles_y = (f->height + 7) / 8;
-    // the tile cone of half-angle wbound as wave_cone holds a cone: cos
-    // rounded down, sin and chord (+1e-6 like wave_cone) rounded up
-    const double cw = std::cos((double)wb);
-    float cwf = (float)cw;
-    if ((double)cwf > cw) cwf = std::nextafter(cwf, -INFINITY);
-    const double sw = std::sqrt(std::max(0.0, 1.0 - (double)cwf * cwf)) + 1e-6, ch = std::sqrt(2.0 * (1.0 - cwf)) + 1e-6;
-    float swf = (float)sw, chf = (float)ch;
-    if ((double)swf < sw) swf = std::nextafter(swf, INFINITY);
-    if ((double)chf < ch) chf = std::nextafter(chf, INFINITY);
-    T.cosW = cwf;
-    T.sinW = swf;
-    T.chord = chf;
-    for (int j = 0; j < m; ++j) {
-        const int k = ord[j];
-        float4* r = T.rec + 8 * j;
-        r[0] = cone[2 * k];
-        for (int e = 0; e < 3; ++e) r[1 + e] = cone[2 * n + 3 * k + e];
-        for (int q = 0; q < 4; ++q) r[4 + q] = tc[4 * k + q];
-        r[7].z = key[k];
-        r[7].w = cone[2 * k + 1].w;  // sinT
-    }
-}
-
-// The frame's records, cached per camera (the host's part of a moving frame).
-static const TinyCam& tiny_prepare(rt_ctx* c, const rt_frame* f)
-{
-    float key[30];
-    cb_key_of(f, key);
-    if (!c->tiny_valid || std::memcmp(key, c->tiny_key, sizeof key) != 0) {
-        tiny_build(c, f, c->tiny);
-        std::memcpy(c->tiny_key, key, sizeof key);
-        c->tiny_valid = true;
-    }
-    return c->tiny;
-}
-
-// Tile masks of the launch-camera path, one buffer per stream (launches on
-// one stream run in order, so a stream's masks are rewritten only after its
-// earlier renders read them).  A hipGraph capture cannot allocate: it takes
-// a buffer of its own from a pool kept filled by uncaptured calls (the graph
-// recomputes its masks at every replay; the buffer is retired, freed at the
-// next upload) — or, with the pool empty, renders its launch unmasked (the
-// same image).  *cap_buf: a capture's buffer shared by the frames of one
-// sequence call on one internal stream (nullptr: take one per launch).
-// Sets T.mask; launches rt_tiny_masks when the masks are not the frame's.
-constexpr int kMaskPool = 8;
-static int tiny_masks(rt_ctx* c, const rt_frame* f, hipStream_t st, bool capturing, TinyCam& T,
-                      unsigned** cap_buf = nullptr)
-{
-    if (!T.masked) return RT_OK;
-    const size_t nt = (size_t)T.tiles_x * T.tiles_y;
-    FrameDev F;
-    frame_dev(f, F);
-    const unsigned blocks = (unsigned)((nt + 255) / 256);
-    if (capturing) {
-        unsigned* d = cap_buf ? *cap_buf : nullptr;
-        if (!d) {
-            if (c->mask_pool.empty() || c->mask_pool_nt < nt) {
-                T.masked = 0;  // no buffer to spare inside a capture: every listed triangle
-                return RT_OK;
-            }
-            d = c->mask_pool.back();
-            c->mask_pool.pop_back();
-            c->retired.push_back(d);
-            if (cap_buf) *cap_buf = d;
-        }
-        T.mask = d;
-        hipLaunchKernelGGL(rt_tiny_masks, dim3(blocks), dim3(256), 0, st, F, T, d);
-        HIP_TRY(c, hipGetLastError());
-        return RT_OK;
-    }
-    rt_ctx::MaskBuf* b = nullptr;
-    for (auto& q : c->tiny_masks)
-        if (q.stream == st) b = &q;
-    if (!b) {
-        c->tiny_masks.push_back(rt_ctx::MaskBuf{});
-        b = &c->tiny_masks.back();
-        b->stream = st;
-    }
-    float key[30];
-    cb_key_of(f, key);
-    if (b->cap < nt) {
-        if (b->d) free_later(c, b->d);
-        b->d = nullptr;
-        b->cap = 0;
-        b->valid = false;
-        HIP_TRY(c, hipMalloc((void**)&b->d, nt * sizeof(unsigned)));
-        b->cap = nt;
-    }
-    T.mask = b->d;
-    if (!b->valid || std::memcmp(key, b->key, sizeof key) != 0) {
-        hipLaunchKernelGGL(rt_tiny_masks, dim3(blocks), dim3(256), 0, st, F, T, b->d);
-        HIP_TRY(c, hipGetLastError());
-        std::memcpy(b->key, key, sizeof key);
-        b->valid = true;
-    }
-    // the capture pool, sized for this frame
-    if (c->mask_pool_nt < nt) {
-        for (unsigned* d : c->mask_pool) free_later(c, d);
-        c->mask_pool.clear();
-        c->mask_pool_nt = nt;
-    }
-    while ((int)c->mask_pool.size() < kMaskPool) {
-        unsigned* d = nullptr;
-        HIP_TRY(c, hipMalloc((void**)&d, nt * sizeof(unsigned)));
-        c->mask_pool.push_back(d);
-    }
-    return RT_OK;
-}
-
-static CbDev cb_dev(const rt_ctx::CamBuf& B, const rt_frame* f)
-{
-    CbDev d;
-    d.tcone = B.tcone;
-    d.off = B.off;
-    d.cur = B.cur;
-    d.flag = B.flag;
-    d.ent = B.ent;
-    d.box = B.box;
-    d.tcnt = B.tcnt;
-    d.rmask = B.rmask;
-    d.rcap = (unsigned)std::min<size_t>(B.rcap, 0xFFFFFFF0u);
-    d.lng = B.lng;
-    d.mid = B.mid;
-    d.stat = B.stat;
-    d.cap = (unsigned)B.cap;
-    d.tiles_x = (f->width + 7) / 8;
-    d.tiles_y = (f->height + 7) / 8;
-    d.wbound = tile_wbound(f, d.cos_wbound);
-    return d;
-}
-
-// Build the camera buffer B for frame f on stream st, from the per-camera
-// cone records in S (S.cone_cam; the tricam records for inline entries).
-// No host sync — except with `exact_first` (a synchronous render's first
-// build, when no total was ever read back: the count is read once and the
-// capacity sized to it before the fill).  Needs st ordered after every render that may read
-// B.  capturing: inside a hipGraph capture (no timing events, no read-back).
-static int cb_build(rt_ctx* c, rt_ctx::CamBuf& B, const rt_frame* f, const SceneDev& S, hipStream_t st,
-                    bool exact_first, bool capturing, bool allow_inline)
-{
-    const auto t0 = std::chrono::steady_clock::now();
-    const int tx = (f->width + 7) / 8, ty = (f->height + 7) / 8, nt = tx * ty;
-    B.valid = false;
-    if (B.pinned) {
-        free_later(c, B.off);
-        free_later(c, B.flag);
-        free_later(c, B.ent);
-        free_later(c, B.rec);
-        B.off = B.flag = nullptr;
-        B.ent = nullptr;
-        B.rec = nullptr;
-        B.nt_alloc = 0;  // every per-tile array is reallocated
-        B.cap = B.rec_cap = 0;
-        B.pinned = false;
-    }
-    if (!capturing) cb_harvest(B);
-    if (int rc = cb_ensure(c, B, nt, capturing)) return rc;
-    const size_t fixed = (size_t)c->opt_cb_capacity;  // RT_OPT_CB_CAPACITY (tests)
-    exact_first = exact_first && B.observed == 0 && !capturing && !fixed;
-    if (fixed && !capturing && B.cap != fixed) {
-        free_later(c, B.ent);
-        B.ent = nullptr;
-        B.cap = 0;
-    }
-    // no growth inside a capture (the caller checked B.cap > 0)
-    const size_t want = capturing ? B.cap : (fixed ? fixed : std::max(B.cap, cb_want_cap(B, nt)));
-    if (!exact_first)
-        if (int rc = cb_grow(c, B, want)) return rc;
-    // Device timing (rt_debug_cb_info) of synchronous builds only: a timing
-    // event's record drains the queue, which in an async frame is a gap of
-    // several us before and after the build (rocprofv3 timeline, C3).
-    const bool timed = !capturing && exact_first;
-    if (timed) HIP_TRY(c, hipEventRecord(B.ev0, st));
-    FrameDev F;
-    frame_dev(f, F);
-    CbDev D = cb_dev(B, f);
-    const unsigned tb = (unsigned)((nt + 3) / 4);
-    constexpr unsigned kPairGrid = 2048, kMidGrid = 2048;
-    const bool small = c->n_clu == 0;  // small lists: a tile walk instead of the binning
-    unsigned long long* tot = nullptr;
-    if (small) {
-        hipLaunchKernelGGL(rt_cb_walk<false>, dim3(tb), dim3(256), 0, st, S, F, D);
-        HIP_TRY(c, hipGetLastError());
-        HIP_TRY(c, scan_u32(B.off, (unsigned)nt, B.off, (unsigned long long*)B.scan, st, &tot));
-        if (exact_first) {
-            HIP_TRY(c, hipMemcpyAsync(B.h_tot, tot, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
-            HIP_TRY(c, hipStreamSynchronize(st));
-            B.entries = (size_t)B.h_tot[0];
-            B.observed = std::max(B.observed, B.entries);
-            if (int rc = cb_grow(c, B, cb_want_cap(B, nt))) return rc;
-            D.ent = B.ent;
-            D.cap = (unsigned)B.cap;
-        }
-        hipLaunchKernelGGL(rt_cb_walk<true>, dim3(tb), dim3(256), 0, st, S, F, D);
-    } else {
-    const unsigned nbb = (unsigned)((c->n_tri + 255) / 256);
-    hipLaunchKernelGGL(rt_cb_tiles_boxes, dim3(nbb + tb), dim3(256), 0, st, S, F, D, nbb);
-    HIP_TRY(c, hipGetLastError());
-    unsigned long long* ptot = nullptr;  // the candidate pairs' 64-bit total
-    HIP_TRY(c, scan_u32(B.tcnt, (unsigned)c->n_tri, B.tcnt, (unsigned long long*)B.scan, st, &ptot));
-    if (exact_first) {  // the pass masks sized to the candidate pairs (one read back)
-        HIP_TRY(c, hipMemcpyAsync(B.h_tot, ptot, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
-        HIP_TRY(c, hipStreamSynchronize(st));
-        const size_t pairs = (size_t)std::min<unsigned long long>(B.h_tot[0], 0xFFFFFFFFull);
-        B.observed_pairs = std::max(B.observed_pairs, pairs);
-        const size_t runs = (pairs + 63) / 64 + 1024;
-        if (runs > B.rcap) {
-            free_later(c, B.rmask);
-            B.rmask = nullptr;
-            B.rcap = 0;
-            HIP_TRY(c, hipMalloc((void**)&B.rmask, runs * sizeof(unsigned long long)));
-            B.rcap = runs;
-        }
-        D.rmask = B.rmask;
-        D.rcap = (unsigned)std::min<size_t>(B.rcap, 0xFFFFFFF0u);
-    }
-    hipLaunchKernelGGL(rt_cb_pairs<false>, dim3(kPairGrid), dim3(256), 0, st, S, D, (const unsigned long long*)ptot);
-    HIP_TRY(c, hipGetLastError());
-    HIP_TRY(c, scan_u32(B.off, (unsigned)nt, B.off, (unsigned long long*)B.scan, st, &tot));
-    if (exact_first) {  // size the entries to the count (the fill is the only reader of the capacity)
-        HIP_TRY(c, hipMemcpyAsync(B.h_tot, tot, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
-        HIP_TRY(c, hipStreamSynchronize(st));
-        B.entries = (size_t)B.h_tot[0];
-        B.observed = std::max(B.observed, B.entries);
-        if (int rc = cb_grow(c, B, cb_want_cap(B, nt))) return rc;
-        D.ent = B.ent;
-        D.cap = (unsigned)B.cap;
-    }
-    hipLaunchKernelGGL(rt_cb_pairs<true>, dim3(kPairGrid), dim3(256), 0, st, S, D, (const unsigned long long*)nullptr);
-    }
-    hipLaunchKernelGGL(rt_cb_keys_small, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, st, D, nt);
-    hipLaunchKernelGGL(rt_cb_keys_rest, dim3(kMidGrid), dim3(256), 0, st, D, (const unsigned long long*)tot,
-                       capturing ? (unsigned long long*)nullptr : B.h_tot);
-    HIP_TRY(c, hipGetLastError());
-    // inline records while the capacity fits RT_OPT_CB_INLINE_MAX_MB
-    B.inline_rec = allow_inline && (double)B.cap * 4 * sizeof(float4) <= c->opt_cb_inline_mb * 1048576.0;
-    if (B.inline_rec) {
-        if (B.rec_cap < B.cap || !B.rec) {
-            free_later(c, B.rec);
-            B.rec = nullptr;
-            B.rec_cap = 0;
-            HIP_TRY(c, hipMalloc((void**)&B.rec, B.cap * 4 * sizeof(float4)));
-            B.rec_cap = B.cap;
-        }
-        hipLaunchKernelGGL(rt_cb_expand, dim3((unsigned)((B.cap + 255) / 256)), dim3(256), 0, st,
-                           (const int2*)B.ent, (const unsigned long long*)tot, (unsigned)B.cap,
-                           (const float4*)S.tricam, B.rec);
-        HIP_TRY(c, hipGetLastError());
-    }
-    if (!capturing) {
-        HIP_TRY(c, hipEventRecord(B.ev_tot, st));  // rt_cb_keys_rest wrote h_tot
-        B.tot_pending = true;
-        if (timed) HIP_TRY(c, hipEventRecord(B.ev1, st));
-        B.timed = timed;
-    }
-    cb_key_of(f, B.key);
-    B.tiles_x = tx;
-    B.ntiles = nt;
-    B.valid = true;
-    B.built_cap = B.cap;
-    B.built_rcap = B.rcap;
-    B.host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    return RT_OK;
-}
-
-static bool cb_matches(const rt_ctx::CamBuf& B, const rt_frame* f)
-{
-    if (!B.valid) return false;
-    float key[30];
-    cb_key_of(f, key);
-    return std::memcmp(key, B.key, sizeof key) == 0;
-}
-
-static bool frame_ok(const rt_frame* f)
-{
-    return !(f->width <= 0 || f->height <= 0 || f->row_begin < 0 || f->row_end > f->height ||
-             f->row_begin > f->row_end || f->max_bounces < 0 ||
-             (f->band_rows != 0 && rt_band_rows(f->height, f->band_rows, f->band_count, f->band_index) < 0));
-}
-
-// Does building a new camera's buffer on the stream pay for an async or
-// sequence frame?  Measured (round 3, tools/camera_probe.py, moving camera):
-// the build costs ~0.24 ms + 0.017 ms per Mpx (its ~15 launches dominate
-// at 1080p), the buffer saves the trace kernel ~0.05-0.09 ms per Mpx of
-// per-wave culling on a big list (C3 1080p: 0.418 ms per frame per-wave,
-// 0.54 with the build; C5 7680 x 4320: 3.72 per-wave, 3.03 with it); on
-// small lists (<= 1,024 triangles) it saves a few us (C2 -3.6%).  So: big
-// lists from 4 Mpx of output rows; RT_OPT_CAMERA_BUFFER 2 builds for every
-// frame (tests).  Synchronous renders always build (they sync anyway).
-static bool cb_async_pays(const rt_ctx* c, const rt_frame* f)
-{
-    if (c->opt_camera_buffer == 2) return true;
-    return c->n_tri > kClusterMinTriangles && (double)f->width * frame_rows(f) >= 4e6;
-}
+#include "rt_camhost.h"
 
 // Make the per-camera state current for frame f, ordered on stream st: the
 // camera prepass when the camera moved, and the camera buffer when the
