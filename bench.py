@@ -334,16 +334,46 @@ def frame_costs(scene, frame, W, cold):
         ctx.render_async(f, dev.data_ptr(), 0, stream)
     torch.cuda.synchronize()
     async_ms = (time.perf_counter() - t0) * 1e3 / nfr
+    ev = moving_camera_events(ctx, frames2[1:], dev.data_ptr(), stream)
     res["moving_camera_ms_per_frame"] = round(sync_ms, 4)
     res["progressive"] = progressive(ctx, frame, W, rows)
     res["moving_camera"] = {"sync_host_ms_per_frame": round(sync_ms, 4),
                             "async_device_ms_per_frame": round(async_ms, 4), "frames": nfr,
+                            "same_cameras": ev,
                             "note": "camera translated every frame; sync = rt_render into pinned host memory "
                                     "(camera prepass + camera buffer + kernel + PCIe copy); async = "
                                     "rt_render_async into HBM, no host sync: the camera prepass, and the camera "
                                     "buffer where its build pays (big lists, >= 4 Mpx), on the stream"}
     ctx.close()
     return res
+
+
+def moving_camera_events(ctx, frames, dst, stream, repeats=3):
+    """The per-camera cost, apart from the picture: each moved camera rendered
+    1 + `repeats` times in a row, one HIP event pair around each launch on the
+    render stream — the camera's first frame (its per-camera work: prepasses,
+    camera buffer or tile masks) against the same camera's later frames (a
+    static camera at that position).  A moved camera sees a different picture
+    than the bench's static one, so only this pair isolates the per-camera cost."""
+    import torch
+
+    assert stream == torch.cuda.current_stream().cuda_stream  # the events' stream
+    first, again = [], []
+    for f in frames:
+        for r in range(1 + repeats):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            ctx.render_async(f, dst, 0, stream)
+            e1.record()
+            (first if r == 0 else again).append((e0, e1))
+    torch.cuda.synchronize()
+    a = sorted(e0.elapsed_time(e1) for e0, e1 in first)
+    b = sorted(e0.elapsed_time(e1) for e0, e1 in again)
+    na, nb = a[len(a) // 2], b[len(b) // 2]
+    return {"new_camera_ms": round(na, 4), "same_camera_ms": round(nb, 4), "ratio": round(na / nb, 3),
+            "cameras": len(frames), "repeats": repeats,
+            "note": "medians of per-launch HIP event pairs (dispatch gap included) over the moved cameras: each "
+                    "camera's first frame vs the same camera's next frames"}
 
 
 def main():
@@ -671,6 +701,9 @@ def main():
                 # re-renders one camera whose per-camera state is built once)
                 out["moving_camera_async_ms"] = mc["async_device_ms_per_frame"]
                 out["moving_camera_async_mray_s"] = round(W * H / mc["async_device_ms_per_frame"] / 1e3, 3)
+                # the same moved cameras, each camera's first frame against its
+                # repeats: the per-camera cost without the picture change
+                out["moving_camera_same_cameras"] = mc.get("same_cameras")
             out["frame_costs"] = fc
         if world == 1 and not args.no_cpu_baseline:
             cb = cpu_baseline(path, W, H, depth, args.cpu_seconds)

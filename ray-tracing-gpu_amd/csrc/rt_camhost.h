@@ -181,6 +181,28 @@ static float tile_wbound(const rt_frame* f, float& cos_wbound, bool* uncapped = 
     return w;
 }
 
+// The analytic tile cone (the launch-camera path's and the one-pass
+// build's): half-angle wbound as wave_cone holds a cone — cos rounded down,
+// sin and chord (+1e-6 like wave_cone) rounded up.  False when the bound is
+// capped (wide pixels) or the frame is not a rotation camera (cb_frame_ok).
+static bool tile_cone(const rt_frame* f, float& cosW, float& sinW, float& chord)
+{
+    float cwb = 0.f;
+    bool uncapped = false;
+    const float wb = tile_wbound(f, cwb, &uncapped);
+    const double cw = std::cos((double)wb);
+    float cwf = (float)cw;
+    if ((double)cwf > cw) cwf = std::nextafter(cwf, -INFINITY);
+    const double sw = std::sqrt(std::max(0.0, 1.0 - (double)cwf * cwf)) + 1e-6, ch = std::sqrt(2.0 * (1.0 - cwf)) + 1e-6;
+    float swf = (float)sw, chf = (float)ch;
+    if ((double)swf < sw) swf = std::nextafter(swf, INFINITY);
+    if ((double)chf < ch) chf = std::nextafter(chf, INFINITY);
+    cosW = cwf;
+    sinW = swf;
+    chord = chf;
+    return uncapped && cb_frame_ok(f);
+}
+
 // ---- camera records in the launch (tiny scenes; rt_cull.h TinyCam)
 // Used for depth-0 frames of scenes of 1..kTinyMax triangles whose shadow
 // rays go through the light buffer (RT_OPT_LAUNCH_CAMERA, on by default):
@@ -189,6 +211,20 @@ static bool tiny_ok(const rt_ctx* c, int depth, bool lbuf)
 {
     return c->opt_launch_camera && depth == 0 && lbuf && c->n_tri > 0 && c->n_tri <= kTinyMax &&
            (int)c->h_tri.size() == 3 * c->n_tri;
+}
+
+// One mask half-space of rt_cull.h tiny_tile_mask: dot(w, p.xyz) >= p.w,
+// the threshold lowered by 1e-6 more than the wave test's margin (the
+// device's fused dot product is within 3e-7 of the wave test's) and rounded
+// down; a plane with a NaN passes everything, as the wave test's NaN
+// comparisons do.
+static float4 tiny_plane(const float4 n, double thr)
+{
+    if (n.x != n.x || n.y != n.y || n.z != n.z || thr != thr) return make_float4(0.f, 0.f, 0.f, -INFINITY);
+    thr -= 1e-6;
+    float t = (float)thr;
+    if ((double)t > thr) t = std::nextafter(t, -INFINITY);
+    return make_float4(n.x, n.y, n.z, t);
 }
 
 // The frame's camera records (rt_cull.h TinyCam): per triangle the camera
@@ -204,9 +240,6 @@ static void tiny_build(const rt_ctx* c, const rt_frame* f, TinyCam& T)
     for (int k = 0; k < n; ++k)
         cone_record(c->h_tri.data(), c->h_sph.data(), c->h_nrm.data(), c->h_coef.data(), n, f->cam_pos[0],
                     f->cam_pos[1], f->cam_pos[2], 1, 0.0f, cone, tc, k);
-    float cwb = 0.f;
-    bool uncapped = false;
-    const float wb = tile_wbound(f, cwb, &uncapped);
     int ord[kTinyMax], m = 0;
     float key[kTinyMax];
     for (int k = 0; k < n; ++k) {
@@ -217,29 +250,36 @@ static void tiny_build(const rt_ctx* c, const rt_frame* f, TinyCam& T)
     std::sort(ord, ord + m, [&](int a, int b) { return key[a] < key[b] || (key[a] == key[b] && a < b); });
     T = TinyCam{};
     T.n = m;
-    T.masked = cb_frame_ok(f) && uncapped ? 1 : 0;
+    float cwf, swf, chf;
+    T.masked = tile_cone(f, cwf, swf, chf) ? 1 : 0;
     T.tiles_x = (f->width + 7) / 8;
     T.tiles_y = (f->height + 7) / 8;
-    // the tile cone of half-angle wbound as wave_cone holds a cone: cos
-    // rounded down, sin and chord (+1e-6 like wave_cone) rounded up
-    const double cw = std::cos((double)wb);
-    float cwf = (float)cw;
-    if ((double)cwf > cw) cwf = std::nextafter(cwf, -INFINITY);
-    const double sw = std::sqrt(std::max(0.0, 1.0 - (double)cwf * cwf)) + 1e-6, ch = std::sqrt(2.0 * (1.0 - cwf)) + 1e-6;
-    float swf = (float)sw, chf = (float)ch;
-    if ((double)swf < sw) swf = std::nextafter(swf, INFINITY);
-    if ((double)chf < ch) chf = std::nextafter(chf, INFINITY);
     T.cosW = cwf;
     T.sinW = swf;
     T.chord = chf;
     for (int j = 0; j < m; ++j) {
         const int k = ord[j];
         float4* r = T.rec + 8 * j;
-        r[0] = cone[2 * k];
-        for (int e = 0; e < 3; ++e) r[1 + e] = cone[2 * n + 3 * k + e];
+        const float4 c0 = cone[2 * k];
+        const float sinT = cone[2 * k + 1].w;
+        // cone_overlap at ang 0: pass iff !(cosT > 0) or dot(w, axis) >=
+        // cosW cosT - sinW sinT - 2e-6
+        float4 p[4];
+        p[0] = c0.w > 0.0f ? tiny_plane(c0, (double)cwf * c0.w - (double)swf * sinT - 2e-6)
+                           : make_float4(0.f, 0.f, 0.f, -INFINITY);
+        // edge_open at ang 0: pass iff !(dot(w, e) + chord + 2e-6 < e.w)
+        for (int e = 0; e < 3; ++e) {
+            const float4 ed = cone[2 * n + 3 * k + e];
+            p[1 + e] = tiny_plane(ed, (double)ed.w - (double)chf - 2e-6);
+        }
+        for (int h = 0; h < 2; ++h) {  // paired for the packed FMAs (TinyLane)
+            const float4 u = p[2 * h], v = p[2 * h + 1];
+            r[2 * h] = make_float4(u.x, v.x, u.y, v.y);
+            r[2 * h + 1] = make_float4(u.z, v.z, u.w, v.w);
+        }
         for (int q = 0; q < 4; ++q) r[4 + q] = tc[4 * k + q];
         r[7].z = key[k];
-        r[7].w = cone[2 * k + 1].w;  // sinT
+        r[7].w = 0.0f;
     }
 }
 
@@ -258,22 +298,22 @@ static const TinyCam& tiny_prepare(rt_ctx* c, const rt_frame* f)
 
 // Tile masks of the launch-camera path, one buffer per stream (launches on
 // one stream run in order, so a stream's masks are rewritten only after its
-// earlier renders read them).  A hipGraph capture cannot allocate: it takes
-// a buffer of its own from a pool kept filled by uncaptured calls (the graph
-// recomputes its masks at every replay; the buffer is retired, freed at the
-// next upload) — or, with the pool empty, renders its launch unmasked (the
-// same image).  *cap_buf: a capture's buffer shared by the frames of one
-// sequence call on one internal stream (nullptr: take one per launch).
-// Sets T.mask; launches rt_tiny_masks when the masks are not the frame's.
+// earlier renders read them).  A camera's first frame on a stream computes
+// them in the trace kernel (*self = true: the WAVE bit 64 variant stores
+// each tile's mask); its later frames read them.  A hipGraph capture cannot
+// allocate: it takes a buffer of its own from a pool kept filled by
+// uncaptured calls and always computes (its replays recompute in place; the
+// buffer is retired, freed at the next upload) — or, with the pool empty,
+// renders unmasked (the same image).  *cap_buf: a capture's buffer shared by
+// the frames of one sequence call on one internal stream (nullptr: one per
+// launch).  Sets T.mask.
 constexpr int kMaskPool = 8;
-static int tiny_masks(rt_ctx* c, const rt_frame* f, hipStream_t st, bool capturing, TinyCam& T,
+static int tiny_masks(rt_ctx* c, const rt_frame* f, hipStream_t st, bool capturing, TinyCam& T, bool* self,
                       unsigned** cap_buf = nullptr)
 {
+    *self = false;
     if (!T.masked) return RT_OK;
     const size_t nt = (size_t)T.tiles_x * T.tiles_y;
-    FrameDev F;
-    frame_dev(f, F);
-    const unsigned blocks = (unsigned)((nt + 7) / 8);  // 8 tiles per 256-thread block
     if (capturing) {
         unsigned* d = cap_buf ? *cap_buf : nullptr;
         if (!d) {
@@ -287,8 +327,7 @@ static int tiny_masks(rt_ctx* c, const rt_frame* f, hipStream_t st, bool capturi
             if (cap_buf) *cap_buf = d;
         }
         T.mask = d;
-        hipLaunchKernelGGL(rt_tiny_masks, dim3(blocks), dim3(256), 0, st, F, T, d);
-        HIP_TRY(c, hipGetLastError());
+        *self = true;
         return RT_OK;
     }
     rt_ctx::MaskBuf* b = nullptr;
@@ -311,8 +350,7 @@ static int tiny_masks(rt_ctx* c, const rt_frame* f, hipStream_t st, bool capturi
     }
     T.mask = b->d;
     if (!b->valid || std::memcmp(key, b->key, sizeof key) != 0) {
-        hipLaunchKernelGGL(rt_tiny_masks, dim3(blocks), dim3(256), 0, st, F, T, b->d);
-        HIP_TRY(c, hipGetLastError());
+        *self = true;
         std::memcpy(b->key, key, sizeof key);
         b->valid = true;
     }
@@ -480,8 +518,76 @@ static int cb_build(rt_ctx* c, rt_ctx::CamBuf& B, const rt_frame* f, const Scene
     B.tiles_x = tx;
     B.ntiles = nt;
     B.valid = true;
+    B.fixed = 0;
     B.built_cap = B.cap;
     B.built_rcap = B.rcap;
+    B.host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return RT_OK;
+}
+
+// The one-pass build (rt_cambuf.h rt_cb_bin) of a moving camera's frame:
+// big lists (clusters: the lists' overflow takes the clustered per-wave
+// path), the analytic tile cone within its bound, and t K entry offsets in
+// 32 bits.  RT_OPT_CAMERA_BUFFER 3: for any scene with triangles (tests).
+constexpr unsigned kCbBinK = 64;
+static bool cb_bin_ok(const rt_ctx* c, const rt_frame* f)
+{
+    if (c->opt_camera_buffer != 3 && (c->opt_camera_buffer != 1 || c->n_clu == 0)) return false;
+    float cw, sw, ch;
+    const size_t nt = (size_t)((f->width + 7) / 8) * ((f->height + 7) / 8);
+    return tile_cone(f, cw, sw, ch) && nt * kCbBinK < 0xFFFFFFF0ull;
+}
+
+static int cb_build_bin(rt_ctx* c, rt_ctx::CamBuf& B, const rt_frame* f, const SceneDev& S, hipStream_t st,
+                        bool capturing)
+{
+    const auto t0 = std::chrono::steady_clock::now();
+    const int tx = (f->width + 7) / 8, ty = (f->height + 7) / 8, nt = tx * ty;
+    B.valid = false;
+    if (B.pinned) {  // a captured render reads the current arrays: write fresh ones
+        free_later(c, B.off);
+        free_later(c, B.flag);
+        free_later(c, B.ent);
+        free_later(c, B.rec);
+        B.off = B.flag = nullptr;
+        B.ent = nullptr;
+        B.rec = nullptr;
+        B.nt_alloc = 0;
+        B.cap = B.rec_cap = 0;
+        B.pinned = false;
+    }
+    if (!capturing) cb_harvest(B);
+    if (int rc = cb_ensure(c, B, nt, capturing)) return rc;
+    const size_t want = (size_t)nt * kCbBinK;
+    if (B.cap < want) {
+        if (capturing) return RT_OK;  // no allocation inside a capture: no buffer (the per-wave path)
+        free_later(c, B.ent);
+        B.ent = nullptr;
+        B.cap = 0;
+        if (int rc = cb_grow(c, B, want)) return rc;
+    }
+    CbBin P;
+    tile_cone(f, P.cosW, P.sinW, P.chord);
+    P.K = kCbBinK;
+    FrameDev F;
+    frame_dev(f, F);
+    const CbDev D = cb_dev(B, f);
+    const unsigned nbb = (unsigned)((c->n_tri + 255) / 256);
+    hipLaunchKernelGGL(rt_cb_bin_boxes, dim3(nbb + (unsigned)((nt + 255) / 256)), dim3(256), 0, st, S, F, D, nbb);
+    HIP_TRY(c, hipGetLastError());
+    hipLaunchKernelGGL(rt_cb_bin, dim3((unsigned)((c->n_tri + 3) / 4)), dim3(256), 0, st, S, F, D, P);
+    HIP_TRY(c, hipGetLastError());
+    B.inline_rec = false;
+    cb_key_of(f, B.key);
+    B.tiles_x = tx;
+    B.ntiles = nt;
+    B.valid = true;
+    B.fixed = kCbBinK;
+    B.bin_frame = F;
+    B.bin = P;
+    B.built_cap = B.cap;
+    B.built_rcap = B.rcap;
+    B.timed = false;
     B.host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return RT_OK;
 }

@@ -338,13 +338,14 @@ __device__ __forceinline__ int closest_hit_camera_list(const SceneDev& S, int ti
                                     make_float4(b.w, c.x, c.y, 0.f), O, D, t);
         take_min(ok, t, __float_as_int(c.z), bt, bi);
     }
-    const unsigned e1 = S.cb_off[tile + 1];
+    const unsigned e0 = S.cb_fixed ? (unsigned)tile * S.cb_fixed : S.cb_off[tile];
+    const unsigned e1 = S.cb_fixed ? e0 + S.cb_off[tile] : S.cb_off[tile + 1];
     if constexpr (INLINE) {
         constexpr unsigned W = kCbLdsW;
         const int lane = (int)(threadIdx.x & 63);
         const LdsWin win = lds_window();
         const bool inl = INLINE && S.cb_rec;
-        for (unsigned w0 = S.cb_off[tile]; w0 < e1; w0 += W) {
+        for (unsigned w0 = e0; w0 < e1; w0 += W) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             if ((unsigned)lane < W && w0 + lane < e1) {
@@ -387,7 +388,7 @@ __device__ __forceinline__ int closest_hit_camera_list(const SceneDev& S, int ti
         return bi;
     }
     if (INLINE && S.cb_rec) {  // records inline: one scalar load round trip per entry
-        for (unsigned e = S.cb_off[tile]; e < e1; ++e) {
+        for (unsigned e = e0; e < e1; ++e) {
             const float4* r = S.cb_rec + 4 * (size_t)e;
             const float4 a = r[0], b = r[1], c = r[2], d = r[3];  // key in d.z
             if (!__any((bi < 0) | !(bt < d.z))) break;
@@ -395,7 +396,7 @@ __device__ __forceinline__ int closest_hit_camera_list(const SceneDev& S, int ti
             camera_tri(a, b, c, d, D, bt, bi, cnt);
         }
     } else {
-        for (unsigned e = S.cb_off[tile]; e < e1; ++e) {
+        for (unsigned e = e0; e < e1; ++e) {
             const int2 en = S.cb_ent[e];
             if (!__any((bi < 0) | !(bt < __int_as_float(en.y)))) break;
             RT_EV(cnt, 2);
@@ -412,65 +413,84 @@ __device__ __forceinline__ int closest_hit_camera_list(const SceneDev& S, int ti
 // camera cone and edge records (cone_record, in double), its tricam record
 // (the values Triangle.cpp:139-160 computes for a ray from the camera) and
 // its dmin (no reported hit nearer), sorted nearest first, and passes them BY
-// VALUE with the kernel launches — no camera prepass, no per-camera arrays:
+// VALUE with the kernel launch — no camera prepass, no per-camera arrays:
 // the records arrive by scalar loads from the kernel-argument segment.
-// A tile's triangles are a bit mask (rt_tiny_masks, one thread per 8x8
-// tile, a few us): triangle j is kept iff the camera wave test passes for a
-// cone that holds every ray of the tile — axis = the tile's reference ray
-// (lane 36, pixel (8tx + 4, 8ty + 4) clamped), half-angle = wbound, the
-// analytic bound on every tile's spread (the host's tile_wbound).  That is
-// the camera buffer's test with the tile's measured cone replaced by a
-// provably wider one, so the kept set holds every triangle any of the
-// tile's rays can be reported hitting.  Static cameras reuse the masks.
+// A tile's triangles are a bit mask: triangle j is kept iff the camera wave
+// test passes for a cone that holds every ray of the tile — axis = the
+// direction of the tile's lane 36 (pixel (8tx + 4, py0 + 4), clamped like
+// every lane, so every lane's pixel lies within 4 pixels of it in each
+// axis), half-angle = wbound, the analytic bound on that spread (the host's
+// tile_wbound).  That is the camera buffer's test with the tile's measured
+// cone replaced by a provably wider one, so the kept set holds every
+// triangle any ray of the tile can be reported hitting.  The first frame of
+// a camera on a stream (WAVE bit 64) computes each tile's mask in the trace
+// kernel itself — lane j tests triangle j, one ballot — and stores it; later
+// frames of that camera on that stream read it (one scalar load).
 constexpr int kTinyMax = 20;
 struct TinyCam {
     int n;       // listed triangles (never-hit ones left out)
-    int masked;  // 1: mask[] holds the tiles' bits (rows aligned to the tile grid); 0: test all
+    int masked;  // 1: tile masks hold (rows aligned to the tile grid); 0: test every listed triangle
     int tiles_x, tiles_y;
-    float cosW, sinW, chord;  // the tile cone's width (wbound), as wave_cone would hold it
-    int grid_x, grid_y;       // (the persistent-wave A/B build: the launch's tile grid)
-    const unsigned* mask;          // per tile of the full frame: bit j = keep triangle j
-    // per triangle, nearest first: [c0 = axis, cosT] [edge 0] [edge 1] [edge 2]
-    // [tricam 0] [1] [2] [3 = tq, file index, dmin, sinT]
+    float cosW, sinW, chord, pad;  // the tile cone's width (wbound), as wave_cone would hold it
+    unsigned* mask;                // per tile of the full frame: bit j = keep triangle j
+    // per triangle, nearest first: the mask planes (cone, edge 0, edge 1,
+    // edge 2 paired as TinyLane holds them), the tricam record [0] [1] [2]
+    // [3 = tq, file index, dmin, unused]
     float4 rec[8 * kTinyMax];
 };
 
-// rt_tiny_masks: 32 lanes per tile (lane & 31 = triangle j), two tiles per
-// wave, only the tiles of the rows the frame renders; each half-wave's
-// ballot is its tile's mask.  (One thread per tile walking the triangles
-// took 7 us at C2: 127 workgroups, a serial chain per thread.)
-static_assert(kTinyMax <= 32, "one half-wave per tile");
-__global__ __launch_bounds__(256) void rt_tiny_masks(const FrameDev F, const TinyCam T, unsigned* __restrict__ mask)
+// The tile's mask, computed by the wave: lane j < n tests triangle j against
+// the tile cone around lane 36's direction (full wave: depth-0 kernels run
+// every lane).  The camera wave test (cone_overlap, edges_open) at the fixed
+// tile width is four half-space tests of that direction: dot(w, p.xyz) >=
+// p.w, with the planes and thresholds made on the host (tiny_build, margins
+// widened by 1e-6 over the wave test's, which covers the fused products
+// here), so the test is two packed FMA chains and four compares.  The
+// lane's planes are loaded at the top of the kernel (tiny_lane_load), so
+// their latency hides under the ray set-up.
+struct TinyLane {
+    float4 q[4];  // planes (0, 1) and (2, 3) paired: [x0 x1 y0 y1] [z0 z1 w0 w1] [x2 x3 y2 y3] [z2 z3 w2 w3]
+};
+__device__ __forceinline__ TinyLane tiny_lane_load(const TinyCam& T)
 {
-    const int lane = (int)(threadIdx.x & 63), j = lane & 31;
-    const int t = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 5);
-    const bool in = t < T.tiles_x * T.tiles_y;
-    const int tx = in ? t % T.tiles_x : 0, ty = in ? t / T.tiles_x : 0;
-    const int rb = F.band_rows > 0 ? 0 : F.row_begin, re = F.band_rows > 0 ? F.height : F.row_end;
-    const bool rows = in && ty * 8 < re && ty * 8 + 8 > rb;  // rows this frame renders
-    bool keep = false;
-    if (rows && j < T.n) {
-        const int px = min(tx * 8 + 4, F.width - 1), py = min(ty * 8 + 4, F.height - 1);
-        WaveCone wc;
-        wc.w = camera_dir(F, px, py);
-        wc.cosW = T.cosW;
-        wc.sinW = T.sinW;
-        wc.chord = T.chord;
-        wc.ok = true;
-        const float4* r = T.rec + 8 * j;
-        keep = cone_overlap(wc, r[0], r[7].w, 0.0f) && edges_open(wc, r + 1, 0.0f);
-    }
-    const unsigned long long b = __ballot(keep);
-    if (rows && j == 0) mask[t] = (unsigned)(lane < 32 ? b : b >> 32);
+    const int lane = (int)(threadIdx.x & 63);
+    const float4* r = T.rec + 8 * (lane < kTinyMax ? lane : kTinyMax - 1);
+    return TinyLane{{r[0], r[1], r[2], r[3]}};
+}
+__device__ __forceinline__ unsigned tiny_tile_mask(const TinyCam& T, const TinyLane& L, const Vec3 D)
+{
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const float wx = readlanef(D.x, 36), wy = readlanef(D.y, 36), wz = readlanef(D.z, 36);
+    const f2 X = {wx, wx}, Y = {wy, wy}, Z = {wz, wz};
+    f2 a = Z * f2{L.q[1].x, L.q[1].y}, b = Z * f2{L.q[3].x, L.q[3].y};
+    a = __builtin_elementwise_fma(Y, f2{L.q[0].z, L.q[0].w}, a);
+    b = __builtin_elementwise_fma(Y, f2{L.q[2].z, L.q[2].w}, b);
+    a = __builtin_elementwise_fma(X, f2{L.q[0].x, L.q[0].y}, a);
+    b = __builtin_elementwise_fma(X, f2{L.q[2].x, L.q[2].y}, b);
+    const bool keep = ((int)(threadIdx.x & 63) < T.n) & (a.x >= L.q[1].z) & (a.y >= L.q[1].w) & (b.x >= L.q[3].z) &
+                      (b.y >= L.q[3].w);
+    return (unsigned)__ballot(keep);
 }
 
 // Closest hit for camera rays from the launch's records: planes and quadrics
 // first, then the tile's kept triangles nearest first (tile < 0 or no masks:
 // every listed triangle), leaving once every lane holds a hit nearer than
 // the next dmin (t >= dmin > best: no later triangle can win or tie).
-__device__ __forceinline__ int closest_hit_camera_tiny(const SceneDev& S, const TinyCam& T, int tile, const Vec3 O,
-                                                       const Vec3 D, float& best_t, Counters& cnt)
+// SELF: the wave computed the tile's mask (tmask, tiny_tile_mask); store it
+// for the camera's later frames.
+template <bool SELF>
+__device__ __forceinline__ int closest_hit_camera_tiny(const SceneDev& S, const TinyCam& T, int tile, unsigned tmask,
+                                                       const Vec3 O, const Vec3 D, float& best_t, Counters& cnt)
 {
+    unsigned m = T.n >= 32 ? ~0u : (1u << T.n) - 1u;
+    if (T.masked && tile >= 0) {
+        if constexpr (SELF) {
+            m = tmask;
+            if ((threadIdx.x & 63) == 0) T.mask[tile] = m;
+        } else {
+            m = T.mask[tile];  // wave-uniform (scalar) load
+        }
+    }
     float bt = -1.0f;
     int bi = -1;
     for (int k = 0; k < S.n_plane; ++k) {
@@ -489,8 +509,6 @@ __device__ __forceinline__ int closest_hit_camera_tiny(const SceneDev& S, const 
                                     make_float4(b.w, c.x, c.y, 0.f), O, D, t);
         take_min(ok, t, __float_as_int(c.z), bt, bi);
     }
-    unsigned m = T.n >= 32 ? ~0u : (1u << T.n) - 1u;
-    if (T.masked && tile >= 0) m = T.mask[tile];  // wave-uniform (scalar) load
     while (m) {
         const int j = (int)__builtin_ctz(m);
         m &= m - 1u;
@@ -509,9 +527,10 @@ __device__ __forceinline__ int closest_hit_camera_tiny(const SceneDev& S, const 
 // tile >= 0: the wave is that camera-buffer tile (WAVE bit 8).
 template <int WAVE>
 __device__ __forceinline__ int closest_hit_primary(const SceneDev& S, const Vec3 O, const Vec3 D, float& t,
-                                                   Counters& cnt, int tile = -1, const TinyCam* T = nullptr)
+                                                   Counters& cnt, int tile = -1, const TinyCam* T = nullptr,
+                                                   unsigned tmask = 0)
 {
-    if constexpr ((WAVE & 32) != 0) return closest_hit_camera_tiny(S, *T, tile, O, D, t, cnt);
+    if constexpr ((WAVE & 32) != 0) return closest_hit_camera_tiny<(WAVE & 64) != 0>(S, *T, tile, tmask, O, D, t, cnt);
     if ((WAVE & 8) && tile >= 0 && wave_full())
         return closest_hit_camera_list<(WAVE & 2) != 0>(S, tile, O, D, t, cnt);
     if ((WAVE & 3) > 0 && wave_full()) {

@@ -64,13 +64,13 @@ struct Refr {
 
 template <int MAXD, int LB, int WAVE>
 __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, Counters& cnt, bool live, int tile,
-                          const TinyCam* T)
+                          const TinyCam* T, unsigned tmask = 0)
 {
     const Color bg{F.bg[0], F.bg[1], F.bg[2]};
     if constexpr (MAXD == 0) {
         float t;
         RT_MARK(cnt, 0);
-        const int idx = closest_hit_primary<(WAVE & 43)>(S, O, D, t, cnt, tile, T);
+        const int idx = closest_hit_primary<(WAVE & 107)>(S, O, D, t, cnt, tile, T, tmask);
         RT_MARK(cnt, 1);
         // Lanes that miss (or lie outside the frame) stay in step through the
         // shading so the wave stays whole for wave-level shadow culling.
@@ -102,7 +102,7 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
         for (;;) {
             if (trace) {
                 float t;
-                const int idx = camera_ray ? closest_hit_primary<(WAVE & 43)>(S, O, D, t, cnt, tile, T)
+                const int idx = camera_ray ? closest_hit_primary<(WAVE & 107)>(S, O, D, t, cnt, tile, T)
                                            : closest_hit<false>(S, O, D, t, cnt);
                 camera_ray = false;
                 ret = bg;
@@ -240,6 +240,8 @@ __device__ __forceinline__ void trace_tile(const SceneDev& S, const FrameDev& F,
     cnt.last = __builtin_amdgcn_s_memtime();
 #endif
     Color c{0.f, 0.f, 0.f};
+    TinyLane tl;
+    if constexpr ((WAVE & 64) != 0) tl = tiny_lane_load(*T);  // the mask's records, in flight under the set-up
     // Without bounces every lane runs (lanes outside the frame on a clamped
     // pixel, result dropped) so edge waves stay whole for wave-level culling.
     if (MAXD == 0 || valid) {
@@ -254,10 +256,12 @@ __device__ __forceinline__ void trace_tile(const SceneDev& S, const FrameDev& F,
         int tile = -1;
         if ((WAVE & 8) && S.cb_tiles_x > 0 && (py0 & 7) == 0) {
             tile = (py0 >> 3) * S.cb_tiles_x + tile_x;
-            if (S.cb_flag[tile]) tile = -1;
+            if (S.cb_fixed ? S.cb_off[tile] > S.cb_fixed : S.cb_flag[tile] != 0) tile = -1;
         }
+        unsigned tmask = 0;
         if ((WAVE & 32) && (py0 & 7) == 0) tile = (py0 >> 3) * T->tiles_x + tile_x;
-        c = radiance<MAXD, LB, WAVE>(S, F, O, D, cnt, valid, tile, T);
+        if constexpr ((WAVE & 64) != 0) tmask = tiny_tile_mask(*T, tl, D);
+        c = radiance<MAXD, LB, WAVE>(S, F, O, D, cnt, valid, tile, T, tmask);
         if (valid) {
             const size_t o = (size_t)ly * F.width + px;
             if (rgbf) {
@@ -363,23 +367,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(waves_per_eu
 
 // Tiny scenes (WAVE bit 32): the camera records come with the launch
 // (TinyCam by value, read from the kernel-argument segment by scalar loads).
-#ifndef RT_PERSIST
-#define RT_PERSIST 0
-#endif
 template <int MAXD, int LB, int WAVE, bool COUNT>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(waves_per_eu(MAXD, WAVE)))) void rt_trace_tiny(
     const SceneDev S, const FrameDev F, const TinyCam T, unsigned* __restrict__ rgba, float* __restrict__ rgbf,
     StatsDev* __restrict__ stats)
 {
-#if RT_PERSIST  // A/B: persistent waves over the launch's tile grid (T.grid_x x T.grid_y)
-    const int gx = T.grid_x, nt = gx * T.grid_y;
-    for (int w = (int)blockIdx.x; w < nt; w += (int)gridDim.x)
-        trace_tile<MAXD, LB, WAVE, COUNT>(S, F, rgba, rgbf, stats, &T, w % gx, w / gx);
-#else
     int bx, by;
     tile_of_block<WAVE>(bx, by);
     trace_tile<MAXD, LB, WAVE, COUNT>(S, F, rgba, rgbf, stats, &T, bx, by);
-#endif
 }
 
 // Compiled bounce-stack capacities.  The host picks the smallest one that
@@ -504,6 +499,9 @@ struct rt_ctx {
         bool pinned = false;
         double host_ms = 0.0, build_ms = 0.0;
         bool timed = false;
+        unsigned fixed = 0;         // > 0: the one-pass build's fixed-capacity lists (SceneDev::cb_fixed)
+        FrameDev bin_frame{};       // the one-pass build's frame and tile cone (rt_debug_cb_verify)
+        CbBin bin{};
     };
     CamBuf cb;
     // Camera state of rt_render_sequence_async: kSeqSlots slots of the
@@ -739,7 +737,7 @@ RT_EXPORT int rt_set_option(rt_ctx* c, int32_t opt, double v)
         c->opt_light_buffer = (int)v;
         return RT_OK;
     case RT_OPT_CAMERA_BUFFER:
-        if (v != 0 && v != 1 && v != 2) return RT_E_ARG;
+        if (v != 0 && v != 1 && v != 2 && v != 3) return RT_E_ARG;
         if ((int)v != c->opt_camera_buffer) c->cb.valid = false;
         c->opt_camera_buffer = (int)v;
         return RT_OK;
@@ -1688,30 +1686,26 @@ static void trace_dims(kernel_fn k, int width, int rows, dim3& grid, dim3& block
 }
 
 // The launch-camera kernel (tiny scenes: camera buffer replaced by the
-// launch's records, light-buffer shadows, one light per pass).
+// launch's records, light-buffer shadows, one light per pass); SELF: the
+// camera's first frame on the stream, which computes and stores the masks.
 template <bool COUNT>
-static const void* tiny_kernel()
+static const void* tiny_kernel(bool self)
 {
-    return (const void*)&rt_trace_tiny<0, 1, 37, COUNT>;
+    return self ? (const void*)&rt_trace_tiny<0, 1, 101, COUNT> : (const void*)&rt_trace_tiny<0, 1, 37, COUNT>;
 }
 
 // One trace launch over `rows` output rows (T: the launch-camera kernel with
 // its records, else kernel k).
 static int launch_trace(rt_ctx* c, kernel_fn k, const TinyCam* T, bool count, SceneDev& S, FrameDev& F, int width,
-                        int rows, unsigned* oa, float* ob, StatsDev* stats, hipStream_t st)
+                        int rows, unsigned* oa, float* ob, StatsDev* stats, hipStream_t st, bool self = false)
 {
     dim3 grid, block;
     unsigned lds = 0;
     trace_dims(k, width, rows, grid, block, lds);
     if (T) {
         TinyCam Tv = *T;
-#if RT_PERSIST
-        Tv.grid_x = (int)grid.x;
-        Tv.grid_y = (int)grid.y;
-        grid = dim3(std::min(grid.x * grid.y, (unsigned)c->n_cu * 4u * RT_WAVES_PER_EU), 1);  // resident waves
-#endif
         void* args[] = {&S, &F, &Tv, &oa, &ob, &stats};
-        HIP_TRY(c, hipLaunchKernel(count ? tiny_kernel<true>() : tiny_kernel<false>(), grid, block, args, 0, st));
+        HIP_TRY(c, hipLaunchKernel(count ? tiny_kernel<true>(self) : tiny_kernel<false>(self), grid, block, args, 0, st));
         return RT_OK;
     }
     void* args[] = {&S, &F, &oa, &ob, &stats};
@@ -1828,7 +1822,7 @@ static SceneDev scene_dev(rt_ctx* c, bool lbuf, bool cbuf)
                     lbuf ? c->lb_levels : 0, c->d_lb_off, c->d_lb_ent, c->d_lb_dcap, c->d_lb_meta,
                     (c->d_uni && c->opt_union) ? c->d_uni : nullptr,
                     c->cb.off, c->cb.ent, c->cb.flag, cbuf ? c->cb.tiles_x : 0,
-                    c->cb.inline_rec ? c->cb.rec : nullptr};
+                    c->cb.inline_rec ? c->cb.rec : nullptr, c->cb.fixed};
 }
 
 #include "rt_camhost.h"
@@ -1855,7 +1849,14 @@ static int prepare_state(rt_ctx* c, const rt_frame* f, hipStream_t st, bool sync
     }
     if (!capturing) cb_harvest(c->cb);
     const bool need_prep = camera_needs_prepass(c, f, cb_want);
-    const bool need_cb = cb_want && !(cb_matches(c->cb, f) && !need_prep) && (sync_path || cb_async_pays(c, f));
+    // Which build (round 4): a new camera's async frame takes the one-pass
+    // build where it applies (big lists, the analytic tile cone); a
+    // synchronous render, or the camera's next async frame (a static
+    // camera), the sorted lists of cb_build; else cb_build where it pays.
+    const bool current = cb_matches(c->cb, f) && !need_prep;
+    const bool bin = cb_want && !sync_path && !current && cb_bin_ok(c, f);
+    const bool upgrade = cb_want && current && c->cb.fixed && c->opt_camera_buffer != 3;
+    const bool need_cb = bin || upgrade || (cb_want && !current && (sync_path || cb_async_pays(c, f)));
     if (capturing) {
         if (need_prep) {
             c->err = "hipGraph capture: the frame's camera is not prepared (rt_render or rt_prepare_camera first)";
@@ -1872,7 +1873,8 @@ static int prepare_state(rt_ctx* c, const rt_frame* f, hipStream_t st, bool sync
     }
     if (need_cb) {
         const SceneDev S = scene_dev(c, false, false);
-        if (int rc = cb_build(c, c->cb, f, S, st, sync_path, false, true)) return rc;
+        if (int rc = bin ? cb_build_bin(c, c->cb, f, S, st, false) : cb_build(c, c->cb, f, S, st, sync_path, false, true))
+            return rc;
     }
     if (!sync_path) {
         HIP_TRY(c, hipEventRecord(c->ev_state, st));
@@ -1916,10 +1918,11 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
     // tiny scenes: the camera records travel with the launch (no device state)
     TinyCam Tl;
     const TinyCam* tiny = nullptr;
+    bool self = false;  // the camera's first frame on st: the kernel computes the tile masks
     if (tiny_ok(c, depth, lbuf)) {
         Tl = tiny_prepare(c, f);
         if (rows > 0)
-            if (int rc = tiny_masks(c, f, st, capturing, Tl)) return rc;
+            if (int rc = tiny_masks(c, f, st, capturing, Tl, &self)) return rc;
         tiny = &Tl;
     }
     if (rows > 0 && !tiny) {
@@ -1954,7 +1957,7 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
                         : 1;
     if (nch <= 1) {
         if (int rc = launch_trace(c, k, tiny, f->flags & RT_FLAG_STATS, S, F, f->width, rows, rgba_dev, rgb_dev, stats,
-                                  st))
+                                  st, self))
             return rc;
         if (host_out)
             HIP_TRY(c, hipMemcpyAsync(host_out, rgba_dev ? (void*)rgba_dev : (void*)rgb_dev,
@@ -1971,7 +1974,8 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
             Fc.row_end = f->row_begin + r1;
             unsigned* oa = rgba_dev ? rgba_dev + (size_t)r0 * f->width : nullptr;
             float* ob = rgb_dev ? rgb_dev + (size_t)r0 * f->width * 3 : nullptr;
-            if (int rc = launch_trace(c, k, tiny, f->flags & RT_FLAG_STATS, S, Fc, f->width, r1 - r0, oa, ob, stats, st))
+            if (int rc = launch_trace(c, k, tiny, f->flags & RT_FLAG_STATS, S, Fc, f->width, r1 - r0, oa, ob, stats, st,
+                                      self))
                 return rc;
             HIP_TRY(c, hipEventRecord(c->ev_chunk[n], st));
         }
@@ -2153,14 +2157,17 @@ RT_EXPORT int rt_render_sequence_async(rt_ctx* c, const rt_frame* frames, int32_
         // the same image)
         const int nt = ((f->width + 7) / 8) * ((f->height + 7) / 8);
         TinyCam T;
+        bool tself = false;
         const bool tiny = tiny_ok(c, depth, lbuf);
         if (tiny) {
             tiny_build(c, f, T);
-            if (int rc = tiny_masks(c, f, fs, capturing, T, &seq_cap[i % kSeqSlots])) return rc;
+            if (int rc = tiny_masks(c, f, fs, capturing, T, &tself, &seq_cap[i % kSeqSlots])) return rc;
         }
-        const bool cbuf = !tiny && depth == 0 && c->n_tri > 0 && c->opt_camera_buffer && cb_frame_ok(f) &&
-                          cb_async_pays(c, f) &&
-                          (!capturing || (q.cb.cap > 0 && q.cb.rcap > 0 && q.cb.nt_alloc >= nt && q.cb.big_alloc >= c->n_tri));
+        const bool cb_want = !tiny && depth == 0 && c->n_tri > 0 && c->opt_camera_buffer && cb_frame_ok(f);
+        const bool bin = cb_want && cb_bin_ok(c, f) &&
+                         (!capturing || (q.cb.cap >= (size_t)nt * kCbBinK && q.cb.nt_alloc >= nt && q.cb.big_alloc >= c->n_tri));
+        const bool cbuf = bin || (cb_want && cb_async_pays(c, f) &&
+                                  (!capturing || (q.cb.cap > 0 && q.cb.rcap > 0 && q.cb.nt_alloc >= nt && q.cb.big_alloc >= c->n_tri)));
         if (c->n_tri > 0 && !tiny) {
             if (int rc = camera_records(c, f->cam_pos, fs, cbuf, q.tricam, q.cone_cam, q.uni, q.clu_cam)) return rc;
         }
@@ -2172,7 +2179,9 @@ RT_EXPORT int rt_render_sequence_async(rt_ctx* c, const rt_frame* frames, int32_
         S.clu_cam = q.clu_cam;
         S.uni = (q.uni && c->opt_union) ? q.uni : nullptr;
         if (cbuf) {
-            if (int rc = cb_build(c, q.cb, f, S, fs, false, capturing, false)) return rc;
+            if (int rc = bin ? cb_build_bin(c, q.cb, f, S, fs, capturing) : cb_build(c, q.cb, f, S, fs, false, capturing, false))
+                return rc;
+            S.cb_fixed = q.cb.fixed;
             S.cb_off = q.cb.off;
             S.cb_ent = q.cb.ent;
             S.cb_flag = q.cb.flag;
@@ -2183,7 +2192,8 @@ RT_EXPORT int rt_render_sequence_async(rt_ctx* c, const rt_frame* frames, int32_
         frame_dev(f, F);
         unsigned* rgba = rgba8_dev ? (unsigned*)(rgba8_dev + (size_t)i * rgba8_stride) : nullptr;
         float* rgb = rgb_dev ? (float*)((char*)rgb_dev + (size_t)i * rgb_stride) : nullptr;
-        if (int rc = launch_trace(c, k, tiny ? &T : nullptr, false, S, F, f->width, rows, rgba, rgb, c->d_stats, fs))
+        if (int rc = launch_trace(c, k, tiny ? &T : nullptr, false, S, F, f->width, rows, rgba, rgb, c->d_stats, fs,
+                                  tself))
             return rc;
     }
     // Join: st continues after every frame.
@@ -2373,9 +2383,9 @@ RT_EXPORT int rt_debug_cb_verify(rt_ctx* c, unsigned long long* out)
         return RT_E_STATE;
     }
     unsigned* d = nullptr;
-    HIP_TRY(c, hipMalloc((void**)&d, 2 * sizeof(unsigned)));
+    HIP_TRY(c, hipMalloc((void**)&d, 3 * sizeof(unsigned)));
     int rc = RT_OK;
-    if (hipMemset(d, 0, 2 * sizeof(unsigned)) != hipSuccess) rc = RT_E_HIP;
+    if (hipMemset(d, 0, 3 * sizeof(unsigned)) != hipSuccess) rc = RT_E_HIP;
     CbDev D{};
     D.tcone = B.tcone;
     D.off = B.off;
@@ -2386,8 +2396,20 @@ RT_EXPORT int rt_debug_cb_verify(rt_ctx* c, unsigned long long* out)
     D.tiles_x = B.tiles_x;
     D.tiles_y = B.ntiles / std::max(1, B.tiles_x);
     const SceneDev S = scene_dev(c, false, true);
-    unsigned h[2] = {0, 0};
+    unsigned h[3] = {0, 0, 0};
     std::vector<unsigned> flags((size_t)B.ntiles);
+    if (rc == RT_OK && B.fixed) {
+        hipLaunchKernelGGL(rt_cb_verify_bin, dim3((unsigned)((B.ntiles + 3) / 4)), dim3(256), 0, c->stream, S,
+                           B.bin_frame, D, B.bin, d);
+        if (hipGetLastError() != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess ||
+            hipMemcpy(h, d, sizeof h, hipMemcpyDeviceToHost) != hipSuccess)
+            rc = RT_E_HIP;
+        hipFree(d);
+        out[0] = h[0];
+        out[1] = h[1];
+        out[2] = h[2];
+        return rc;
+    }
     if (rc == RT_OK) {
         hipLaunchKernelGGL(rt_cb_verify, dim3((unsigned)((B.ntiles + 3) / 4)), dim3(256), 0, c->stream, S, D, d);
         if (hipGetLastError() != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess ||

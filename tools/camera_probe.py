@@ -74,6 +74,7 @@ def main():
         ctx.render_async(f, dev.data_ptr(), 0, stream)
     torch.cuda.synchronize()
     res["moving_async_ms"] = round((time.perf_counter() - t0) * 1e3 / n, 4)
+    res["same_cameras"] = bench.moving_camera_events(ctx, fr[1:], dev.data_ptr(), stream)
     ring = torch.empty((n, H, W, 4), dtype=torch.uint8, device="cuda")
     path = rt_amd.camera_path(scene.frame, n, yaw_deg=0.25, step=(0.3, 0.0, -0.2))
     ctx.render_sequence_async(path, ring.data_ptr(), H * W * 4, 0, 0, stream)
