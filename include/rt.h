@@ -218,13 +218,12 @@ enum {
     RT_OPT_LIGHT_BUFFER = 1,    /* upload+launch: shadow rays through the light buffer:
                                    1 every depth-0 scene with opaque triangles (default),
                                    2 only above 1,024 triangles, 0 never (wave culling) */
-    RT_OPT_CAMERA_BUFFER = 2,   /* launch: per-camera tile lists: 1 (default) sorted
-                                   lists built by synchronous renders and by an async
-                                   frame repeating its camera; an async / sequence frame
-                                   of a new camera builds the one-pass lists above 1,024
-                                   triangles (else the sorted ones from 4 Mpx of output
-                                   rows); 2 sorted lists by every frame; 3 one-pass lists
-                                   by every async frame of a new camera (tests); 0 never */
+    RT_OPT_CAMERA_BUFFER = 2,   /* launch: per-camera tile lists: 1 (default) built by
+                                   synchronous renders, by an async frame repeating the
+                                   previous async frame's camera, and by async / sequence
+                                   frames of a new camera where the build pays (more than
+                                   1,024 triangles and at least 4 Mpx of output rows);
+                                   2 by every frame; 0 never */
     RT_OPT_UNION_PRETEST = 3,   /* launch: small lists' union cone pre-test, 1 (default) / 0 */
     RT_OPT_LB_SCALE = 4,        /* upload: light-buffer cells per cone radius; 0 = auto (4,
                                    at least 128 cells per face edge; 6 above 1,024

@@ -473,67 +473,6 @@ __global__ __launch_bounds__(256) void rt_cb_pairs(const SceneDev S, CbDev B, co
     }
 }
 
-// ---- the one-pass build (round 4: a moving camera's frame, big lists)
-// Fixed-capacity lists (SceneDev::cb_fixed): tile t's entries at [t K, t K +
-// n_t), n_t = off[t] (n_t > K: the per-wave path).  The tile's cone is the
-// launch-camera path's analytic one (rt_cull.h TinyCam): axis = the
-// direction of the tile's centre pixel (8 tx + 4, 8 ty + 4) clamped to the
-// frame — every pixel of the tile, clamped, lies within 4 pixels of it in
-// each axis — and half-angle wbound, the host's analytic bound on that
-// spread (tile_wbound; used only while uncapped).  So a list holds every
-// triangle a ray of its tile can be reported hitting, and cb_box, which
-// assumes exactly that axis and W <= wbound, holds every tile where the test
-// can pass.  No tile cones, no scans, no count pass: the boxes, then one wave
-// per triangle testing its box's tiles one per lane, each passing pair at an
-// atomic slot of its tile.  The entries come in atomic order, keyed -inf
-// (the walk tests them all: no early exit; the closest hit is order-free).
-struct CbBin {
-    float cosW, sinW, chord;  // the tile cone (wave_cone's rounding: cos down, sin and chord up)
-    unsigned K;               // entries per tile
-};
-
-// The boxes (blocks < nbb, a thread per triangle) and the zeroed counts.
-__global__ __launch_bounds__(256) void rt_cb_bin_boxes(const SceneDev S, const FrameDev F, CbDev B, unsigned nbb)
-{
-    if (blockIdx.x < nbb) {
-        cb_boxes_block(S, F, B, blockIdx.x);
-        return;
-    }
-    const unsigned t = (blockIdx.x - nbb) * 256 + threadIdx.x;
-    if (t < (unsigned)(B.tiles_x * B.tiles_y)) B.off[t] = 0u;
-    if (blockIdx.x == nbb && threadIdx.x < 8) B.stat[threadIdx.x] = 0u;
-}
-
-// One wave per triangle: the tiles of its box, one per lane.
-__global__ __launch_bounds__(256) void rt_cb_bin(const SceneDev S, const FrameDev F, CbDev B, CbBin P)
-{
-    const int lane = (int)(threadIdx.x & 63);
-    const int k = (int)(blockIdx.x * 4 + (threadIdx.x >> 6));
-    if (k >= S.n_tri) return;  // wave-uniform
-    const int4 bx = B.box[k];
-    const unsigned n = (unsigned)bx.w;
-    if (n == 0) return;
-    const float4 c0 = S.cone_cam[2 * k], c1 = S.cone_cam[2 * k + 1];
-    const float4* ep = S.cone_cam + 2 * (size_t)S.n_tri + 3 * (size_t)k;
-    const float4 e[3] = {ep[0], ep[1], ep[2]};
-    WaveCone wc;
-    wc.cosW = P.cosW;
-    wc.sinW = P.sinW;
-    wc.chord = P.chord;
-    wc.ok = true;
-    for (unsigned q = (unsigned)lane; q < n; q += 64) {
-        const int ty = bx.y + (int)(q / (unsigned)bx.z), tx = bx.x + (int)(q % (unsigned)bx.z);
-        if (!cb_tile_row_needed(F, ty)) continue;
-        const int px = tx * 8 + 4, py = ty * 8 + 4;
-        wc.w = camera_dir(F, px < F.width ? px : F.width - 1, py < F.height ? py : F.height - 1);
-        if (cone_overlap(wc, c0, c1.w, 0.0f) && edges_open(wc, e, 0.0f)) {
-            const unsigned t = (unsigned)(ty * B.tiles_x + tx);
-            const unsigned s = atomicAdd(&B.off[t], 1u);
-            if (s < P.K) B.ent[(size_t)t * P.K + s] = make_int2(k, __float_as_int(-INFINITY));
-        }
-    }
-}
-
 // Keys: entry e's key = min dmin over entries [e, end) of its tile, so a
 // wave may stop at the first key beyond its hits.  Lists of up to
 // RT_CB_SORT entries are first sorted nearest-first (the closest hit is
@@ -791,55 +730,6 @@ __global__ __launch_bounds__(256) void rt_cb_verify(const SceneDev S, const CbDe
     }
     if (lane == 0) {
         atomicAdd(&out[1], n);
-        if (bad) atomicAdd(&out[0], 1u);
-    }
-}
-
-// The same for the one-pass build's lists: a tile with a list (n_t <= K)
-// must hold exactly the triangles whose test against the analytic tile cone
-// passes (rt_cb_bin's test, against every triangle: so the boxes missed no
-// passing tile), each once (as many entries as passing triangles, every
-// entry passing), keyed -inf; a tile of a row the frame does not cover, none.
-// out[2] += tiles with a list.
-__global__ __launch_bounds__(256) void rt_cb_verify_bin(const SceneDev S, const FrameDev F, const CbDev B, CbBin P,
-                                                        unsigned* __restrict__ out)
-{
-    const int lane = (int)(threadIdx.x & 63);
-    const int t = (int)(blockIdx.x * 4 + (threadIdx.x >> 6));
-    if (t >= B.tiles_x * B.tiles_y) return;
-    const unsigned m = B.off[t];
-    if (m > P.K) return;
-    const int tx = t % B.tiles_x, ty = t / B.tiles_x;
-    const bool needed = cb_tile_row_needed(F, ty);
-    WaveCone wc;
-    const int px = tx * 8 + 4, py = ty * 8 + 4;
-    wc.w = camera_dir(F, px < F.width ? px : F.width - 1, py < F.height ? py : F.height - 1);
-    wc.cosW = P.cosW;
-    wc.sinW = P.sinW;
-    wc.chord = P.chord;
-    wc.ok = true;
-    auto test = [&](int k) {
-        return cone_overlap(wc, S.cone_cam[2 * k], S.cone_cam[2 * k + 1].w, 0.0f) &&
-               edges_open(wc, S.cone_cam + 2 * (size_t)S.n_tri + 3 * (size_t)k, 0.0f);
-    };
-    unsigned n = 0;
-    for (int k0 = 0; needed && k0 < S.n_tri; k0 += 64) {
-        const int k = k0 + lane;
-        n += (unsigned)__popcll(__ballot(k < S.n_tri && test(k)));
-    }
-    bool bad = m != n;
-    for (unsigned i0 = 0; i0 < m; i0 += 64) {
-        const unsigned i = i0 + (unsigned)lane;
-        bool wrong = false;
-        if (i < m) {
-            const int2 e = B.ent[(size_t)t * P.K + i];
-            wrong = e.x < 0 || e.x >= S.n_tri || e.y != __float_as_int(-INFINITY) || !test(e.x);
-        }
-        bad |= __any(wrong);
-    }
-    if (lane == 0) {
-        atomicAdd(&out[1], n);
-        atomicAdd(&out[2], 1u);
         if (bad) atomicAdd(&out[0], 1u);
     }
 }

@@ -181,8 +181,7 @@ static float tile_wbound(const rt_frame* f, float& cos_wbound, bool* uncapped = 
     return w;
 }
 
-// The analytic tile cone (the launch-camera path's and the one-pass
-// build's): half-angle wbound as wave_cone holds a cone — cos rounded down,
+// The analytic tile cone of the launch-camera path: half-angle wbound as wave_cone holds a cone — cos rounded down,
 // sin and chord (+1e-6 like wave_cone) rounded up.  False when the bound is
 // capped (wide pixels) or the frame is not a rotation camera (cb_frame_ok).
 static bool tile_cone(const rt_frame* f, float& cosW, float& sinW, float& chord)
@@ -518,76 +517,8 @@ static int cb_build(rt_ctx* c, rt_ctx::CamBuf& B, const rt_frame* f, const Scene
     B.tiles_x = tx;
     B.ntiles = nt;
     B.valid = true;
-    B.fixed = 0;
     B.built_cap = B.cap;
     B.built_rcap = B.rcap;
-    B.host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    return RT_OK;
-}
-
-// The one-pass build (rt_cambuf.h rt_cb_bin) of a moving camera's frame:
-// big lists (clusters: the lists' overflow takes the clustered per-wave
-// path), the analytic tile cone within its bound, and t K entry offsets in
-// 32 bits.  RT_OPT_CAMERA_BUFFER 3: for any scene with triangles (tests).
-constexpr unsigned kCbBinK = 64;
-static bool cb_bin_ok(const rt_ctx* c, const rt_frame* f)
-{
-    if (c->opt_camera_buffer != 3 && (c->opt_camera_buffer != 1 || c->n_clu == 0)) return false;
-    float cw, sw, ch;
-    const size_t nt = (size_t)((f->width + 7) / 8) * ((f->height + 7) / 8);
-    return tile_cone(f, cw, sw, ch) && nt * kCbBinK < 0xFFFFFFF0ull;
-}
-
-static int cb_build_bin(rt_ctx* c, rt_ctx::CamBuf& B, const rt_frame* f, const SceneDev& S, hipStream_t st,
-                        bool capturing)
-{
-    const auto t0 = std::chrono::steady_clock::now();
-    const int tx = (f->width + 7) / 8, ty = (f->height + 7) / 8, nt = tx * ty;
-    B.valid = false;
-    if (B.pinned) {  // a captured render reads the current arrays: write fresh ones
-        free_later(c, B.off);
-        free_later(c, B.flag);
-        free_later(c, B.ent);
-        free_later(c, B.rec);
-        B.off = B.flag = nullptr;
-        B.ent = nullptr;
-        B.rec = nullptr;
-        B.nt_alloc = 0;
-        B.cap = B.rec_cap = 0;
-        B.pinned = false;
-    }
-    if (!capturing) cb_harvest(B);
-    if (int rc = cb_ensure(c, B, nt, capturing)) return rc;
-    const size_t want = (size_t)nt * kCbBinK;
-    if (B.cap < want) {
-        if (capturing) return RT_OK;  // no allocation inside a capture: no buffer (the per-wave path)
-        free_later(c, B.ent);
-        B.ent = nullptr;
-        B.cap = 0;
-        if (int rc = cb_grow(c, B, want)) return rc;
-    }
-    CbBin P;
-    tile_cone(f, P.cosW, P.sinW, P.chord);
-    P.K = kCbBinK;
-    FrameDev F;
-    frame_dev(f, F);
-    const CbDev D = cb_dev(B, f);
-    const unsigned nbb = (unsigned)((c->n_tri + 255) / 256);
-    hipLaunchKernelGGL(rt_cb_bin_boxes, dim3(nbb + (unsigned)((nt + 255) / 256)), dim3(256), 0, st, S, F, D, nbb);
-    HIP_TRY(c, hipGetLastError());
-    hipLaunchKernelGGL(rt_cb_bin, dim3((unsigned)((c->n_tri + 3) / 4)), dim3(256), 0, st, S, F, D, P);
-    HIP_TRY(c, hipGetLastError());
-    B.inline_rec = false;
-    cb_key_of(f, B.key);
-    B.tiles_x = tx;
-    B.ntiles = nt;
-    B.valid = true;
-    B.fixed = kCbBinK;
-    B.bin_frame = F;
-    B.bin = P;
-    B.built_cap = B.cap;
-    B.built_rcap = B.rcap;
-    B.timed = false;
     B.host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return RT_OK;
 }

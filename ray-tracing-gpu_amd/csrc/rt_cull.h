@@ -338,8 +338,7 @@ __device__ __forceinline__ int closest_hit_camera_list(const SceneDev& S, int ti
                                     make_float4(b.w, c.x, c.y, 0.f), O, D, t);
         take_min(ok, t, __float_as_int(c.z), bt, bi);
     }
-    const unsigned e0 = S.cb_fixed ? (unsigned)tile * S.cb_fixed : S.cb_off[tile];
-    const unsigned e1 = S.cb_fixed ? e0 + S.cb_off[tile] : S.cb_off[tile + 1];
+    const unsigned e0 = S.cb_off[tile], e1 = S.cb_off[tile + 1];
     if constexpr (INLINE) {
         constexpr unsigned W = kCbLdsW;
         const int lane = (int)(threadIdx.x & 63);
@@ -348,8 +347,10 @@ __device__ __forceinline__ int closest_hit_camera_list(const SceneDev& S, int ti
         for (unsigned w0 = e0; w0 < e1; w0 += W) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
-            if ((unsigned)lane < W && w0 + lane < e1) {
-                float4 a, b, c, d;
+            const bool live = (unsigned)lane < W && w0 + lane < e1;
+            const unsigned n = e1 - w0 < W ? e1 - w0 : W;
+            float4 a, b, c, d;
+            if (live) {
                 if (inl) {
                     const float4* r = S.cb_rec + 4 * (size_t)(w0 + lane);
                     a = r[0];
@@ -365,13 +366,14 @@ __device__ __forceinline__ int closest_hit_camera_list(const SceneDev& S, int ti
                     d = r[3];
                     d.z = __int_as_float(en.y);
                 }
+            }
+            if (live) {
                 win.a[2 * lane] = a;
                 win.a[2 * lane + 1] = b;
                 win.b[2 * lane] = c;
                 win.b[2 * lane + 1] = d;
             }
             wave_lds_sync();
-            const unsigned n = e1 - w0 < W ? e1 - w0 : W;
             bool stop = false;
             for (unsigned j = 0; j < n; ++j) {
                 const float4 d = win.b[2 * j + 1];

@@ -256,7 +256,7 @@ __device__ __forceinline__ void trace_tile(const SceneDev& S, const FrameDev& F,
         int tile = -1;
         if ((WAVE & 8) && S.cb_tiles_x > 0 && (py0 & 7) == 0) {
             tile = (py0 >> 3) * S.cb_tiles_x + tile_x;
-            if (S.cb_fixed ? S.cb_off[tile] > S.cb_fixed : S.cb_flag[tile] != 0) tile = -1;
+            if (S.cb_flag[tile]) tile = -1;
         }
         unsigned tmask = 0;
         if ((WAVE & 32) && (py0 & 7) == 0) tile = (py0 >> 3) * T->tiles_x + tile_x;
@@ -499,11 +499,11 @@ struct rt_ctx {
         bool pinned = false;
         double host_ms = 0.0, build_ms = 0.0;
         bool timed = false;
-        unsigned fixed = 0;         // > 0: the one-pass build's fixed-capacity lists (SceneDev::cb_fixed)
-        FrameDev bin_frame{};       // the one-pass build's frame and tile cone (rt_debug_cb_verify)
-        CbBin bin{};
     };
     CamBuf cb;
+    // the last async frame's camera (cb_key_of): a repeat builds the sorted lists
+    float last_async_key[30] = {};
+    bool last_async_valid = false;
     // Camera state of rt_render_sequence_async: kSeqSlots slots of the
     // per-camera records and camera buffers, apart from the state above;
     // frame i of a sequence uses slot i % kSeqSlots on internal stream
@@ -737,7 +737,7 @@ RT_EXPORT int rt_set_option(rt_ctx* c, int32_t opt, double v)
         c->opt_light_buffer = (int)v;
         return RT_OK;
     case RT_OPT_CAMERA_BUFFER:
-        if (v != 0 && v != 1 && v != 2 && v != 3) return RT_E_ARG;
+        if (v != 0 && v != 1 && v != 2) return RT_E_ARG;
         if ((int)v != c->opt_camera_buffer) c->cb.valid = false;
         c->opt_camera_buffer = (int)v;
         return RT_OK;
@@ -1822,7 +1822,7 @@ static SceneDev scene_dev(rt_ctx* c, bool lbuf, bool cbuf)
                     lbuf ? c->lb_levels : 0, c->d_lb_off, c->d_lb_ent, c->d_lb_dcap, c->d_lb_meta,
                     (c->d_uni && c->opt_union) ? c->d_uni : nullptr,
                     c->cb.off, c->cb.ent, c->cb.flag, cbuf ? c->cb.tiles_x : 0,
-                    c->cb.inline_rec ? c->cb.rec : nullptr, c->cb.fixed};
+                    c->cb.inline_rec ? c->cb.rec : nullptr};
 }
 
 #include "rt_camhost.h"
@@ -1849,14 +1849,19 @@ static int prepare_state(rt_ctx* c, const rt_frame* f, hipStream_t st, bool sync
     }
     if (!capturing) cb_harvest(c->cb);
     const bool need_prep = camera_needs_prepass(c, f, cb_want);
-    // Which build (round 4): a new camera's async frame takes the one-pass
-    // build where it applies (big lists, the analytic tile cone); a
-    // synchronous render, or the camera's next async frame (a static
-    // camera), the sorted lists of cb_build; else cb_build where it pays.
+    // The camera buffer is built by a synchronous render, by an async frame
+    // repeating the previous async frame's camera (round 4: a static camera
+    // rendered async gets its lists at its second frame), and by a new
+    // camera's async frame where the build pays (cb_async_pays).
+    float key[30];
+    cb_key_of(f, key);
+    const bool repeat = !sync_path && c->last_async_valid && std::memcmp(key, c->last_async_key, sizeof key) == 0;
+    if (!sync_path) {
+        std::memcpy(c->last_async_key, key, sizeof key);
+        c->last_async_valid = true;
+    }
     const bool current = cb_matches(c->cb, f) && !need_prep;
-    const bool bin = cb_want && !sync_path && !current && cb_bin_ok(c, f);
-    const bool upgrade = cb_want && current && c->cb.fixed && c->opt_camera_buffer != 3;
-    const bool need_cb = bin || upgrade || (cb_want && !current && (sync_path || cb_async_pays(c, f)));
+    const bool need_cb = cb_want && !current && (sync_path || repeat || cb_async_pays(c, f));
     if (capturing) {
         if (need_prep) {
             c->err = "hipGraph capture: the frame's camera is not prepared (rt_render or rt_prepare_camera first)";
@@ -1873,8 +1878,7 @@ static int prepare_state(rt_ctx* c, const rt_frame* f, hipStream_t st, bool sync
     }
     if (need_cb) {
         const SceneDev S = scene_dev(c, false, false);
-        if (int rc = bin ? cb_build_bin(c, c->cb, f, S, st, false) : cb_build(c, c->cb, f, S, st, sync_path, false, true))
-            return rc;
+        if (int rc = cb_build(c, c->cb, f, S, st, sync_path, false, true)) return rc;
     }
     if (!sync_path) {
         HIP_TRY(c, hipEventRecord(c->ev_state, st));
@@ -2163,11 +2167,9 @@ RT_EXPORT int rt_render_sequence_async(rt_ctx* c, const rt_frame* frames, int32_
             tiny_build(c, f, T);
             if (int rc = tiny_masks(c, f, fs, capturing, T, &tself, &seq_cap[i % kSeqSlots])) return rc;
         }
-        const bool cb_want = !tiny && depth == 0 && c->n_tri > 0 && c->opt_camera_buffer && cb_frame_ok(f);
-        const bool bin = cb_want && cb_bin_ok(c, f) &&
-                         (!capturing || (q.cb.cap >= (size_t)nt * kCbBinK && q.cb.nt_alloc >= nt && q.cb.big_alloc >= c->n_tri));
-        const bool cbuf = bin || (cb_want && cb_async_pays(c, f) &&
-                                  (!capturing || (q.cb.cap > 0 && q.cb.rcap > 0 && q.cb.nt_alloc >= nt && q.cb.big_alloc >= c->n_tri)));
+        const bool cbuf = !tiny && depth == 0 && c->n_tri > 0 && c->opt_camera_buffer && cb_frame_ok(f) &&
+                          cb_async_pays(c, f) &&
+                          (!capturing || (q.cb.cap > 0 && q.cb.rcap > 0 && q.cb.nt_alloc >= nt && q.cb.big_alloc >= c->n_tri));
         if (c->n_tri > 0 && !tiny) {
             if (int rc = camera_records(c, f->cam_pos, fs, cbuf, q.tricam, q.cone_cam, q.uni, q.clu_cam)) return rc;
         }
@@ -2179,9 +2181,7 @@ RT_EXPORT int rt_render_sequence_async(rt_ctx* c, const rt_frame* frames, int32_
         S.clu_cam = q.clu_cam;
         S.uni = (q.uni && c->opt_union) ? q.uni : nullptr;
         if (cbuf) {
-            if (int rc = bin ? cb_build_bin(c, q.cb, f, S, fs, capturing) : cb_build(c, q.cb, f, S, fs, false, capturing, false))
-                return rc;
-            S.cb_fixed = q.cb.fixed;
+            if (int rc = cb_build(c, q.cb, f, S, fs, false, capturing, false)) return rc;
             S.cb_off = q.cb.off;
             S.cb_ent = q.cb.ent;
             S.cb_flag = q.cb.flag;
@@ -2383,9 +2383,9 @@ RT_EXPORT int rt_debug_cb_verify(rt_ctx* c, unsigned long long* out)
         return RT_E_STATE;
     }
     unsigned* d = nullptr;
-    HIP_TRY(c, hipMalloc((void**)&d, 3 * sizeof(unsigned)));
+    HIP_TRY(c, hipMalloc((void**)&d, 2 * sizeof(unsigned)));
     int rc = RT_OK;
-    if (hipMemset(d, 0, 3 * sizeof(unsigned)) != hipSuccess) rc = RT_E_HIP;
+    if (hipMemset(d, 0, 2 * sizeof(unsigned)) != hipSuccess) rc = RT_E_HIP;
     CbDev D{};
     D.tcone = B.tcone;
     D.off = B.off;
@@ -2396,20 +2396,8 @@ RT_EXPORT int rt_debug_cb_verify(rt_ctx* c, unsigned long long* out)
     D.tiles_x = B.tiles_x;
     D.tiles_y = B.ntiles / std::max(1, B.tiles_x);
     const SceneDev S = scene_dev(c, false, true);
-    unsigned h[3] = {0, 0, 0};
+    unsigned h[2] = {0, 0};
     std::vector<unsigned> flags((size_t)B.ntiles);
-    if (rc == RT_OK && B.fixed) {
-        hipLaunchKernelGGL(rt_cb_verify_bin, dim3((unsigned)((B.ntiles + 3) / 4)), dim3(256), 0, c->stream, S,
-                           B.bin_frame, D, B.bin, d);
-        if (hipGetLastError() != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess ||
-            hipMemcpy(h, d, sizeof h, hipMemcpyDeviceToHost) != hipSuccess)
-            rc = RT_E_HIP;
-        hipFree(d);
-        out[0] = h[0];
-        out[1] = h[1];
-        out[2] = h[2];
-        return rc;
-    }
     if (rc == RT_OK) {
         hipLaunchKernelGGL(rt_cb_verify, dim3((unsigned)((B.ntiles + 3) / 4)), dim3(256), 0, c->stream, S, D, d);
         if (hipGetLastError() != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess ||

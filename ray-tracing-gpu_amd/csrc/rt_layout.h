@@ -121,11 +121,6 @@ struct SceneDev {
     // the records' extra bytes cost more: C5 +3%, against C3 -4 to -5%).
     // Walked inline by the big-list kernel only (small lists: no gain).
     const float4* __restrict__ cb_rec;
-    // Fixed-capacity lists (the one-pass build of a moving camera, rt_cb_bin):
-    // cb_fixed = K > 0: tile t's entries at [t K, t K + cb_off[t]) in any
-    // order, keyed -inf (the walk tests them all); cb_off[t] > K: no list
-    // (the per-wave path; cb_flag unused).  0: the offsets layout above.
-    unsigned cb_fixed;
 };
 
 struct FrameDev {

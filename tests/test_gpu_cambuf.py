@@ -63,54 +63,6 @@ def test_lists_equal_brute_force(heightfield_path, which, w, h):
     ctx.close()
 
 
-@pytest.mark.parametrize("which,w,h", [("scene2", 640, 360), ("scene2", 333, 197), ("hf", 640, 360), ("hf", 250, 131),
-                                       ("hf", 1920, 1080)])
-def test_one_pass_lists_equal_brute_force(heightfield_path, which, w, h):
-    """The one-pass build (rt_cb_bin, a new camera's async frame) for every
-    camera of the set: each tile's list is exactly the triangles passing the
-    analytic tile-cone test — against every triangle, so the boxes missed
-    no passing tile — and the frame is the per-wave path's."""
-    path = heightfield_path if which == "hf" else scene(int(which[-1]))
-    s = rt_amd.Scene(path, w, h, 0)
-    ctx = rt_amd.Context(0, camera_buffer=3, launch_camera=0)
-    ctx.upload(s)
-    ref = rt_amd.Context(0, camera_buffer=0, launch_camera=0)
-    ref.upload(s)
-    st = torch.cuda.current_stream()
-    for i, f in enumerate(cameras.cameras(s.frame)):
-        o = torch.empty((h, w, 3), dtype=torch.float32, device="cuda")
-        ctx.render_async(f, 0, o.data_ptr(), st.cuda_stream)
-        torch.cuda.synchronize()
-        bad, pairs, listed = _verify(ctx)
-        assert bad == 0, (i, bad, pairs, listed)
-        assert bits_equal(o.cpu().numpy(), ref.render_float(f)), i
-    ctx.close()
-    ref.close()
-
-
-@pytest.mark.parametrize("rows,bands", [((40, 176), None), (None, (16, 3, 1))])
-def test_one_pass_partial_frame_lists(heightfield_path, rows, bands):
-    s = rt_amd.Scene(heightfield_path, 480, 270, 0)
-    ctx = rt_amd.Context(0, camera_buffer=3)
-    ctx.upload(s)
-    ref = rt_amd.Context(0, camera_buffer=0)
-    ref.upload(s)
-    f = cameras.turned(s.frame, cameras.rot(1, 5.0), (1.0, 0.0, 1.0))
-    if rows:
-        f.row_begin, f.row_end = rows
-    if bands:
-        f.band_rows, f.band_count, f.band_index = bands
-    want = ref.render_float(f)
-    o = torch.empty(want.shape, dtype=torch.float32, device="cuda")
-    ctx.render_async(f, 0, o.data_ptr(), torch.cuda.current_stream().cuda_stream)
-    torch.cuda.synchronize()
-    bad, pairs, listed = _verify(ctx)
-    assert bad == 0 and listed > 0, (bad, listed)
-    assert bits_equal(o.cpu().numpy(), want)
-    ctx.close()
-    ref.close()
-
-
 @pytest.mark.parametrize("rows,bands", [((40, 176), None), (None, (16, 3, 1))])
 def test_partial_frame_lists_equal_brute_force(heightfield_path, rows, bands):
     s = rt_amd.Scene(heightfield_path, 480, 270, 0)
@@ -143,15 +95,12 @@ def test_moved_cameras_equal_reference(heightfield_path, which, lc, kind):
 
 
 @pytest.mark.parametrize("which,cbopt,lc", [("scene2", 1, 1), ("scene2", 1, 0), ("scene2", 2, 0), ("hf", 2, 1),
-                                           ("hf", 1, 1), ("scene7", 1, 1), ("scene9", 1, 1), ("hf", 3, 1),
-                                           ("scene2", 3, 0)])
+                                           ("hf", 1, 1), ("scene7", 1, 1), ("scene9", 1, 1)])
 def test_async_moving_camera_matches_reference(heightfield_path, which, cbopt, lc):
     """rt_render_async of a camera path, no host sync between frames: each
     new camera's records travel with the launch (scene2, lc 1), or its device
     state (and, with camera_buffer 2 or where it pays, its camera buffer) is
-    built on the caller's stream — the one-pass lists of a new camera (hf at
-    camera_buffer 1, anything at 3) or the sorted ones (2); every frame is
-    the reference's."""
+    built on the caller's stream; every frame is the reference's."""
     r = CamRef(which, heightfield_path)
     frames = r.frames["path"]
     ctx = rt_amd.Context(0, camera_buffer=cbopt, launch_camera=lc)
@@ -168,9 +117,6 @@ def test_async_moving_camera_matches_reference(heightfield_path, which, cbopt, l
         assert info[1] > 0  # the last camera's buffer, built by the async render
         if info[0] == 1.0:
             assert _verify(ctx)[0] == 0
-    if cbopt == 3 and r.depth == 0:
-        bad, pairs, listed = _verify(ctx)  # the last camera's one-pass lists
-        assert bad == 0 and listed > 0 and pairs > 0
     for i, o in enumerate(outs):
         assert r.matches(o.cpu().numpy(), "path", i), (which, i)
     ctx.close()
@@ -211,8 +157,7 @@ def test_non_rotation_orientation_renders_without_buffer():
     b.close()
 
 
-@pytest.mark.parametrize("which,cbopt,lc", [("hf", 1, 1), ("hf", 2, 1), ("scene2", 2, 0), ("scene2", 1, 1),
-                                           ("hf", 3, 1), ("scene2", 3, 0)])
+@pytest.mark.parametrize("which,cbopt,lc", [("hf", 1, 1), ("hf", 2, 1), ("scene2", 2, 0), ("scene2", 1, 1)])
 def test_sequence_slots_build_camera_buffers(heightfield_path, which, cbopt, lc):
     r = CamRef(which, heightfield_path)
     frames = r.frames["path"]
@@ -234,7 +179,7 @@ def test_async_two_streams_interleaved(heightfield_path, cbopt):
     """Renders of alternating and repeated cameras on two streams, with no
     host sync between calls and a synchronous render in the middle: every
     output is the reference's frame of its camera (camera_buffer 1: a new
-    camera's one-pass lists, replaced by the sorted ones at its repeat)."""
+    camera per-wave, its repeat on the same stream building the lists)."""
     r = CamRef("hf", heightfield_path)
     cams = r.frames["path"][:4]
     ctx = rt_amd.Context(0, camera_buffer=cbopt)

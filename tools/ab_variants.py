@@ -7,6 +7,8 @@ RTLD_LOCAL so their identical symbol names do not collide.
 A variant may carry context options (rt_set_option, names as in
 rt_amd.OPTIONS) set before its upload, e.g. lib/librt_amd.so@lb_scale=2
 (several: @a=1,b=2; the far light-buffer ladder as far=6:64).
+--moving: each round renders a path of moved cameras (a new camera every
+frame, as bench.py's moving-camera leg) instead of the static camera.
 """
 import argparse
 import ctypes
@@ -40,6 +42,7 @@ def main():
     ap.add_argument("--config", default="c2")
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--frames", type=int, default=10)
+    ap.add_argument("--moving", action="store_true")
     ap.add_argument("libs", nargs="+")
     a = ap.parse_args()
     name, W, H, depth = bench.CONFIGS[a.config]
@@ -79,19 +82,28 @@ def main():
         img = out.clone()
         same = True if ref is None else bool(torch.equal(img, ref))
         ref = img if ref is None else ref
-        vs.append(dict(lib=os.path.basename(lp) + ("@" + envs if envs else ""), L=L, ctx=ctx, fr=fr, sc=sc, times=[], same_as_first=same))
+        path_frames = []
+        for k in range(a.frames):
+            f = rt_amd.Frame()
+            ctypes.pointer(f)[0] = fr
+            f.cam_pos[0] -= 0.29 * (k + 1)
+            f.cam_pos[2] += 0.17 * (k + 1)
+            path_frames.append(f)
+        vs.append(dict(lib=os.path.basename(lp) + ("@" + envs if envs else ""), L=L, ctx=ctx, fr=fr, sc=sc, times=[],
+                       same_as_first=same, path=path_frames))
     for _ in range(a.rounds):
         for v in vs:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            for _ in range(a.frames):
-                v["L"].rt_render_async(v["ctx"], ctypes.byref(v["fr"]), out.data_ptr(), None, None)
+            for k in range(a.frames):
+                f = v["path"][k] if a.moving else v["fr"]
+                v["L"].rt_render_async(v["ctx"], ctypes.byref(f), out.data_ptr(), None, None)
             e1.record()
             torch.cuda.synchronize()
             v["times"].append(e0.elapsed_time(e1) / a.frames)
     res = [{"lib": v["lib"], "median_ms": round(statistics.median(v["times"]), 4),
             "min_ms": round(min(v["times"]), 4), "identical_output": v["same_as_first"]} for v in vs]
-    print(json.dumps({"config": a.config, "results": res}))
+    print(json.dumps({"config": a.config, "moving": a.moving, "results": res}))
 
 
 if __name__ == "__main__":
