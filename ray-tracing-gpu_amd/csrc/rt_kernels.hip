@@ -201,9 +201,17 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
 #ifndef RT_WAVES_PER_EU_BIG
 #define RT_WAVES_PER_EU_BIG 7
 #endif
+#ifndef RT_WAVES_PER_EU_TINY
+#define RT_WAVES_PER_EU_TINY 7
+#endif
+#ifndef RT_TINY_HOIST
+#define RT_TINY_HOIST 1
+#endif
 constexpr int waves_per_eu(int maxd, int wave)
 {
-    return maxd != 0 ? 1 : ((wave & 15) == 14 ? RT_WAVES_PER_EU_BIG : RT_WAVES_PER_EU);
+    return maxd != 0 ? 1
+                     : ((wave & 32) ? RT_WAVES_PER_EU_TINY
+                                    : ((wave & 15) == 14 ? RT_WAVES_PER_EU_BIG : RT_WAVES_PER_EU));
 }
 // One 8 x 8 tile (the body of both trace kernels below).
 // COUNT: also tally the exact tests executed (the RT_FLAG_STATS launch); in
@@ -241,7 +249,7 @@ __device__ __forceinline__ void trace_tile(const SceneDev& S, const FrameDev& F,
 #endif
     Color c{0.f, 0.f, 0.f};
     TinyLane tl;
-    if constexpr ((WAVE & 64) != 0) tl = tiny_lane_load(*T);  // the mask's records, in flight under the set-up
+    if constexpr ((WAVE & 64) != 0 && RT_TINY_HOIST) tl = tiny_lane_load(*T);  // the mask's records, in flight under the set-up
     // Without bounces every lane runs (lanes outside the frame on a clamped
     // pixel, result dropped) so edge waves stay whole for wave-level culling.
     if (MAXD == 0 || valid) {
@@ -260,6 +268,7 @@ __device__ __forceinline__ void trace_tile(const SceneDev& S, const FrameDev& F,
         }
         unsigned tmask = 0;
         if ((WAVE & 32) && (py0 & 7) == 0) tile = (py0 >> 3) * T->tiles_x + tile_x;
+        if constexpr ((WAVE & 64) != 0 && !RT_TINY_HOIST) tl = tiny_lane_load(*T);
         if constexpr ((WAVE & 64) != 0) tmask = tiny_tile_mask(*T, tl, D);
         c = radiance<MAXD, LB, WAVE>(S, F, O, D, cnt, valid, tile, T, tmask);
         if (valid) {
