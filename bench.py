@@ -682,7 +682,14 @@ def main():
                                        "157.3 TF with packed FMA; no dense contraction, so no MFMA instructions",
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
                          "frac_vs_nofma_issue_peak": round(achieved / PEAK_NOFMA_TOPS, 4),
-                         "flops_per_launch": int(flops), "kernel": f"rt_trace_kernel<{st.stack_depth},{st.light_batch}>",
+                         "flops_per_launch": int(flops),
+                         # depth-0 frames of 1..20-triangle scenes take the launch-camera kernel
+                         # (RT_OPT_LAUNCH_CAMERA, on by default; its camera's first frame on a
+                         # stream the mask-computing variant <0,1,101>, later ones <0,1,37>)
+                         "kernel": (f"rt_trace_tiny<0,{st.light_batch},37>"
+                                    if st.stack_depth == 0 and 0 < int(np.sum(types == 0)) <= 20
+                                    and not ctx_opts.get("launch_camera", 1) == 0
+                                    else f"rt_trace_kernel<{st.stack_depth},{st.light_batch}>"),
                          "work": "exact ray-primitive tests executed (after culling) x SURVEY 8(d) ops + set-up + shading",
                          "tests_executed": int(run_tests), "tests_brute_force": int(brute_tests),
                          "brute_force_equiv_tflops": round(brute / (kernel_ms * 1e-3) / 1e12, 3)},

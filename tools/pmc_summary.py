@@ -14,14 +14,23 @@ import sys
 from collections import defaultdict
 
 
-def main(d="gpurun_out/pmc", kernel="rt_trace_kernel"):
+def main(d="gpurun_out/pmc", kernel="rt::rt_trace_"):
     out = {}
     for f in sorted(glob.glob(f"{d}/*counter_collection.csv")):
         rows = [r for r in csv.DictReader(open(f)) if kernel in r["Kernel_Name"]]
         # the timed launches only: the non-counting instantiation (COUNT =
         # false) over the whole frame — not the counted launch, nor the row
         # chunks of synchronous renders into host memory (RT_OPT_HOST_CHUNK_MB)
+        # — of the kernel dispatched most (rt_trace_kernel, or the launch-camera
+        # rt_trace_tiny<.., 37, ..> after its camera's first, mask-computing frame)
         timed = [r for r in rows if "false>" in r["Kernel_Name"]] or rows
+        names = defaultdict(int)
+        for r in timed:
+            names[r["Kernel_Name"]] += 1
+        if names:
+            top = max(names, key=names.get)
+            timed = [r for r in timed if r["Kernel_Name"] == top]
+            out["kernel"] = top.split("(")[0]
         grid = max((int(r["Grid_Size"]) for r in timed), default=0)
         per = defaultdict(list)
         for r in timed:
