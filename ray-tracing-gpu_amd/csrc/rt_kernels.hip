@@ -201,8 +201,13 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
 #ifndef RT_WAVES_PER_EU_BIG
 #define RT_WAVES_PER_EU_BIG 7
 #endif
+// The launch-camera kernel that computes its tile masks (WAVE bit 64) is
+// held to 64 VGPRs, 8 waves/SIMD (A/B, moving C2 camera: -2.3% against 7;
+// the mask-reading kernel fits 58 VGPRs anyway, and asked for 8 measured
+// +2.4% static).  RT_TINY_HOIST: its mask planes are loaded at the top of
+// the kernel (A/B: -2.7% against loading them where the mask is computed).
 #ifndef RT_WAVES_PER_EU_TINY
-#define RT_WAVES_PER_EU_TINY 7
+#define RT_WAVES_PER_EU_TINY 8
 #endif
 #ifndef RT_TINY_HOIST
 #define RT_TINY_HOIST 1
@@ -210,7 +215,7 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
 constexpr int waves_per_eu(int maxd, int wave)
 {
     return maxd != 0 ? 1
-                     : ((wave & 32) ? RT_WAVES_PER_EU_TINY
+                     : ((wave & 64) ? RT_WAVES_PER_EU_TINY
                                     : ((wave & 15) == 14 ? RT_WAVES_PER_EU_BIG : RT_WAVES_PER_EU));
 }
 // One 8 x 8 tile (the body of both trace kernels below).
