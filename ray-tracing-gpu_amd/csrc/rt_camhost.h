@@ -295,40 +295,22 @@ static const TinyCam& tiny_prepare(rt_ctx* c, const rt_frame* f)
     return c->tiny;
 }
 
-// Tile masks of the launch-camera path, one buffer per stream (launches on
-// one stream run in order, so a stream's masks are rewritten only after its
-// earlier renders read them).  A camera's first frame on a stream computes
-// them in the trace kernel (*self = true: the WAVE bit 64 variant stores
-// each tile's mask); its later frames read them.  A hipGraph capture cannot
-// allocate: it takes a buffer of its own from a pool kept filled by
-// uncaptured calls and always computes (its replays recompute in place; the
-// buffer is retired, freed at the next upload) — or, with the pool empty,
-// renders unmasked (the same image).  *cap_buf: a capture's buffer shared by
-// the frames of one sequence call on one internal stream (nullptr: one per
-// launch).  Sets T.mask.
-constexpr int kMaskPool = 8;
-static int tiny_masks(rt_ctx* c, const rt_frame* f, hipStream_t st, bool capturing, TinyCam& T, bool* self,
-                      unsigned** cap_buf = nullptr)
+// Tile masks of the launch-camera path (*mode, the trace kernel's: 0 read
+// the stream's stored masks, 1 compute them in the kernel, 2 compute and
+// store them).  One buffer per stream: launches on one stream run in order,
+// so a stream's masks are rewritten only after its earlier renders read
+// them.  A camera's first frame on a stream computes its masks without
+// storing them — a moving camera never reads them back, and the store cost
+// a moving C2 frame 7% (A/B) —, its next frame on the stream computes and
+// stores them, its later frames read them.  A hipGraph capture computes them
+// (its replays recompute: no buffer).  Sets T.mask.
+static int tiny_masks(rt_ctx* c, const rt_frame* f, hipStream_t st, bool capturing, TinyCam& T, int* mode)
 {
-    *self = false;
-    if (!T.masked) return RT_OK;
+    *mode = 0;
+    if (!T.masked) return RT_OK;  // every listed triangle
+    *mode = 1;
+    if (capturing) return RT_OK;
     const size_t nt = (size_t)T.tiles_x * T.tiles_y;
-    if (capturing) {
-        unsigned* d = cap_buf ? *cap_buf : nullptr;
-        if (!d) {
-            if (c->mask_pool.empty() || c->mask_pool_nt < nt) {
-                T.masked = 0;  // no buffer to spare inside a capture: every listed triangle
-                return RT_OK;
-            }
-            d = c->mask_pool.back();
-            c->mask_pool.pop_back();
-            c->retired.push_back(d);
-            if (cap_buf) *cap_buf = d;
-        }
-        T.mask = d;
-        *self = true;
-        return RT_OK;
-    }
     rt_ctx::MaskBuf* b = nullptr;
     for (auto& q : c->tiny_masks)
         if (q.stream == st) b = &q;
@@ -339,7 +321,17 @@ static int tiny_masks(rt_ctx* c, const rt_frame* f, hipStream_t st, bool capturi
     }
     float key[30];
     cb_key_of(f, key);
-    if (b->cap < nt) {
+    if (b->valid && b->cap >= nt && std::memcmp(key, b->key, sizeof key) == 0) {
+        T.mask = b->d;
+        *mode = 0;
+        return RT_OK;
+    }
+    if (!b->pend_valid || std::memcmp(key, b->pend, sizeof key) != 0) {
+        std::memcpy(b->pend, key, sizeof key);  // a new camera: compute only
+        b->pend_valid = true;
+        return RT_OK;
+    }
+    if (b->cap < nt) {  // the camera's second frame: compute and store
         if (b->d) free_later(c, b->d);
         b->d = nullptr;
         b->cap = 0;
@@ -347,23 +339,11 @@ static int tiny_masks(rt_ctx* c, const rt_frame* f, hipStream_t st, bool capturi
         HIP_TRY(c, hipMalloc((void**)&b->d, nt * sizeof(unsigned)));
         b->cap = nt;
     }
+    std::memcpy(b->key, key, sizeof key);
+    b->valid = true;
+    b->pend_valid = false;
     T.mask = b->d;
-    if (!b->valid || std::memcmp(key, b->key, sizeof key) != 0) {
-        *self = true;
-        std::memcpy(b->key, key, sizeof key);
-        b->valid = true;
-    }
-    // the capture pool, sized for this frame
-    if (c->mask_pool_nt < nt) {
-        for (unsigned* d : c->mask_pool) free_later(c, d);
-        c->mask_pool.clear();
-        c->mask_pool_nt = nt;
-    }
-    while ((int)c->mask_pool.size() < kMaskPool) {
-        unsigned* d = nullptr;
-        HIP_TRY(c, hipMalloc((void**)&d, nt * sizeof(unsigned)));
-        c->mask_pool.push_back(d);
-    }
+    *mode = 2;
     return RT_OK;
 }
 

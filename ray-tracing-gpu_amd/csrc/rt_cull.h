@@ -424,10 +424,11 @@ __device__ __forceinline__ int closest_hit_camera_list(const SceneDev& S, int ti
 // axis), half-angle = wbound, the analytic bound on that spread (the host's
 // tile_wbound).  That is the camera buffer's test with the tile's measured
 // cone replaced by a provably wider one, so the kept set holds every
-// triangle any ray of the tile can be reported hitting.  The first frame of
-// a camera on a stream (WAVE bit 64) computes each tile's mask in the trace
-// kernel itself — lane j tests triangle j, one ballot — and stores it; later
-// frames of that camera on that stream read it (one scalar load).
+// triangle any ray of the tile can be reported hitting.  A camera's first two
+// frames on a stream (WAVE bit 64) compute each tile's mask in the trace
+// kernel itself — lane j tests triangle j, one ballot —, the second also
+// stores it (bit 128, rt_camhost.h tiny_masks); its later frames on that
+// stream read it (one scalar load).
 constexpr int kTinyMax = 20;
 struct TinyCam {
     int n;       // listed triangles (never-hit ones left out)
@@ -453,11 +454,17 @@ struct TinyCam {
 struct TinyLane {
     float4 q[4];  // planes (0, 1) and (2, 3) paired: [x0 x1 y0 y1] [z0 z1 w0 w1] [x2 x3 y2 y3] [z2 z3 w2 w3]
 };
+// Only the lanes of listed triangles load (each wave reads n x 64 B through
+// its CU's L1, not 64 x 64 B: A/B -1.4% on a moving C2 camera).
 __device__ __forceinline__ TinyLane tiny_lane_load(const TinyCam& T)
 {
     const int lane = (int)(threadIdx.x & 63);
-    const float4* r = T.rec + 8 * (lane < kTinyMax ? lane : kTinyMax - 1);
-    return TinyLane{{r[0], r[1], r[2], r[3]}};
+    TinyLane L{};
+    if (lane < T.n) {
+        const float4* r = T.rec + 8 * lane;
+        L = TinyLane{{r[0], r[1], r[2], r[3]}};
+    }
+    return L;
 }
 __device__ __forceinline__ unsigned tiny_tile_mask(const TinyCam& T, const TinyLane& L, const Vec3 D)
 {
@@ -478,8 +485,8 @@ __device__ __forceinline__ unsigned tiny_tile_mask(const TinyCam& T, const TinyL
 // first, then the tile's kept triangles nearest first (tile < 0 or no masks:
 // every listed triangle), leaving once every lane holds a hit nearer than
 // the next dmin (t >= dmin > best: no later triangle can win or tie).
-// SELF: the wave computed the tile's mask (tmask, tiny_tile_mask); store it
-// for the camera's later frames.
+// SELF: the wave computed the tile's mask (tmask, tiny_tile_mask); else it
+// reads the stored one.
 template <bool SELF>
 __device__ __forceinline__ int closest_hit_camera_tiny(const SceneDev& S, const TinyCam& T, int tile, unsigned tmask,
                                                        const Vec3 O, const Vec3 D, float& best_t, Counters& cnt)
@@ -488,7 +495,6 @@ __device__ __forceinline__ int closest_hit_camera_tiny(const SceneDev& S, const 
     if (T.masked && tile >= 0) {
         if constexpr (SELF) {
             m = tmask;
-            if ((threadIdx.x & 63) == 0) T.mask[tile] = m;
         } else {
             m = T.mask[tile];  // wave-uniform (scalar) load
         }

@@ -296,6 +296,11 @@ __device__ __forceinline__ void trace_tile(const SceneDev& S, const FrameDev& F,
                 else rgba[o] = px8;
             }
         }
+        // the tile's mask for its camera's later frames on this stream (WAVE
+        // bit 128), stored last: at the top of the kernel the store's
+        // completion held up the loads behind it (A/B: C2 -2.8%, C4 -2.5%)
+        if constexpr ((WAVE & 128) != 0)
+            if (lane == 0 && T->masked && tile >= 0) T->mask[tile] = tmask;
     }
 #ifdef RT_PROF
     RT_MARK(cnt, 6);
@@ -559,12 +564,12 @@ struct rt_ctx {
         hipStream_t stream = nullptr;
         unsigned* d = nullptr;
         size_t cap = 0;
-        float key[30] = {};
+        float key[30] = {};   // the camera whose masks d holds (valid)
         bool valid = false;
+        float pend[30] = {};  // the camera of the stream's last computing frame (pend_valid)
+        bool pend_valid = false;
     };
     std::vector<MaskBuf> tiny_masks;  // per stream
-    std::vector<unsigned*> mask_pool;  // spare mask buffers for hipGraph captures
-    size_t mask_pool_nt = 0;
     bool tricam_all = false;  // tricam holds every triangle for cam_key
     StatsDev* d_stats = nullptr;
     void* d_scratch = nullptr;  // staging for host outputs
@@ -868,7 +873,6 @@ RT_EXPORT void rt_destroy(rt_ctx* c)
     hipFree(c->d_lb_meta);
     hipFree(c->d_uni);
     for (auto& q : c->tiny_masks) hipFree(q.d);
-    for (unsigned* d : c->mask_pool) hipFree(d);
     cb_free(c->cb);
     for (auto& q : c->seq) {
         hipFree(q.tricam);
@@ -1462,7 +1466,7 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
     nrm.resize(std::max<size_t>(nrm.size(), 4));
     coef.resize(std::max<size_t>(coef.size(), 4));
     c->tiny_valid = false;
-    for (auto& q : c->tiny_masks) q.valid = false;  // the masks of the old scene's triangles
+    for (auto& q : c->tiny_masks) q.valid = q.pend_valid = false;  // the old scene's triangles
     if (ntr > 0 && ntr <= (size_t)kTinyMax) {  // the launch-camera path's host records
         auto f4 = [](const std::vector<float>& v, size_t n) {
             std::vector<float4> o(n);
@@ -1703,15 +1707,17 @@ static void trace_dims(kernel_fn k, int width, int rows, dim3& grid, dim3& block
 // launch's records, light-buffer shadows, one light per pass); SELF: the
 // camera's first frame on the stream, which computes and stores the masks.
 template <bool COUNT>
-static const void* tiny_kernel(bool self)
+static const void* tiny_kernel(int mode)
 {
-    return self ? (const void*)&rt_trace_tiny<0, 1, 101, COUNT> : (const void*)&rt_trace_tiny<0, 1, 37, COUNT>;
+    return mode == 2   ? (const void*)&rt_trace_tiny<0, 1, 229, COUNT>
+           : mode == 1 ? (const void*)&rt_trace_tiny<0, 1, 101, COUNT>
+                       : (const void*)&rt_trace_tiny<0, 1, 37, COUNT>;
 }
 
 // One trace launch over `rows` output rows (T: the launch-camera kernel with
 // its records, else kernel k).
 static int launch_trace(rt_ctx* c, kernel_fn k, const TinyCam* T, bool count, SceneDev& S, FrameDev& F, int width,
-                        int rows, unsigned* oa, float* ob, StatsDev* stats, hipStream_t st, bool self = false)
+                        int rows, unsigned* oa, float* ob, StatsDev* stats, hipStream_t st, int mode = 0)
 {
     dim3 grid, block;
     unsigned lds = 0;
@@ -1719,7 +1725,7 @@ static int launch_trace(rt_ctx* c, kernel_fn k, const TinyCam* T, bool count, Sc
     if (T) {
         TinyCam Tv = *T;
         void* args[] = {&S, &F, &Tv, &oa, &ob, &stats};
-        HIP_TRY(c, hipLaunchKernel(count ? tiny_kernel<true>(self) : tiny_kernel<false>(self), grid, block, args, 0, st));
+        HIP_TRY(c, hipLaunchKernel(count ? tiny_kernel<true>(mode) : tiny_kernel<false>(mode), grid, block, args, 0, st));
         return RT_OK;
     }
     void* args[] = {&S, &F, &oa, &ob, &stats};
@@ -1936,11 +1942,11 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
     // tiny scenes: the camera records travel with the launch (no device state)
     TinyCam Tl;
     const TinyCam* tiny = nullptr;
-    bool self = false;  // the camera's first frame on st: the kernel computes the tile masks
+    int tmode = 0;  // the tile masks: 0 read, 1 computed by the kernel, 2 computed and stored (tiny_masks)
     if (tiny_ok(c, depth, lbuf)) {
         Tl = tiny_prepare(c, f);
         if (rows > 0)
-            if (int rc = tiny_masks(c, f, st, capturing, Tl, &self)) return rc;
+            if (int rc = tiny_masks(c, f, st, capturing, Tl, &tmode)) return rc;
         tiny = &Tl;
     }
     if (rows > 0 && !tiny) {
@@ -1975,7 +1981,7 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
                         : 1;
     if (nch <= 1) {
         if (int rc = launch_trace(c, k, tiny, f->flags & RT_FLAG_STATS, S, F, f->width, rows, rgba_dev, rgb_dev, stats,
-                                  st, self))
+                                  st, tmode))
             return rc;
         if (host_out)
             HIP_TRY(c, hipMemcpyAsync(host_out, rgba_dev ? (void*)rgba_dev : (void*)rgb_dev,
@@ -1993,7 +1999,7 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
             unsigned* oa = rgba_dev ? rgba_dev + (size_t)r0 * f->width : nullptr;
             float* ob = rgb_dev ? rgb_dev + (size_t)r0 * f->width * 3 : nullptr;
             if (int rc = launch_trace(c, k, tiny, f->flags & RT_FLAG_STATS, S, Fc, f->width, r1 - r0, oa, ob, stats, st,
-                                      self))
+                                      tmode))
                 return rc;
             HIP_TRY(c, hipEventRecord(c->ev_chunk[n], st));
         }
@@ -2161,7 +2167,6 @@ RT_EXPORT int rt_render_sequence_async(rt_ctx* c, const rt_frame* frames, int32_
         HIP_TRY(c, hipEventRecord(c->seq_fork, st));
         for (int j = 0; j < nstreams; ++j) HIP_TRY(c, hipStreamWaitEvent(c->seq_streams[j], c->seq_fork, 0));
     }
-    unsigned* seq_cap[kSeqSlots] = {};  // a capture's mask buffer per internal stream
     for (int i = 0; i < n; ++i) {
         const rt_frame* f = frames + i;
         rt_ctx::CamSlot& q = c->seq[i % kSeqSlots];
@@ -2175,11 +2180,11 @@ RT_EXPORT int rt_render_sequence_async(rt_ctx* c, const rt_frame* frames, int32_
         // the same image)
         const int nt = ((f->width + 7) / 8) * ((f->height + 7) / 8);
         TinyCam T;
-        bool tself = false;
+        int tmode = 0;
         const bool tiny = tiny_ok(c, depth, lbuf);
         if (tiny) {
             tiny_build(c, f, T);
-            if (int rc = tiny_masks(c, f, fs, capturing, T, &tself, &seq_cap[i % kSeqSlots])) return rc;
+            if (int rc = tiny_masks(c, f, fs, capturing, T, &tmode)) return rc;
         }
         const bool cbuf = !tiny && depth == 0 && c->n_tri > 0 && c->opt_camera_buffer && cb_frame_ok(f) &&
                           cb_async_pays(c, f) &&
@@ -2207,7 +2212,7 @@ RT_EXPORT int rt_render_sequence_async(rt_ctx* c, const rt_frame* frames, int32_
         unsigned* rgba = rgba8_dev ? (unsigned*)(rgba8_dev + (size_t)i * rgba8_stride) : nullptr;
         float* rgb = rgb_dev ? (float*)((char*)rgb_dev + (size_t)i * rgb_stride) : nullptr;
         if (int rc = launch_trace(c, k, tiny ? &T : nullptr, false, S, F, f->width, rows, rgba, rgb, c->d_stats, fs,
-                                  tself))
+                                  tmode))
             return rc;
     }
     // Join: st continues after every frame.
