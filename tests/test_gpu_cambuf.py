@@ -278,3 +278,61 @@ def test_candidate_pairs_past_32_bits(tmp_path):
     assert bits_equal(ctx.render_float(f), ref.render_float(f))
     ctx.close()
     ref.close()
+
+
+def test_launch_camera_mask_modes_on_one_stream(heightfield_path):
+    """The launch-camera path's three mask modes on one stream (rt_camhost.h
+    tiny_masks): camera A's first frame computes its tile masks, its second
+    computes and stores them, its third reads them; a new camera B computes
+    without storing, so A's stored masks stay valid and A's next frame reads
+    them; B's second frame then overwrites them with B's.  Every frame is the
+    reference's (scene2 moved cameras, RGBA8 and float RGB)."""
+    r = CamRef("scene2", heightfield_path)
+    cams = r.frames["cams"]
+    order = [0, 0, 0, 1, 0, 0, 1, 1, 1, 0]
+    ctx = rt_amd.Context(0, launch_camera=1)
+    ctx.upload(r.scene)
+    st = torch.cuda.Stream()
+    outs = []
+    with torch.cuda.stream(st):
+        for i, k in enumerate(order):
+            if i % 2:
+                o = torch.empty((r.h, r.w, 4), dtype=torch.uint8, device="cuda")
+                ctx.render_async(cams[k], o.data_ptr(), 0, st.cuda_stream)
+            else:
+                o = torch.empty((r.h, r.w, 3), dtype=torch.float32, device="cuda")
+                ctx.render_async(cams[k], 0, o.data_ptr(), st.cuda_stream)
+            outs.append((k, o))
+    st.synchronize()
+    for i, (k, o) in enumerate(outs):
+        assert r.matches(o.cpu().numpy(), "cams", k), (i, k)
+    ctx.close()
+
+
+@pytest.mark.parametrize("kind", ["cams", "path"])
+def test_async_repeat_builds_the_sorted_lists(heightfield_path, kind):
+    """An async frame repeating the previous async frame's camera builds the
+    camera buffer (the heightfield at 480x270 is below the 4 Mpx at which a
+    new camera's async frame builds it): after each camera's second frame the
+    buffer is that camera's and equals brute force, and every frame is the
+    reference's."""
+    r = CamRef("hf", heightfield_path)
+    ctx = rt_amd.Context(0)
+    ctx.upload(r.scene)
+    # synchronous renders first: they read each build's size back, so the
+    # capacity fits every camera (an async build that overflows is flagged
+    # and rebuilt at its camera's next frame, by design)
+    for i, f in enumerate(r.frames[kind][:4]):
+        assert r.matches(ctx.render_float(f), kind, i), i
+    st = torch.cuda.current_stream()
+    for i, f in enumerate(r.frames[kind][:4]):
+        for rep in range(2):
+            o = torch.empty((r.h, r.w, 3), dtype=torch.float32, device="cuda")
+            ctx.render_async(f, 0, o.data_ptr(), st.cuda_stream)
+            torch.cuda.synchronize()
+            assert r.matches(o.cpu().numpy(), kind, i), (i, rep)
+        info = _cb_info(ctx)
+        assert info[0] == 1.0, i  # built by the repeat
+        bad, pairs, listed = _verify(ctx)
+        assert bad == 0 and listed > 0, (i, bad)
+    ctx.close()
