@@ -242,14 +242,16 @@ enum {
                                    0 (default) = sized from earlier builds' totals.  A
                                    tile whose list does not fit renders by the per-wave
                                    path (tests: a small value exercises that path) */
-    RT_OPT_LAUNCH_CAMERA = 12   /* launch (ABI 6): depth-0 frames of scenes of 1-32
+    RT_OPT_LAUNCH_CAMERA = 12   /* launch (ABI 6): depth-0 frames of scenes of 1-20
                                    triangles with light-buffer shadows take their camera
                                    records with the kernel launch — per-triangle camera
-                                   values, nearest-hit bounds and screen boxes computed on
-                                   the host per camera — so no camera prepass, camera
-                                   buffer or other per-camera device state exists and a
-                                   moving camera renders like a static one: 1 (default) /
-                                   0 (the device camera buffer) */
+                                   values, nearest-hit bounds and tile-mask planes
+                                   computed on the host per camera; the trace kernel
+                                   computes its tile masks (stored per stream from a
+                                   camera's second frame) — so no camera prepass or
+                                   camera buffer exists and a moving camera renders
+                                   like a static one: 1 (default) / 0 (the device
+                                   camera buffer) */
     /* 9-11 (ABI 5: the async camera-state ring, the bounce lane-refill kernel,
        compact light-buffer entries) were measured slower or no faster and are
        removed in ABI 6: rt_set_option returns RT_E_ARG for them.  Their code
