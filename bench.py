@@ -376,6 +376,25 @@ def moving_camera_events(ctx, frames, dst, stream, repeats=3):
                     "camera's first frame vs the same camera's next frames"}
 
 
+def spawn_ranks(n: int) -> int:
+    """`bench.py --gpus N` run bare: start the N ranks (one process per GPU)
+    with torch.distributed.run as a child process — never an exec: this
+    process has not touched the GPU and stays the parent — on a free local
+    port, the same arguments forwarded; rank 0's JSON line goes straight to
+    our stdout.  Returns the launcher's exit code."""
+    import socket
+    import subprocess
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "1")  # the launcher's default; silences its warning
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -411,11 +430,32 @@ def main():
     args = ap.parse_args()
     ctx_opts = {k: float(v) for k, v in (o.split("=", 1) for o in args.option)}
 
+    # --gpus N is the number of ranks.  Launched bare (no WORLD_SIZE), N > 1
+    # starts N ranks itself — torch.distributed.run as a CHILD process, before
+    # this process touches torch or the GPU — and exits with its code (rank 0
+    # prints the JSON line).  Under a launcher the world must be N.
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:
+            sys.exit(spawn_ranks(args.gpus))
+    elif int(os.environ["WORLD_SIZE"]) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}: refusing to report "
+              f"{os.environ['WORLD_SIZE']} rank(s) as {args.gpus} GPU(s)", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if args.gpus < 1:
+        print("bench.py: --gpus must be >= 1", file=sys.stderr, flush=True)
+        sys.exit(2)
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import numpy as np
     import torch
+
+    if world > 1 and args.dist_backend == "nccl" and world > torch.cuda.device_count():
+        # RCCL needs one GPU per rank ("Duplicate GPU detected"); gloo ranks may share one
+        print(f"bench.py: {world} RCCL ranks but {torch.cuda.device_count()} visible GPU(s); use "
+              f"--dist-backend gloo to share GPUs", file=sys.stderr, flush=True)
+        sys.exit(2)
 
     # one GPU per rank (ranks beyond the visible GPUs share them: gloo only)
     device = local % max(1, torch.cuda.device_count())
@@ -429,6 +469,21 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", device))
         else:
             dist.init_process_group("gloo")
+    ranks_seen, gpus_used = 1, 1
+    if use_dist:
+        # the ranks that joined the collective: one all-reduce of a 1 per rank
+        one = torch.ones(1, dtype=torch.float64, device="cuda" if args.dist_backend == "nccl" else "cpu")
+        dist.all_reduce(one)
+        ranks_seen = int(one.item())
+        if ranks_seen != world or dist.get_world_size() != world:
+            print(f"bench.py: {ranks_seen} ranks joined the all-reduce, WORLD_SIZE={world}", file=sys.stderr,
+                  flush=True)
+            sys.exit(2)
+        # distinct GPUs the ranks render on (gloo ranks may share one)
+        used = torch.zeros(max(1, torch.cuda.device_count()), dtype=torch.float64, device=one.device)
+        used[device] = 1.0
+        dist.all_reduce(used, op=dist.ReduceOp.MAX)
+        gpus_used = int(used.sum().item())
     import rt_amd
 
     name, W, H, depth = CONFIGS[args.config]
@@ -639,6 +694,8 @@ def main():
             "value": round(value, 3),
             "unit": "Mray/s",
             "n_gpus": world,
+            "ranks_seen": ranks_seen,
+            "gpus_used": gpus_used,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms, 4),

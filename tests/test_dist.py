@@ -157,3 +157,28 @@ def test_band_layout_covers_frame():
                 # band sets tile the frame's bands exactly once
                 assert all(band_rows(h, br, world, r) <= rows for r in range(world))
                 assert sum(band_rows(h, br, world, r) for r in range(world)) == -(-h // br) * br
+
+
+# ---- bench.py's --gpus contract, before any GPU call
+def _bench_rc(args, extra_env):
+    import subprocess
+    import sys
+
+    from conftest import REPO
+
+    env = dict(os.environ, **extra_env)
+    return subprocess.run([sys.executable, "bench.py"] + args, cwd=REPO, capture_output=True, text=True,
+                          timeout=120, env=env)
+
+
+def test_bench_refuses_world_size_other_than_gpus():
+    r = _bench_rc(["--gpus", "1", "--steps", "1"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode == 2
+    assert "WORLD_SIZE=2" in r.stderr and '{"metric"' not in r.stdout
+    r = _bench_rc(["--gpus", "8", "--steps", "1"], {"WORLD_SIZE": "4", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode == 2
+
+
+def test_bench_refuses_zero_gpus():
+    r = _bench_rc(["--gpus", "0"], {})
+    assert r.returncode == 2

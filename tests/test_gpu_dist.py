@@ -59,7 +59,7 @@ def one_rank():
     (3, "slabs", 3, 4), (2, "slabs", 1, 4)])
 def test_scene2_ranks_match_reference_digest(one_rank, digests, n, partition, gather_batch, gather_channels):
     out = _bench(n, "c2", partition, gather_batch, gather_channels)
-    assert out["n_gpus"] == n
+    assert out["n_gpus"] == out["ranks_seen"] == n
     assert out["frame_rgba8_sha256"] == one_rank["c2"]["frame_rgba8_sha256"]
     # scene2 has no reflective/refractive surface: depth 3 renders the depth-0 image
     assert out["frame_rgba8_sha256"] == digests["scene2_1920x1080_d0_rgba8_sha256"]
@@ -67,6 +67,43 @@ def test_scene2_ranks_match_reference_digest(one_rank, digests, n, partition, ga
     want = "row-band16" if partition == "bands" else ("row-slab" if partition == "slabs" else None)
     if want:
         assert out["config"]["parallelism"].startswith(want)
+
+
+def _bare(args, timeout=240):
+    """bench.py started the way the driver may start it — no launcher."""
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    return subprocess.run([sys.executable, "bench.py"] + args, cwd=REPO, capture_output=True, text=True,
+                          timeout=timeout, env=env)
+
+
+def test_bare_bench_gpus_n_runs_n_ranks(one_rank, digests):
+    """`bench.py --gpus 2` without a launcher starts the
+    two ranks itself (torch.distributed.run as a child) — here sharing the
+    one GPU over gloo — and the line proves both joined the collective."""
+    r = _bare(["--gpus", "2", "--dist-backend", "gloo", "--frame-sha", "--steps", "3", "--warmup", "1",
+               "--config", "c2", "--no-cpu-baseline", "--no-host-boundary"])
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith('{"metric"')]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == out["ranks_seen"] == 2
+    assert out["gpus_used"] == 1  # both gloo ranks on the box's one GPU
+    assert out["frame_rgba8_sha256"] == digests["scene2_1920x1080_d0_rgba8_sha256"]
+    assert out["frame_rgba8_sha256"] == one_rank["c2"]["frame_rgba8_sha256"]
+
+
+def test_bare_bench_refuses_more_rccl_ranks_than_gpus():
+    """Two RCCL ranks on a one-GPU box: refused with a message, non-zero."""
+    import torch
+
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("more than one GPU visible")
+    r = _bare(["--gpus", "2", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--no-host-boundary"])
+    assert r.returncode != 0
+    assert "visible GPU" in r.stderr
+    assert '{"metric"' not in r.stdout
 
 
 @pytest.mark.parametrize("n", [2, 3])
