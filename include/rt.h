@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 6
+#define RT_ABI_VERSION 7
 
 enum {
     RT_OK = 0,
@@ -113,6 +113,13 @@ typedef struct rt_stats {
     uint64_t triangle_tests;
     uint64_t plane_tests;
     uint64_t quadric_tests;
+    /* ABI 7: bounce rays (reflected / refracted, Scene.cpp:1779-1823): their
+       exact triangle tests (part of triangle_tests; brute force: every
+       triangle per ray) and the BVH inner nodes they visited (RT_OPT_BVH)  */
+    uint64_t bounce_triangle_tests;
+    uint64_t bvh_nodes_visited;
+    char kernel[48];       /* the trace kernel that ran, e.g.
+                              "rt_trace_tiny<0,1,37>"                        */
 } rt_stats;
 
 /* ------------------------------------------------------------ host scene */
@@ -242,6 +249,16 @@ enum {
                                    0 (default) = sized from earlier builds' totals.  A
                                    tile whose list does not fit renders by the per-wave
                                    path (tests: a small value exercises that path) */
+    RT_OPT_BVH = 13,            /* launch (ABI 7): bounce rays of scenes with at least
+                                   64 triangles and a reflective or refractive surface
+                                   walk the exact BVH built at upload (rt_bvh.h), with
+                                   the depth-0 kernels' camera buffer and light-buffer
+                                   shadows: 1 (default) / 0 (every triangle per bounce ray) */
+    RT_OPT_WAVEFRONT = 14,      /* launch (ABI 7): such frames (RT_OPT_BVH) render their
+                                   bounce levels as compacted queues in HBM, one launch
+                                   per level then a fold per level (up to 8 levels,
+                                   not inside a hipGraph capture or a sequence): 1
+                                   (default) / 0 (one kernel, a per-lane DFS stack) */
     RT_OPT_LAUNCH_CAMERA = 12   /* launch (ABI 6): depth-0 frames of scenes of 1-20
                                    triangles with light-buffer shadows take their camera
                                    records with the kernel launch — per-triangle camera

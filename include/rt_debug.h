@@ -47,6 +47,18 @@ int rt_debug_upload_info(rt_ctx*, double* out, int n);
  * mod 2^32; *total = the 64-bit total. */
 int rt_debug_scan(int device, const unsigned* in, unsigned n, unsigned* out, unsigned long long* total);
 
+/* ABI 7: the bounce-ray BVH of the uploaded scene (rt_bvh.h): out[0] built
+ * (0/1), out[1] inner nodes, out[2] leaves, out[3] depth (deepest leaf's
+ * inner-node path), out[4] host build ms. */
+int rt_debug_bvh_info(rt_ctx*, double* out, int n);
+
+/* Bounce-ray closest hits of n arbitrary rays (rays: O.xyz D.xyz per ray),
+ * each through the BVH and through every triangle (planes and quadrics
+ * too, both ways; synchronous): out_idx / out_t (2 per ray) = [BVH, brute
+ * force] winners (file index or -1, t); tally2 = the BVH walk's triangle
+ * tests and inner nodes visited, summed.  RT_E_STATE without a BVH. */
+int rt_debug_bvh_rays(rt_ctx*, const float* rays, int n, int* out_idx, float* out_t, unsigned long long* tally2);
+
 /* Run the wave-primitive self-test (wave min / max / sum, wave cones) over
  * `blocks` workgroups on `device`; *failures = lanes that disagreed. */
 int rt_debug_selftest(int device, int blocks, unsigned* failures);

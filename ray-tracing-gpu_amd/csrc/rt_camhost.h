@@ -304,6 +304,12 @@ static const TinyCam& tiny_prepare(rt_ctx* c, const rt_frame* f)
 // a moving C2 frame 7% (A/B) —, its next frame on the stream computes and
 // stores them, its later frames read them.  A hipGraph capture computes them
 // (its replays recompute: no buffer).  Sets T.mask.
+// Buffers are found by the stream's handle, which a destroyed stream's
+// successor may reuse: the storing kernel is followed by an event
+// (tiny_masks_stored) that a reader waits for while it has not passed.  At
+// most kMaskBufs buffers: the least recently used one is dropped (freed at
+// the next host sync).
+constexpr size_t kMaskBufs = 16;
 static int tiny_masks(rt_ctx* c, const rt_frame* f, hipStream_t st, bool capturing, TinyCam& T, int* mode)
 {
     *mode = 0;
@@ -315,13 +321,27 @@ static int tiny_masks(rt_ctx* c, const rt_frame* f, hipStream_t st, bool capturi
     for (auto& q : c->tiny_masks)
         if (q.stream == st) b = &q;
     if (!b) {
+        if (c->tiny_masks.size() >= kMaskBufs) {
+            auto lru = std::min_element(c->tiny_masks.begin(), c->tiny_masks.end(),
+                                        [](const rt_ctx::MaskBuf& x, const rt_ctx::MaskBuf& y) { return x.used < y.used; });
+            if (lru->d) free_later(c, lru->d);
+            if (lru->ev) HIP_TRY(c, hipEventDestroy(lru->ev));  // (released once it has passed)
+            c->tiny_masks.erase(lru);
+        }
         c->tiny_masks.push_back(rt_ctx::MaskBuf{});
         b = &c->tiny_masks.back();
         b->stream = st;
     }
+    b->used = ++c->mask_clock;
     float key[30];
     cb_key_of(f, key);
     if (b->valid && b->cap >= nt && std::memcmp(key, b->key, sizeof key) == 0) {
+        if (b->ev_set) {
+            const hipError_t q = hipEventQuery(b->ev);
+            if (q == hipErrorNotReady) HIP_TRY(c, hipStreamWaitEvent(st, b->ev, 0));
+            else if (q == hipSuccess) b->ev_set = false;
+            else return hip_fail(c, q, "hipEventQuery");
+        }
         T.mask = b->d;
         *mode = 0;
         return RT_OK;
@@ -344,6 +364,18 @@ static int tiny_masks(rt_ctx* c, const rt_frame* f, hipStream_t st, bool capturi
     b->pend_valid = false;
     T.mask = b->d;
     *mode = 2;
+    return RT_OK;
+}
+
+// After the kernel that stored stream st's masks (mode 2): their event.
+static int tiny_masks_stored(rt_ctx* c, hipStream_t st)
+{
+    for (auto& q : c->tiny_masks)
+        if (q.stream == st) {
+            if (!q.ev) HIP_TRY(c, hipEventCreateWithFlags(&q.ev, hipEventDisableTiming));
+            HIP_TRY(c, hipEventRecord(q.ev, st));
+            q.ev_set = true;
+        }
     return RT_OK;
 }
 
@@ -441,8 +473,11 @@ static int cb_build(rt_ctx* c, rt_ctx::CamBuf& B, const rt_frame* f, const Scene
     if (exact_first) {  // the pass masks sized to the candidate pairs (one read back)
         HIP_TRY(c, hipMemcpyAsync(B.h_tot, ptot, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
         HIP_TRY(c, hipStreamSynchronize(st));
-        const size_t pairs = (size_t)std::min<unsigned long long>(B.h_tot[0], 0xFFFFFFFFull);
-        B.observed_pairs = std::max(B.observed_pairs, pairs);
+        // past 2^32 - 1 pairs the pass tests none and flags every tile (the
+        // per-wave path): no masks to size, nothing to remember (as cb_harvest)
+        const bool over = B.h_tot[0] > 0xFFFFFFFFull;
+        const size_t pairs = over ? 0 : (size_t)B.h_tot[0];
+        if (!over) B.observed_pairs = std::max(B.observed_pairs, pairs);
         const size_t runs = (pairs + 63) / 64 + 1024;
         if (runs > B.rcap) {
             free_later(c, B.rmask);

@@ -42,6 +42,8 @@
 #include "rt_cpu.hpp"
 #include "rt_scan.h"
 #include "rt_shade.h"
+#include "rt_bvh.h"
+#include "rt_wavefront.h"
 
 #pragma clang fp contract(off)
 
@@ -62,9 +64,12 @@ struct Refr {
     float rior, energy;
 };
 
+// WAVE bit 512 (MAXD 0, the wavefront's level 0, rt_wavefront.h): a hit
+// that spawns children writes a node record and its child rays instead of
+// its colour (deferred: rt_wf_fold writes the pixel).
 template <int MAXD, int LB, int WAVE>
 __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, Counters& cnt, bool live, int tile,
-                          const TinyCam* T, unsigned tmask = 0)
+                          const TinyCam* T, unsigned tmask, unsigned pix, bool& deferred)
 {
     const Color bg{F.bg[0], F.bg[1], F.bg[2]};
     if constexpr (MAXD == 0) {
@@ -91,6 +96,7 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
         }
         const Vec3 P = O + t * D;
         const Color c = shade_local<LB, WAVE>(S, m, P, N, D, cnt, hit & live);
+        if constexpr ((WAVE & 512) != 0) deferred = wf_children(F, 0, hit & live, m, P, N, D, 1.0f, 1.0f, c, pix);
         return hit ? c : bg;
     } else {
         Frame stk[MAXD];
@@ -102,8 +108,13 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
         for (;;) {
             if (trace) {
                 float t;
-                const int idx = camera_ray ? closest_hit_primary<(WAVE & 107)>(S, O, D, t, cnt, tile, T)
-                                           : closest_hit<false>(S, O, D, t, cnt);
+                int idx;
+                if (camera_ray)
+                    idx = closest_hit_primary<(WAVE & 107)>(S, O, D, t, cnt, tile, T);
+                else if constexpr ((WAVE & 256) != 0)  // bounce rays through the BVH (rt_bvh.h)
+                    idx = closest_hit_bvh(S, O, D, t, cnt);
+                else
+                    idx = closest_hit<false>(S, O, D, t, cnt);
                 camera_ray = false;
                 ret = bg;
                 if (idx >= 0) {
@@ -275,9 +286,10 @@ __device__ __forceinline__ void trace_tile(const SceneDev& S, const FrameDev& F,
         if ((WAVE & 32) && (py0 & 7) == 0) tile = (py0 >> 3) * T->tiles_x + tile_x;
         if constexpr ((WAVE & 64) != 0 && !RT_TINY_HOIST) tl = tiny_lane_load(*T);
         if constexpr ((WAVE & 64) != 0) tmask = tiny_tile_mask(*T, tl, D);
-        c = radiance<MAXD, LB, WAVE>(S, F, O, D, cnt, valid, tile, T, tmask);
-        if (valid) {
-            const size_t o = (size_t)ly * F.width + px;
+        const size_t o = (size_t)ly * F.width + px;
+        bool deferred = false;
+        c = radiance<MAXD, LB, WAVE>(S, F, O, D, cnt, valid, tile, T, tmask, (unsigned)o, deferred);
+        if (valid & !deferred) {
             if (rgbf) {
                 rgbf[3 * o] = c.r;
                 rgbf[3 * o + 1] = c.g;
@@ -325,22 +337,20 @@ __device__ __forceinline__ void trace_tile(const SceneDev& S, const FrameDev& F,
     // Only the COUNT variant (the RT_FLAG_STATS launch, pick_kernel) tallies:
     // in the timed kernels every counter is dead code.
     if (COUNT && (F.flags & RT_FLAG_STATS)) {
-        unsigned long long v[7] = {cnt.primary, cnt.bounce, cnt.shadow, cnt.skipped, cnt.tri, cnt.pla, cnt.qua};
+        unsigned long long v[9] = {cnt.primary, cnt.bounce, cnt.shadow, cnt.skipped, cnt.tri,
+                                   cnt.pla,     cnt.qua,    cnt.btri,   cnt.bnode};
         StatsDev* sl = stats + ((blockIdx.x + blockIdx.y * gridDim.x) % kStatSlots);
-        unsigned long long* dst[7] = {&sl->primary, &sl->bounce, &sl->shadow, &sl->skipped,
-                                      &sl->tri, &sl->pla, &sl->qua};
-        const int nv = 7;
+        unsigned long long* dst[9] = {&sl->primary, &sl->bounce, &sl->shadow, &sl->skipped, &sl->tri,
+                                      &sl->pla,     &sl->qua,    &sl->btri,   &sl->bnode};
         if (wave_full()) {  // one atomic per counter per wave
 #pragma unroll
-            for (int i = 0; i < 7; ++i)
-                if (i < nv) {
-                    const unsigned long long w = wave_sum_u64(v[i]);
-                    if ((threadIdx.x & 63) == 0) atomicAdd(dst[i], w);
-                }
+            for (int i = 0; i < 9; ++i) {
+                const unsigned long long w = wave_sum_u64(v[i]);
+                if ((threadIdx.x & 63) == 0) atomicAdd(dst[i], w);
+            }
         } else {
 #pragma unroll
-            for (int i = 0; i < 7; ++i)
-                if (i < nv) atomicAdd(dst[i], v[i]);
+            for (int i = 0; i < 9; ++i) atomicAdd(dst[i], v[i]);
         }
     }
 }
@@ -437,6 +447,30 @@ __global__ void rt_selftest_kernel(unsigned seed, unsigned* __restrict__ fails)
     if (wc.ok && live) bad |= dot(d, wc.w) < wc.cosW;
     if (bad) atomicAdd(fails, 1u);
     (void)lane;
+}
+
+// Bounce-ray closest hits of arbitrary rays (rt_debug_bvh_rays): lane i
+// takes ray i (O, D: 6 floats) through the BVH and through every triangle;
+// out_idx / out_t get both winners (file index, t) as [bvh, brute].
+__global__ __launch_bounds__(64) void rt_bvh_rays_kernel(const SceneDev S, const float* __restrict__ rays, int n,
+                                                           int* __restrict__ out_idx, float* __restrict__ out_t,
+                                                           unsigned long long* __restrict__ tally)
+{
+    const int i = (int)(blockIdx.x * 64 + threadIdx.x);
+    if (i >= n) return;
+    const float* r = rays + 6 * (size_t)i;
+    const Vec3 O = make3(r[0], r[1], r[2]), D = make3(r[3], r[4], r[5]);
+    Counters cnt;
+    float tb, tf;
+    const int ib = closest_hit_bvh(S, O, D, tb, cnt);
+    const unsigned tests = cnt.btri, nodes = cnt.bnode;
+    const int jf = closest_hit<false>(S, O, D, tf, cnt);
+    out_idx[2 * i] = ib;
+    out_idx[2 * i + 1] = jf;
+    out_t[2 * i] = tb;
+    out_t[2 * i + 1] = tf;
+    atomicAdd(&tally[0], (unsigned long long)tests);
+    atomicAdd(&tally[1], (unsigned long long)nodes);
 }
 
 }  // namespace rt
@@ -568,8 +602,14 @@ struct rt_ctx {
         bool valid = false;
         float pend[30] = {};  // the camera of the stream's last computing frame (pend_valid)
         bool pend_valid = false;
+        // after the kernel that stored d (a reader on a stream that only
+        // shares this one's handle — a destroyed stream's successor — waits)
+        hipEvent_t ev = nullptr;
+        bool ev_set = false;
+        unsigned long long used = 0;  // last use (LRU eviction)
     };
-    std::vector<MaskBuf> tiny_masks;  // per stream
+    std::vector<MaskBuf> tiny_masks;  // per stream, at most kMaskBufs
+    unsigned long long mask_clock = 0;
     bool tricam_all = false;  // tricam holds every triangle for cam_key
     StatsDev* d_stats = nullptr;
     void* d_scratch = nullptr;  // staging for host outputs
@@ -605,6 +645,27 @@ struct rt_ctx {
     int n_tri_opaque = 0, n_plane_opaque = 0, n_quad_opaque = 0, n_translucent = 0;
     int shadow_split = 0;
     float k_max = 0.0f;         // max(Kr, Kt) over surfaces (NaN ignored)
+    // bounce-ray BVH (rt_bvh.h, built at upload for scenes that can bounce)
+    float4* d_bvh_node = nullptr;
+    float4* d_bvh_tri = nullptr;
+    int bvh_inner = 0, bvh_leaves = 0, bvh_depth = 0;
+    double bvh_build_ms = 0.0;
+    bool opt_bvh = true;        // RT_OPT_BVH
+    // Wavefront bounce queues (rt_wavefront.h), grown on demand; one set per
+    // context: a wavefront frame on another stream than the last one's waits
+    // for that frame (ev_wf) before it reuses them.
+    struct WfBuf {
+        void* mem = nullptr;      // one allocation: counters, then every level's arrays
+        size_t bytes = 0;
+        size_t px = 0;            // pixel capacity (level-0 nodes)
+        size_t cap[kWfMaxLevels + 1] = {};  // ray capacity per level
+        WfDev dev{};
+        hipEvent_t ev = nullptr;  // after the last wavefront frame
+        hipStream_t last = nullptr;
+        bool pending = false;
+    } wf;
+    int opt_wavefront = 1;      // RT_OPT_WAVEFRONT
+    float kr_max = 0.0f, kt_max = 0.0f;  // max Kr, max Kt over surfaces
     bool uploaded = false;
     rt_stats last{};
     std::string err;
@@ -722,6 +783,7 @@ static int sync_all(rt_ctx* c)
     c->async_streams.clear();
     c->state_pending = false;
     c->state_stream = nullptr;
+    c->wf.pending = false;
     free_deferred(c);
     return RT_OK;
 }
@@ -780,6 +842,8 @@ RT_EXPORT int rt_set_option(rt_ctx* c, int32_t opt, double v)
         c->opt_host_chunk_mb = v;
         return RT_OK;
     case RT_OPT_LAUNCH_CAMERA: c->opt_launch_camera = v != 0; return RT_OK;
+    case RT_OPT_BVH: c->opt_bvh = v != 0; return RT_OK;
+    case RT_OPT_WAVEFRONT: c->opt_wavefront = v != 0; return RT_OK;
     case RT_OPT_CB_CAPACITY:
         if (v < 0 || v > 4e9 || v != std::floor(v)) return RT_E_ARG;
         if (v != c->opt_cb_capacity) c->cb.valid = false;
@@ -802,6 +866,8 @@ RT_EXPORT int rt_get_option(rt_ctx* c, int32_t opt, double* v)
     case RT_OPT_HOST_CHUNK_MB: *v = c->opt_host_chunk_mb; return RT_OK;
     case RT_OPT_CB_CAPACITY: *v = c->opt_cb_capacity; return RT_OK;
     case RT_OPT_LAUNCH_CAMERA: *v = c->opt_launch_camera ? 1 : 0; return RT_OK;
+    case RT_OPT_BVH: *v = c->opt_bvh ? 1 : 0; return RT_OK;
+    case RT_OPT_WAVEFRONT: *v = c->opt_wavefront; return RT_OK;
     default: return RT_E_ARG;
     }
 }
@@ -872,7 +938,14 @@ RT_EXPORT void rt_destroy(rt_ctx* c)
     hipFree(c->d_lb_dcap);
     hipFree(c->d_lb_meta);
     hipFree(c->d_uni);
-    for (auto& q : c->tiny_masks) hipFree(q.d);
+    hipFree(c->d_bvh_node);
+    hipFree(c->d_bvh_tri);
+    hipFree(c->wf.mem);
+    if (c->wf.ev) hipEventDestroy(c->wf.ev);
+    for (auto& q : c->tiny_masks) {
+        hipFree(q.d);
+        if (q.ev) hipEventDestroy(q.ev);
+    }
     cb_free(c->cb);
     for (auto& q : c->seq) {
         hipFree(q.tricam);
@@ -903,6 +976,13 @@ RT_EXPORT void rt_destroy(rt_ctx* c)
 }
 
 static bool nonneg_finite(float v) { return std::isfinite(v) && !std::signbit(v); }
+
+#include "rt_bvhhost.h"
+// Bounce rays walk the BVH (rt_bvh.h) in scenes of at least this many
+// triangles (fewer: every triangle, by wave-uniform scalar loads).
+#ifndef RT_BVH_MIN_TRIANGLES
+#define RT_BVH_MIN_TRIANGLES 64
+#endif
 
 // 256 camera records = 16 KB, the scalar data cache.
 static constexpr int kTricamMaxTriangles = 256;
@@ -1283,7 +1363,7 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
     std::vector<float> geom((size_t)std::max(n, 1) * 16, 0.0f), mat((size_t)std::max(n, 1) * 12, 0.0f),
         lig((size_t)std::max(nl, 1) * 8, 0.0f);
     bool opaque = true;
-    float kmax = 0.0f;
+    float kmax = 0.0f, krmax = 0.0f, ktmax = 0.0f;
     for (int i = 0; i < n; ++i) {
         const float* g = s->geom + 12 * (size_t)i;
         const float* m = s->material + 10 * (size_t)i;
@@ -1316,6 +1396,8 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
         for (int k = 0; k < 10; ++k) q[k] = m[k];
         if (m[7] > kmax) kmax = m[7];
         if (m[8] > kmax) kmax = m[8];
+        if (m[7] > krmax) krmax = m[7];
+        if (m[8] > ktmax) ktmax = m[8];
     }
     // Per-kind arrays, opaque surfaces first (file order kept inside each class).
     auto opaque_at = [&](int i) {
@@ -1395,6 +1477,11 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
     c->lb_entries = 0;
     hipFree(c->d_uni);
     c->d_uni = nullptr;
+    hipFree(c->d_bvh_node);
+    hipFree(c->d_bvh_tri);
+    c->d_bvh_node = c->d_bvh_tri = nullptr;
+    c->bvh_inner = c->bvh_leaves = c->bvh_depth = 0;
+    c->bvh_build_ms = 0.0;
     c->cb.valid = false;  // buffers are kept (reallocated on demand)
     c->cam_valid = false;
     c->lb_build_ms = 0.0;
@@ -1411,6 +1498,21 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
     HIP_TRY(c, up((void**)&c->d_quad, qua.data(), qua.size() * sizeof(float)));
     HIP_TRY(c, up((void**)&c->d_translucent, translucent.data(), translucent.size() * sizeof(int)));
     HIP_TRY(c, hipMalloc((void**)&c->d_tricam, (tri.size() / 12) * 16 * sizeof(float)));
+    // the bounce-ray BVH: only a scene with a reflective or refractive
+    // surface has bounce rays (Scene.cpp:1779-1823 gate on Kr, Kt > 0)
+    if (kmax > 0.0f && cnt_tri >= RT_BVH_MIN_TRIANGLES) {
+        const auto tb = std::chrono::steady_clock::now();
+        BvhBuilt B;
+        bvh_build(tri, (size_t)cnt_tri, B);
+        if (B.depth <= kBvhStack) {
+            HIP_TRY(c, up((void**)&c->d_bvh_node, B.nodes.data(), B.nodes.size() * sizeof(float4)));
+            HIP_TRY(c, up((void**)&c->d_bvh_tri, B.tris.data(), B.tris.size() * sizeof(float4)));
+            c->bvh_inner = B.inner;
+            c->bvh_leaves = B.leaves;
+            c->bvh_depth = B.depth;
+        }
+        c->bvh_build_ms = since(tb);
+    }
     // Per triangle (tri[] order), for rt_cone_prepass: the bounding sphere of
     // the triangle the reference tests (p0, p0 + e1, p0 + e2 with the float
     // edges; radius measured from the float-rounded centre), the unit normal
@@ -1613,6 +1715,8 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
     c->n_translucent = cnt_translucent;
     c->shadow_split = opaque ? 1 : 0;
     c->k_max = kmax;
+    c->kr_max = krmax;
+    c->kt_max = ktmax;
     c->uploaded = true;
     c->upload_parts_ms[3] = since(tu0);
     return RT_OK;
@@ -1649,58 +1753,70 @@ typedef void (*kernel_fn)(const SceneDev, const FrameDev, unsigned*, float*, Sta
 #ifndef RT_WAVE_LB
 #define RT_WAVE_LB 1
 #endif
-template <bool COUNT>
-static kernel_fn pick_kernel(int depth, int n_tri, int n_lights, bool lbuf, bool cbuf, int& cap, int& lb)
+// The trace kernel of a frame: its function, bounce-stack capacity (-1:
+// none compiled), lights per shadow pass, dynamic LDS per workgroup, and its
+// name (rt_stats.kernel).
+struct KernelPick {
+    kernel_fn k = nullptr;
+    int cap = 0, lb = 1;
+    unsigned lds = 0;
+    char name[48] = {};
+};
+template <int MAXD, int LB, int WAVE, bool COUNT>
+static KernelPick kpick(unsigned lds)
 {
-    lb = 1;
+    KernelPick p;
+    p.k = (kernel_fn)&rt_trace_kernel<MAXD, LB, WAVE, COUNT>;
+    p.cap = MAXD;
+    p.lb = LB;
+    p.lds = lds;
+    std::snprintf(p.name, sizeof p.name, "rt_trace_kernel<%d,%d,%d>", MAXD, LB, WAVE);
+    return p;
+}
+// bvh: bounce rays through the BVH (depth > 0, the scene's BVH built, light
+// buffer on): WAVE bit 256 with the depth-0 kernels' camera and shadow paths
+// (camera buffer bit 8 — a no-op when S.cb_tiles_x is 0 —, light buffer bit
+// 4, wave culling 1 or clustered 2); its waves carry the traversal stacks in
+// LDS after the staging window.
+template <bool COUNT>
+static KernelPick pick_kernel(int depth, int n_tri, int n_lights, bool lbuf, bool cbuf, int bvh_depth = 0)
+{
+    const bool bvh = bvh_depth > 0;
+    const unsigned win = (unsigned)kLdsWaveBytes;
     if (depth == 0 && n_tri > 0 && lbuf) {  // light-buffer shadows, one light per pass
-        cap = 0;
         if (n_tri > kClusterMinTriangles)
-            return cbuf ? (kernel_fn)&rt_trace_kernel<0, 1, 14, COUNT> : (kernel_fn)&rt_trace_kernel<0, 1, 6, COUNT>;
-        return cbuf ? (kernel_fn)&rt_trace_kernel<0, 1, 13, COUNT> : (kernel_fn)&rt_trace_kernel<0, 1, 5, COUNT>;
+            return cbuf ? kpick<0, 1, 14, COUNT>(win) : kpick<0, 1, 6, COUNT>(win);
+        return cbuf ? kpick<0, 1, 13, COUNT>(0) : kpick<0, 1, 5, COUNT>(0);
     }
-    if (depth == 0 && n_tri > kClusterMinTriangles) {
-        cap = 0;
-        lb = RT_WAVE_LB;
-        return cbuf ? (kernel_fn)&rt_trace_kernel<0, RT_WAVE_LB, 10, COUNT>
-                    : (kernel_fn)&rt_trace_kernel<0, RT_WAVE_LB, 2, COUNT>;
+    if (depth == 0 && n_tri > kClusterMinTriangles)
+        return cbuf ? kpick<0, RT_WAVE_LB, 10, COUNT>(win) : kpick<0, RT_WAVE_LB, 2, COUNT>(win);
+    if (depth == 0 && n_tri > 0)
+        return cbuf ? kpick<0, RT_WAVE_LB, 9, COUNT>(0) : kpick<0, RT_WAVE_LB, 1, COUNT>(0);
+    if (depth == 0 && n_lights > 1) return kpick<0, 3, 0, COUNT>(0);
+    const unsigned bl = (unsigned)(kLdsWaveBytes + (size_t)bvh_depth * 64 * sizeof(int));
+    if (bvh && lbuf && n_tri > 0) {
+#define RT_PICK_BVH(N)                                                                                   \
+    if (depth <= N)                                                                                      \
+        return n_tri > kClusterMinTriangles ? kpick<N, 1, 270, COUNT>(bl) : kpick<N, 1, 269, COUNT>(bl);
+        RT_STACK_DEPTHS(RT_PICK_BVH)
+#undef RT_PICK_BVH
     }
-    if (depth == 0 && n_tri > 0) {
-        cap = 0;
-        lb = RT_WAVE_LB;
-        return cbuf ? (kernel_fn)&rt_trace_kernel<0, RT_WAVE_LB, 9, COUNT>
-                    : (kernel_fn)&rt_trace_kernel<0, RT_WAVE_LB, 1, COUNT>;
-    }
-    if (depth == 0 && n_lights > 1) {
-        cap = 0;
-        lb = 3;
-        return (kernel_fn)&rt_trace_kernel<0, 3, 0, COUNT>;
-    }
-#define RT_PICK(N)                                                        \
-    if (depth <= N) {                                                     \
-        cap = N;                                                          \
-        return (kernel_fn)&rt_trace_kernel<N, 1, 0, COUNT>;        \
-    }
+#define RT_PICK(N) \
+    if (depth <= N) return kpick<N, 1, 0, COUNT>(0);
     RT_STACK_DEPTHS(RT_PICK)
 #undef RT_PICK
-    cap = -1;
-    return nullptr;
+    KernelPick none;
+    none.cap = -1;
+    return none;
 }
 
 // Launch shape of a trace kernel over `rows` output rows: one 8 x 8 tile per
-// workgroup; the big-list kernels get their waves' LDS windows (the staged
-// light-buffer and camera-list walks).
-static void trace_dims(kernel_fn k, int width, int rows, dim3& grid, dim3& block, unsigned& lds)
+// workgroup, the kernel's dynamic LDS (the big-list kernels' staging
+// windows, the BVH kernels' traversal stacks).
+static void trace_dims(int width, int rows, dim3& grid, dim3& block)
 {
-    const bool big = k == (kernel_fn)&rt_trace_kernel<0, 1, 14, false> || k == (kernel_fn)&rt_trace_kernel<0, 1, 14, true> ||
-                     k == (kernel_fn)&rt_trace_kernel<0, 1, 6, false> || k == (kernel_fn)&rt_trace_kernel<0, 1, 6, true> ||
-                     k == (kernel_fn)&rt_trace_kernel<0, RT_WAVE_LB, 10, false> ||
-                     k == (kernel_fn)&rt_trace_kernel<0, RT_WAVE_LB, 10, true> ||
-                     k == (kernel_fn)&rt_trace_kernel<0, RT_WAVE_LB, 2, false> ||
-                     k == (kernel_fn)&rt_trace_kernel<0, RT_WAVE_LB, 2, true>;
     grid = dim3((width + 7) / 8, (rows + 7) / 8);
     block = dim3(64);
-    lds = big ? (unsigned)kLdsWaveBytes : 0u;
 }
 
 // The launch-camera kernel (tiny scenes: camera buffer replaced by the
@@ -1716,12 +1832,11 @@ static const void* tiny_kernel(int mode)
 
 // One trace launch over `rows` output rows (T: the launch-camera kernel with
 // its records, else kernel k).
-static int launch_trace(rt_ctx* c, kernel_fn k, const TinyCam* T, bool count, SceneDev& S, FrameDev& F, int width,
-                        int rows, unsigned* oa, float* ob, StatsDev* stats, hipStream_t st, int mode = 0)
+static int launch_trace(rt_ctx* c, const KernelPick& kp, const TinyCam* T, bool count, SceneDev& S, FrameDev& F,
+                        int width, int rows, unsigned* oa, float* ob, StatsDev* stats, hipStream_t st, int mode = 0)
 {
     dim3 grid, block;
-    unsigned lds = 0;
-    trace_dims(k, width, rows, grid, block, lds);
+    trace_dims(width, rows, grid, block);
     if (T) {
         TinyCam Tv = *T;
         void* args[] = {&S, &F, &Tv, &oa, &ob, &stats};
@@ -1729,7 +1844,7 @@ static int launch_trace(rt_ctx* c, kernel_fn k, const TinyCam* T, bool count, Sc
         return RT_OK;
     }
     void* args[] = {&S, &F, &oa, &ob, &stats};
-    HIP_TRY(c, hipLaunchKernel((const void*)k, grid, block, args, lds, st));
+    HIP_TRY(c, hipLaunchKernel((const void*)kp.k, grid, block, args, kp.lds, st));
     return RT_OK;
 }
 
@@ -1776,6 +1891,7 @@ static void frame_dev(const rt_frame* f, FrameDev& F)
     F.band_rows = f->band_rows;
     F.band_count = f->band_count;
     F.band_index = f->band_index;
+    F.wf = WfDev{};
 }
 
 // Does frame f need the per-camera prepasses (the camera position moved)?
@@ -1842,8 +1958,24 @@ static SceneDev scene_dev(rt_ctx* c, bool lbuf, bool cbuf)
                     lbuf ? c->lb_levels : 0, c->d_lb_off, c->d_lb_ent, c->d_lb_dcap, c->d_lb_meta,
                     (c->d_uni && c->opt_union) ? c->d_uni : nullptr,
                     c->cb.off, c->cb.ent, c->cb.flag, cbuf ? c->cb.tiles_x : 0,
-                    c->cb.inline_rec ? c->cb.rec : nullptr};
+                    c->cb.inline_rec ? c->cb.rec : nullptr, c->d_bvh_node, c->d_bvh_tri};
 }
+
+// The light buffer serves this context's shadow rays (RT_OPT_LIGHT_BUFFER).
+static bool lbuf_on(const rt_ctx* c)
+{
+    const int mode = c->opt_light_buffer;
+    return c->lb_ready && (mode == 1 || (mode == 2 && c->n_tri > kClusterMinTriangles));
+}
+// Bounce rays walk the BVH (rt_bvh.h) in the frame's kernel (the BVH kernels
+// take their shadow rays through the light buffer).
+static bool bvh_on(const rt_ctx* c, int depth, bool lbuf)
+{
+    return depth > 0 && c->d_bvh_node && c->opt_bvh && lbuf && c->n_tri > 0;
+}
+// The frame's camera rays may walk a camera buffer: the depth-0 kernels and
+// the BVH kernels.
+static bool cam_lists(const rt_ctx* c, int depth, bool lbuf) { return depth == 0 || bvh_on(c, depth, lbuf); }
 
 #include "rt_camhost.h"
 
@@ -1915,6 +2047,139 @@ static int prepare_state(rt_ctx* c, const rt_frame* f, hipStream_t st, bool sync
 // per RT_OPT_HOST_CHUNK_MB of output), chunk i's copy on c->copy_stream
 // overlapping chunk i + 1's kernel (the same pixels: every pixel is independent, and the chunks keep
 // the unchunked launch's 8-row wave rows).
+// ---- wavefront bounce levels (rt_wavefront.h)
+// Children one node can spawn: a reflected ray needs some Kr > 0, a
+// refracted one some Kt > 0 (the gates compare K * energy > min_energy >= 0).
+static int wf_branch(const rt_ctx* c) { return (c->kr_max > 0.0f ? 1 : 0) + (c->kt_max > 0.0f ? 1 : 0); }
+
+#ifndef RT_WF_TRACE_WAVES
+#define RT_WF_TRACE_WAVES 32  // trace launch: workgroups (one wave each) per CU
+#endif
+#ifndef RT_WF_MAX_GB
+#define RT_WF_MAX_GB 32.0
+#endif
+// Bytes of the queues for px pixels and `levels` bounce levels: level 0
+// node records (32 B) + parent list (4 B) per pixel; level L >= 1 per ray
+// (px * branch^L rays at most): the ray (32 B), its colour (16 B), and but
+// for the deepest level a node record (32 B) and a parent slot (4 B).
+static size_t wf_bytes(size_t px, int levels, int branch, size_t* cap)
+{
+    size_t tot = 256, n = px, most = 0;
+    cap[0] = px;
+    tot += px * (32 + 4);
+    for (int L = 1; L <= levels; ++L) {
+        n *= (size_t)branch;
+        cap[L] = n;
+        most = std::max(most, n);
+        tot += n * (32 + 16) + (L < levels ? n * (32 + 4) : 0);
+        tot = (tot + 255) & ~(size_t)255;
+    }
+    return tot + most * 8;  // the hit records of the level being shaded
+}
+
+// Would frame f (depth `depth`, its kernel a BVH kernel) render as a
+// wavefront?  RT_OPT_WAVEFRONT, at most kWfMaxLevels levels, a single
+// output chunk, queues within RT_WF_MAX_GB.
+static bool wf_fits(const rt_ctx* c, const rt_frame* f, int depth, int rows)
+{
+    if (!c->opt_wavefront || depth < 1 || depth > kWfMaxLevels || wf_branch(c) == 0) return false;
+    size_t cap[kWfMaxLevels + 1];
+    return (double)wf_bytes((size_t)rows * f->width, depth, wf_branch(c), cap) <= RT_WF_MAX_GB * 1073741824.0;
+}
+
+// The queues for px pixels / `levels` levels (grown, never shrunk; not
+// while capturing).  Fills c->wf.dev.
+static int wf_ensure(rt_ctx* c, size_t px, int levels, bool capturing, bool* ok)
+{
+    rt_ctx::WfBuf& W = c->wf;
+    size_t cap[kWfMaxLevels + 1] = {};
+    const int br = wf_branch(c);
+    const size_t bytes = wf_bytes(px, levels, br, cap);
+    *ok = false;
+    if (bytes > W.bytes) {
+        if (capturing) return RT_OK;  // (the frame renders by the BVH megakernel)
+        free_later(c, W.mem);  // an enqueued frame may still use the old queues
+        W.mem = nullptr;
+        W.bytes = 0;
+        HIP_TRY(c, hipMalloc(&W.mem, bytes));
+        W.bytes = bytes;
+        W.px = 0;
+    }
+    if (!W.ev) HIP_TRY(c, hipEventCreateWithFlags(&W.ev, hipEventDisableTiming));
+    char* p = (char*)W.mem;
+    WfDev& d = W.dev;
+    d = WfDev{};
+    d.count = (unsigned*)p;
+    p += 256;
+    d.node[0] = (float4*)p;
+    p += px * 32;
+    d.plist[0] = (unsigned*)p;
+    p += px * 4;
+    size_t off = (size_t)(p - (char*)W.mem);
+    off = (off + 255) & ~(size_t)255;
+    for (int L = 1; L <= levels; ++L) {
+        p = (char*)W.mem + off;
+        d.ray[L] = (float4*)p;
+        p += cap[L] * 32;
+        d.res[L] = (float4*)p;
+        p += cap[L] * 16;
+        if (L < levels) {
+            d.node[L] = (float4*)p;
+            p += cap[L] * 32;
+            d.plist[L] = (unsigned*)p;
+            p += cap[L] * 4;
+        }
+        off = ((size_t)(p - (char*)W.mem) + 255) & ~(size_t)255;
+    }
+    d.hit = (float2*)((char*)W.mem + off);
+    d.levels = levels;
+    for (int L = 0; L <= levels; ++L) W.cap[L] = cap[L];
+    W.px = px;
+    *ok = true;
+    return RT_OK;
+}
+
+// Level 0 of a wavefront frame: the depth-0 kernel with WAVE bit 512.
+template <bool COUNT>
+static KernelPick pick_wf0(int n_tri, bool cbuf)
+{
+    const unsigned win = (unsigned)kLdsWaveBytes;
+    if (n_tri > kClusterMinTriangles)
+        return cbuf ? kpick<0, 1, 526, COUNT>(win) : kpick<0, 1, 518, COUNT>(win);
+    return cbuf ? kpick<0, 1, 525, COUNT>(0) : kpick<0, 1, 517, COUNT>(0);
+}
+
+// The bounce levels and folds of a wavefront frame, after level 0 on st:
+// per level a trace launch (the BVH walk; LDS = its stack) and a shade
+// launch (LDS = the light-buffer staging window), then the folds.
+static int wf_levels(rt_ctx* c, const SceneDev& S, const FrameDev& F, int levels, bool count, unsigned* rgba,
+                     float* rgbf, StatsDev* stats, hipStream_t st)
+{
+    const bool big = c->n_tri > kClusterMinTriangles;
+    const void* kt = count ? (const void*)&rt_wf_trace<true> : (const void*)&rt_wf_trace<false>;
+    const void* ks = big ? (count ? (const void*)&rt_wf_shade<6, true> : (const void*)&rt_wf_shade<6, false>)
+                         : (count ? (const void*)&rt_wf_shade<5, true> : (const void*)&rt_wf_shade<5, false>);
+    const unsigned lds_t = (unsigned)((size_t)c->bvh_depth * 64 * sizeof(int));
+    const unsigned lds_s = big ? (unsigned)kLdsWaveBytes : 0u;
+    for (int L = 1; L <= levels; ++L) {
+        // enough waves to fill the chip; each strides over the level's queue
+        const size_t waves = (c->wf.cap[L] + 63) / 64;
+        const unsigned gt = (unsigned)std::max<size_t>(1, std::min<size_t>(waves, (size_t)c->n_cu * RT_WF_TRACE_WAVES));
+        const unsigned gs = (unsigned)std::max<size_t>(1, std::min<size_t>(waves, (size_t)c->n_cu * 16));
+        FrameDev Fl = F;
+        int Lv = L;
+        void* args[] = {(void*)&S, (void*)&Fl, (void*)&Lv, (void*)&stats};
+        HIP_TRY(c, hipLaunchKernel(kt, dim3(gt), dim3(64), args, lds_t, st));
+        HIP_TRY(c, hipLaunchKernel(ks, dim3(gs), dim3(64), args, lds_s, st));
+    }
+    for (int L = levels - 1; L >= 0; --L) {
+        const unsigned g = (unsigned)std::min<size_t>((c->wf.cap[L] + 255) / 256, (size_t)c->n_cu * 4);
+        hipLaunchKernelGGL(rt_wf_fold, dim3(std::max(1u, g)), dim3(256), 0, st, F, L, rgba, rgbf);
+        HIP_TRY(c, hipGetLastError());
+    }
+    return RT_OK;
+}
+
 static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_dev, hipStream_t st, bool timed,
                   bool sync_path, void* host_out = nullptr)
 {
@@ -1934,10 +2199,9 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
         capturing = cs != hipStreamCaptureStatusNone;
     }
     const int depth = reachable_depth(c, f);
-    int cap = 0, lb = 1;
-    const int mode = c->opt_light_buffer;
-    const bool lbuf = c->lb_ready && (mode == 1 || (mode == 2 && c->n_tri > kClusterMinTriangles));
-    const bool cb_want = depth == 0 && c->n_tri > 0 && c->opt_camera_buffer && cb_frame_ok(f);
+    const bool lbuf = lbuf_on(c);
+    const bool bvh = bvh_on(c, depth, lbuf);
+    const bool cb_want = cam_lists(c, depth, lbuf) && c->n_tri > 0 && c->opt_camera_buffer && cb_frame_ok(f);
     const int rows = frame_rows(f);
     // tiny scenes: the camera records travel with the launch (no device state)
     TinyCam Tl;
@@ -1953,19 +2217,38 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
         if (int rc = prepare_state(c, f, st, sync_path, capturing, cb_want)) return rc;
     }
     const bool cbuf = !tiny && cb_want && cb_matches(c->cb, f);
-    kernel_fn k = (f->flags & RT_FLAG_STATS)
-                      ? pick_kernel<true>(depth, c->n_tri, c->n_lights, lbuf, cbuf, cap, lb)
-                      : pick_kernel<false>(depth, c->n_tri, c->n_lights, lbuf, cbuf, cap, lb);
-    if (!k) {
+    // Wavefront: a BVH frame's bounce levels as compacted queues (rt_wavefront.h);
+    // its queues are shared by the context's streams: a frame on another
+    // stream than the last wavefront frame waits for that one.  A captured
+    // frame renders by the BVH megakernel instead (no shared state).
+    bool wf = bvh && rows > 0 && !capturing && wf_fits(c, f, depth, rows);
+    if (wf) {
+        bool ok = false;
+        if (int rc = wf_ensure(c, (size_t)rows * f->width, depth, capturing, &ok)) return rc;
+        wf = ok;
+    }
+    const bool count = (f->flags & RT_FLAG_STATS) != 0;
+    const KernelPick kp = wf ? (count ? pick_wf0<true>(c->n_tri, cbuf) : pick_wf0<false>(c->n_tri, cbuf))
+                             : (count ? pick_kernel<true>(depth, c->n_tri, c->n_lights, lbuf, cbuf, bvh ? c->bvh_depth : 0)
+                                      : pick_kernel<false>(depth, c->n_tri, c->n_lights, lbuf, cbuf, bvh ? c->bvh_depth : 0));
+    if (!kp.k) {
         c->err = "reachable bounce depth " + std::to_string(depth) + " exceeds the compiled stack (32)";
         return RT_E_UNSUPPORTED;
     }
     SceneDev S = scene_dev(c, lbuf, cbuf);
     FrameDev F;
     frame_dev(f, F);
+    if (wf) F.wf = c->wf.dev;
     c->last = rt_stats{};
-    c->last.stack_depth = cap;
-    c->last.light_batch = lb;
+    c->last.stack_depth = wf ? depth : kp.cap;
+    c->last.light_batch = kp.lb;
+    if (wf)
+        std::snprintf(c->last.kernel, sizeof c->last.kernel, "wavefront %s + %d levels", kp.name, depth);
+    else if (tiny)
+        std::snprintf(c->last.kernel, sizeof c->last.kernel, "rt_trace_tiny<0,1,%d>",
+                      tmode == 2 ? 229 : (tmode == 1 ? 101 : 37));
+    else
+        std::memcpy(c->last.kernel, kp.name, sizeof kp.name);
     if (rows == 0) return RT_OK;
     if (f->flags & RT_FLAG_STATS) HIP_TRY(c, hipMemsetAsync(c->d_stats, 0, kStatSlots * sizeof(StatsDev), st));
     if (timed) HIP_TRY(c, hipEventRecord(c->ev0, st));
@@ -1976,13 +2259,26 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
     // 7680 x 4320 eight chunks -30%, tools/host_chunks.py)
     const size_t out_bytes = (size_t)rows * f->width * px_bytes;
     const double chunk = c->opt_host_chunk_mb * 1048576.0;
-    const int nch = (host_out && f->band_rows == 0 && chunk > 0)
+    const int nch = (host_out && f->band_rows == 0 && chunk > 0 && !wf)
                         ? (int)std::min(8.0, std::floor((double)out_bytes / chunk))
                         : 1;
+    if (wf) {
+        rt_ctx::WfBuf& W = c->wf;
+        if (W.pending && W.last != st) HIP_TRY(c, hipStreamWaitEvent(st, W.ev, 0));
+        HIP_TRY(c, hipMemsetAsync(W.dev.count, 0, 256, st));
+    }
     if (nch <= 1) {
-        if (int rc = launch_trace(c, k, tiny, f->flags & RT_FLAG_STATS, S, F, f->width, rows, rgba_dev, rgb_dev, stats,
+        if (int rc = launch_trace(c, kp, tiny, f->flags & RT_FLAG_STATS, S, F, f->width, rows, rgba_dev, rgb_dev, stats,
                                   st, tmode))
             return rc;
+        if (tmode == 2)
+            if (int rc = tiny_masks_stored(c, st)) return rc;
+        if (wf) {
+            if (int rc = wf_levels(c, S, F, depth, count, rgba_dev, rgb_dev, stats, st)) return rc;
+            HIP_TRY(c, hipEventRecord(c->wf.ev, st));
+            c->wf.last = st;
+            c->wf.pending = true;
+        }
         if (host_out)
             HIP_TRY(c, hipMemcpyAsync(host_out, rgba_dev ? (void*)rgba_dev : (void*)rgb_dev,
                                       (size_t)rows * f->width * px_bytes, hipMemcpyDeviceToHost, st));
@@ -1998,11 +2294,13 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
             Fc.row_end = f->row_begin + r1;
             unsigned* oa = rgba_dev ? rgba_dev + (size_t)r0 * f->width : nullptr;
             float* ob = rgb_dev ? rgb_dev + (size_t)r0 * f->width * 3 : nullptr;
-            if (int rc = launch_trace(c, k, tiny, f->flags & RT_FLAG_STATS, S, Fc, f->width, r1 - r0, oa, ob, stats, st,
+            if (int rc = launch_trace(c, kp, tiny, f->flags & RT_FLAG_STATS, S, Fc, f->width, r1 - r0, oa, ob, stats, st,
                                       tmode))
                 return rc;
             HIP_TRY(c, hipEventRecord(c->ev_chunk[n], st));
         }
+        if (tmode == 2)
+            if (int rc = tiny_masks_stored(c, st)) return rc;
         if (timed) HIP_TRY(c, hipEventRecord(c->ev1, st));
         const char* src = (const char*)(rgba_dev ? (void*)rgba_dev : (void*)rgb_dev);
         for (int i = 0; i < n; ++i) {
@@ -2033,6 +2331,7 @@ static int finish_sync(rt_ctx* c, const rt_frame* f, hipStream_t st, bool timed)
     c->async_streams.clear();
     c->state_pending = false;
     c->state_stream = nullptr;
+    c->wf.pending = false;
     free_deferred(c);
     if (timed) {
         float ms = 0.f;
@@ -2051,6 +2350,8 @@ static int finish_sync(rt_ctx* c, const rt_frame* f, hipStream_t st, bool timed)
             h.tri += q.tri;
             h.pla += q.pla;
             h.qua += q.qua;
+            h.btri += q.btri;
+            h.bnode += q.bnode;
         }
         c->last.primary_rays = h.primary;
         c->last.bounce_rays = h.bounce;
@@ -2059,6 +2360,8 @@ static int finish_sync(rt_ctx* c, const rt_frame* f, hipStream_t st, bool timed)
         c->last.triangle_tests = h.tri;
         c->last.plane_tests = h.pla;
         c->last.quadric_tests = h.qua;
+        c->last.bounce_triangle_tests = h.btri;
+        c->last.bvh_nodes_visited = h.bnode;
     }
     return RT_OK;
 }
@@ -2141,14 +2444,12 @@ RT_EXPORT int rt_render_sequence_async(rt_ctx* c, const rt_frame* frames, int32_
             c->err = "bad rt_frame geometry (or RT_FLAG_STATS) in a sequence";
             return RT_E_ARG;
         }
-        int cap = 0, lb = 1;
-        if (!pick_kernel<false>(reachable_depth(c, f), c->n_tri, c->n_lights, false, false, cap, lb)) {
+        if (!pick_kernel<false>(reachable_depth(c, f), c->n_tri, c->n_lights, false, false).k) {
             c->err = "reachable bounce depth exceeds the compiled stack (32)";
             return RT_E_UNSUPPORTED;
         }
     }
-    const int mode = c->opt_light_buffer;
-    const bool lbuf = c->lb_ready && (mode == 1 || (mode == 2 && c->n_tri > kClusterMinTriangles));
+    const bool lbuf = lbuf_on(c);
     // The camera slots are shared by every sequence call: one on another
     // stream still in flight must finish first (a captured sequence's
     // ordering against work outside the graph is the caller's, as for any
@@ -2186,14 +2487,14 @@ RT_EXPORT int rt_render_sequence_async(rt_ctx* c, const rt_frame* frames, int32_
             tiny_build(c, f, T);
             if (int rc = tiny_masks(c, f, fs, capturing, T, &tmode)) return rc;
         }
-        const bool cbuf = !tiny && depth == 0 && c->n_tri > 0 && c->opt_camera_buffer && cb_frame_ok(f) &&
+        const bool bvh = bvh_on(c, depth, lbuf);
+        const bool cbuf = !tiny && cam_lists(c, depth, lbuf) && c->n_tri > 0 && c->opt_camera_buffer && cb_frame_ok(f) &&
                           cb_async_pays(c, f) &&
                           (!capturing || (q.cb.cap > 0 && q.cb.rcap > 0 && q.cb.nt_alloc >= nt && q.cb.big_alloc >= c->n_tri));
         if (c->n_tri > 0 && !tiny) {
             if (int rc = camera_records(c, f->cam_pos, fs, cbuf, q.tricam, q.cone_cam, q.uni, q.clu_cam)) return rc;
         }
-        int cap = 0, lb = 1;
-        kernel_fn k = pick_kernel<false>(depth, c->n_tri, c->n_lights, lbuf, cbuf, cap, lb);
+        const KernelPick kp = pick_kernel<false>(depth, c->n_tri, c->n_lights, lbuf, cbuf, bvh ? c->bvh_depth : 0);
         SceneDev S = scene_dev(c, lbuf, false);
         S.tricam = q.tricam;
         S.cone_cam = q.cone_cam;
@@ -2211,9 +2512,11 @@ RT_EXPORT int rt_render_sequence_async(rt_ctx* c, const rt_frame* frames, int32_
         frame_dev(f, F);
         unsigned* rgba = rgba8_dev ? (unsigned*)(rgba8_dev + (size_t)i * rgba8_stride) : nullptr;
         float* rgb = rgb_dev ? (float*)((char*)rgb_dev + (size_t)i * rgb_stride) : nullptr;
-        if (int rc = launch_trace(c, k, tiny ? &T : nullptr, false, S, F, f->width, rows, rgba, rgb, c->d_stats, fs,
+        if (int rc = launch_trace(c, kp, tiny ? &T : nullptr, false, S, F, f->width, rows, rgba, rgb, c->d_stats, fs,
                                   tmode))
             return rc;
+        if (tmode == 2)
+            if (int rc = tiny_masks_stored(c, fs)) return rc;
     }
     // Join: st continues after every frame.
     if (nstreams > 1) {
@@ -2245,12 +2548,13 @@ RT_EXPORT int rt_prepare_camera(rt_ctx* c, const rt_frame* f)
     if (int rc = fence_async(c, c->stream)) return rc;
     if (int rc = wait_state(c, c->stream)) return rc;
     const int depth = reachable_depth(c, f);
-    const bool cb_want = depth == 0 && c->n_tri > 0 && c->opt_camera_buffer && cb_frame_ok(f);
+    const bool cb_want = cam_lists(c, depth, lbuf_on(c)) && c->n_tri > 0 && c->opt_camera_buffer && cb_frame_ok(f);
     if (int rc = prepare_state(c, f, c->stream, true, false, cb_want)) return rc;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     c->async_streams.clear();
     c->state_pending = false;
     c->state_stream = nullptr;
+    c->wf.pending = false;
     free_deferred(c);
     return RT_OK;
 }
@@ -2470,6 +2774,57 @@ RT_EXPORT int rt_debug_scan(int device, const unsigned* in, unsigned n, unsigned
 
 // Diagnostic (include/rt_debug.h): run rt_selftest_kernel over `blocks`
 // workgroups; *failures = lanes whose wave reduction or wave cone was wrong.
+RT_EXPORT int rt_debug_bvh_info(rt_ctx* c, double* out, int n)
+{
+    if (!c || !out || n <= 0) return RT_E_ARG;
+    const double v[5] = {c->d_bvh_node ? 1.0 : 0.0, (double)c->bvh_inner, (double)c->bvh_leaves, (double)c->bvh_depth,
+                         c->bvh_build_ms};
+    for (int i = 0; i < n; ++i) out[i] = i < 5 ? v[i] : 0.0;
+    return RT_OK;
+}
+
+RT_EXPORT int rt_debug_bvh_rays(rt_ctx* c, const float* rays, int n, int* out_idx, float* out_t,
+                                unsigned long long* tally2)
+{
+    if (!c || !rays || n < 0 || !out_idx || !out_t || !tally2) return RT_E_ARG;
+    if (c->cpu) return not_cpu(c);
+    if (!c->uploaded || !c->d_bvh_node) {
+        c->err = "no bounce-ray BVH (scene without reflective/refractive surfaces or < 64 triangles)";
+        return RT_E_STATE;
+    }
+    HIP_TRY(c, hipSetDevice(c->device));
+    if (int rc = sync_all(c)) return rc;
+    if (n == 0) return RT_OK;
+    float* d_rays = nullptr;
+    int* d_idx = nullptr;
+    float* d_t = nullptr;
+    unsigned long long* d_tally = nullptr;
+    int rc = RT_OK;
+    auto chk = [&](hipError_t e, const char* what) {
+        if (e != hipSuccess && rc == RT_OK) rc = hip_fail(c, e, what);
+        return rc == RT_OK;
+    };
+    if (chk(hipMalloc(&d_rays, (size_t)n * 6 * sizeof(float)), "hipMalloc") &&
+        chk(hipMalloc(&d_idx, (size_t)n * 2 * sizeof(int)), "hipMalloc") &&
+        chk(hipMalloc(&d_t, (size_t)n * 2 * sizeof(float)), "hipMalloc") &&
+        chk(hipMalloc(&d_tally, 2 * sizeof(unsigned long long)), "hipMalloc") &&
+        chk(hipMemcpy(d_rays, rays, (size_t)n * 6 * sizeof(float), hipMemcpyHostToDevice), "hipMemcpy") &&
+        chk(hipMemset(d_tally, 0, 2 * sizeof(unsigned long long)), "hipMemset")) {
+        const SceneDev S = scene_dev(c, false, false);
+        hipLaunchKernelGGL(rt_bvh_rays_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64),
+                           (unsigned)(kLdsWaveBytes + kBvhLdsBytes), c->stream, S, d_rays, n, d_idx, d_t, d_tally);
+        if (chk(hipGetLastError(), "rt_bvh_rays_kernel") && chk(hipStreamSynchronize(c->stream), "sync") &&
+            chk(hipMemcpy(out_idx, d_idx, (size_t)n * 2 * sizeof(int), hipMemcpyDeviceToHost), "hipMemcpy") &&
+            chk(hipMemcpy(out_t, d_t, (size_t)n * 2 * sizeof(float), hipMemcpyDeviceToHost), "hipMemcpy"))
+            chk(hipMemcpy(tally2, d_tally, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost), "hipMemcpy");
+    }
+    hipFree(d_rays);
+    hipFree(d_idx);
+    hipFree(d_t);
+    hipFree(d_tally);
+    return rc;
+}
+
 RT_EXPORT int rt_debug_selftest(int device, int blocks, unsigned* failures)
 {
     if (!failures || blocks <= 0) return RT_E_ARG;

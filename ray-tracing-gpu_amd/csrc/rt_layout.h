@@ -121,6 +121,29 @@ struct SceneDev {
     // the records' extra bytes cost more: C5 +3%, against C3 -4 to -5%).
     // Walked inline by the big-list kernel only (small lists: no gain).
     const float4* __restrict__ cb_rec;
+    // Bounce rays (WAVE bit 256, rt_bvh.h): BVH2 inner nodes (5 float4 each,
+    // node 0 the root) over every triangle, and the triangles in leaf order
+    // (tri[]'s 48-byte layout).  nullptr: none.
+    const float4* __restrict__ bvh_node;
+    const float4* __restrict__ bvh_tri;
+};
+
+// Wavefront bounce queues (rt_wavefront.h; the BVH scenes' bounce levels):
+// level L >= 1 holds the rays of bounce L (2 float4 each: [O rior] [D
+// energy]) and their colours (1 float4); level L >= 0 the node records of
+// the rays (level 0: pixels) that spawned children (2 float4: [acc kr]
+// [kt cR cT -], by ray / pixel index) and the list of those parents.
+// count[L]: rays of level L; count[kWfMaxLevels + 1 + L]: parents of
+// level L.  levels = 0: not a wavefront frame.
+constexpr int kWfMaxLevels = 8;
+struct WfDev {
+    float4* ray[kWfMaxLevels + 1];
+    float4* res[kWfMaxLevels + 1];
+    float4* node[kWfMaxLevels + 1];
+    unsigned* plist[kWfMaxLevels + 1];
+    float2* hit;      // the level being shaded: [file index (int bits), t] per ray
+    unsigned* count;
+    int levels;
 };
 
 struct FrameDev {
@@ -133,10 +156,11 @@ struct FrameDev {
     float min_energy, scene_ior;
     int flags;
     int band_rows, band_count, band_index;  // band_rows > 0: cyclic row bands (rt.h)
+    WfDev wf;
 };
 
 struct StatsDev {
-    unsigned long long primary, bounce, shadow, skipped, tri, pla, qua, pad;
+    unsigned long long primary, bounce, shadow, skipped, tri, pla, qua, btri, bnode, pad;
 };
 // Stats tallies land in kStatSlots copies (by block) so the atomics of a
 // launch spread over many addresses instead of serialising on one.
@@ -154,6 +178,7 @@ constexpr unsigned kXcds = 8;  // MI355X: 8 XCDs, one L2 each
 struct Counters {
     unsigned primary = 0, bounce = 0, shadow = 0, skipped = 0;
     unsigned tri = 0, pla = 0, qua = 0;
+    unsigned btri = 0, bnode = 0;  // bounce rays: triangle tests, BVH nodes visited
 #ifdef RT_PROF  // diagnostic build (tools/prof_sections.py): shader clocks per section
     unsigned long long pt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long last = 0;

@@ -33,6 +33,10 @@
 // the same image, the GPU never touched.
 #include <hip/hip_runtime_api.h>
 
+#include <dlfcn.h>
+#include <unistd.h>
+
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -78,81 +82,203 @@ static void print_done(rt_ctx* c0, double total, int frames, int gpus, int band,
                     (unsigned long long)st.quadric_tests);
 }
 
-// The RCCL path of -g N (N distinct GPUs): every rank renders its part into
-// device memory on its own GPU (rt_render_async on the rank's gather
-// stream), then one RCCL group gathers the parts into the root GPU's frame —
-// a slab is one chunk, a band set one chunk per 16-row band (each lands at
-// its rows of the frame) — and the root's frame is copied to the host once.
-// Timed: the whole frame (renders + gather) and, separately, the gather.
+// librt_gather.so, loaded only by the RCCL path (dlopen next to this
+// binary): every other mode — --backend cpu, one GPU, --gather host — runs
+// without RCCL present.
+struct GatherLib {
+    void* h = nullptr;
+    int (*create)(int32_t, const int32_t*, rt_gather**) = nullptr;
+    void* (*stream)(rt_gather*, int32_t) = nullptr;
+    int (*chunks)(rt_gather*, int32_t, const rt_gather_chunk*, void*) = nullptr;
+    int (*sync)(rt_gather*) = nullptr;
+    int (*version)(void) = nullptr;
+    const char* (*error)(rt_gather*) = nullptr;
+    void (*destroy)(rt_gather*) = nullptr;
+};
+
+static bool load_gather(GatherLib& L, std::string& why)
+{
+    char exe[4096];
+    const ssize_t n = readlink("/proc/self/exe", exe, sizeof exe - 1);
+    std::string dir = ".";
+    if (n > 0) {
+        exe[n] = '\0';
+        dir = exe;
+        dir = dir.substr(0, dir.find_last_of('/'));
+    }
+    const std::string path = dir + "/librt_gather.so";
+    L.h = dlopen(path.c_str(), RTLD_NOW | RTLD_LOCAL);
+    if (!L.h) {
+        const char* e = dlerror();
+        why = path + ": " + (e ? e : "dlopen failed");
+        return false;
+    }
+    auto sym = [&](const char* name) { return dlsym(L.h, name); };
+    L.create = (decltype(L.create))sym("rt_gather_create");
+    L.stream = (decltype(L.stream))sym("rt_gather_stream");
+    L.chunks = (decltype(L.chunks))sym("rt_gather_chunks");
+    L.sync = (decltype(L.sync))sym("rt_gather_sync");
+    L.version = (decltype(L.version))sym("rt_gather_rccl_version");
+    L.error = (decltype(L.error))sym("rt_gather_error");
+    L.destroy = (decltype(L.destroy))sym("rt_gather_destroy");
+    if (!L.create || !L.stream || !L.chunks || !L.sync || !L.version || !L.error || !L.destroy) {
+        why = path + ": missing rt_gather_* symbols";
+        return false;
+    }
+    return true;
+}
+
+// The RCCL path of -g N (N distinct GPUs), pipelined: every rank renders
+// frame k into one of two slabs in device memory on its own GPU (on a render
+// stream of its own), and frame k's RCCL group — a slab is one chunk, a band
+// set one chunk per 16-row band, each landing at its rows of the root GPU's
+// frame — runs on the ranks' gather streams while frame k + 1 renders into
+// the other slabs; ordering by events only (render k -> gather k on each
+// rank; gather k -> render k + 2 into the same slab), one host sync at the
+// end.  Reported per frame: the renders (slowest rank, events) and the
+// gather (root's gather stream, events), and the wall time of all frames.
 static int render_rccl(std::vector<rt_ctx*>& ctx, std::vector<rt_frame>& part,
                        const std::vector<std::vector<uint8_t>>& img, int W, int H, int band, int dev0, int ndev,
                        int frames, bool stats, const char* out, rt_scene* scene)
 {
+    GatherLib G;
+    std::string why;
+    if (!load_gather(G, why)) return fail("librt_gather.so", RT_E_UNSUPPORTED, why.c_str());
     const int n = (int)ctx.size();
     std::vector<int32_t> devs((size_t)n);
     for (int r = 0; r < n; ++r) devs[r] = (dev0 + r) % ndev;
     rt_gather* g = nullptr;
-    int rc = rt_gather_create(n, devs.data(), &g);
-    if (rc) return fail("rt_gather_create", rc, rt_gather_error(g));
+    int rc = G.create(n, devs.data(), &g);
+    if (rc) return fail("rt_gather_create", rc, G.error(g));
     const size_t rowb = (size_t)W * 4;
-    std::vector<void*> slab((size_t)n, nullptr);
+    // per rank: two slabs, a render stream, events (render done / gather
+    // done per slab, timing pairs per frame)
+    std::vector<void*> slab((size_t)2 * n, nullptr);
+    std::vector<hipStream_t> rs((size_t)n, nullptr);
+    std::vector<hipEvent_t> ev_r((size_t)2 * n, nullptr), ev_g((size_t)2 * n, nullptr);
+    std::vector<hipEvent_t> t_r0((size_t)n * frames, nullptr), t_r1((size_t)n * frames, nullptr);
+    std::vector<hipEvent_t> t_g0((size_t)frames, nullptr), t_g1((size_t)frames, nullptr);
     void* full = nullptr;
-    std::vector<rt_gather_chunk> ch;
     for (int r = 0; r < n; ++r) {
         (void)hipSetDevice(devs[r]);
-        if (!img[r].empty() && hipMalloc(&slab[r], img[r].size()) != hipSuccess)
-            return fail("hipMalloc", RT_E_HIP, "slab");
+        for (int b = 0; b < 2; ++b)
+            if (!img[r].empty() && hipMalloc(&slab[2 * r + b], img[r].size()) != hipSuccess)
+                return fail("hipMalloc", RT_E_HIP, "slab");
         if (r == 0 && hipMalloc(&full, rowb * H) != hipSuccess) return fail("hipMalloc", RT_E_HIP, "frame");
-        if (img[r].empty()) continue;
-        if (band) {  // packed band j of rank r -> frame rows (j n + r) band ...
-            const int q = (int)(img[r].size() / rowb) / band;
-            for (int j = 0; j < q; ++j) {
-                const int y0 = (j * n + r) * band, rows = std::min(band, H - y0);
-                if (rows > 0)
-                    ch.push_back({r, (const char*)slab[r] + (size_t)j * band * rowb, (size_t)rows * rowb, (size_t)y0 * rowb});
-            }
-        } else {
-            ch.push_back({r, slab[r], img[r].size(), (size_t)part[r].row_begin * rowb});
+        if (hipStreamCreateWithFlags(&rs[r], hipStreamNonBlocking) != hipSuccess) return fail("hipStreamCreate", RT_E_HIP, "");
+        for (int b = 0; b < 2; ++b) {
+            if (hipEventCreateWithFlags(&ev_r[2 * r + b], hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&ev_g[2 * r + b], hipEventDisableTiming) != hipSuccess)
+                return fail("hipEventCreate", RT_E_HIP, "");
         }
+        for (int k = 0; k < frames; ++k)
+            if (hipEventCreate(&t_r0[(size_t)r * frames + k]) != hipSuccess ||
+                hipEventCreate(&t_r1[(size_t)r * frames + k]) != hipSuccess)
+                return fail("hipEventCreate", RT_E_HIP, "");
+        if (r == 0)
+            for (int k = 0; k < frames; ++k)
+                if (hipEventCreate(&t_g0[k]) != hipSuccess || hipEventCreate(&t_g1[k]) != hipSuccess)
+                    return fail("hipEventCreate", RT_E_HIP, "");
     }
-    size_t gbytes = 0;
-    for (const auto& c : ch) gbytes += c.bytes;
-    const int ver = rt_gather_rccl_version();
-    std::printf("[ETAT]: gather: RCCL %d.%d.%d, %d rank(s), %zu chunk(s), %.1f MB into GPU %d\n", ver / 10000,
-                (ver / 100) % 100, ver % 100, n, ch.size(), gbytes / 1e6, devs[0]);
-    std::printf("[ETAT]: Lancer de rayons...\n");
-    double total = 0.0, gtotal = 0.0;
-    for (int k = 0; k < frames; ++k) {
-        const auto t0 = std::chrono::steady_clock::now();
+    auto chunks_of = [&](int b) {
+        std::vector<rt_gather_chunk> ch;
         for (int r = 0; r < n; ++r) {
             if (img[r].empty()) continue;
-            if ((rc = rt_render_async(ctx[r], &part[r], (uint8_t*)slab[r], nullptr, rt_gather_stream(g, r))))
-                return fail("LancerRayons", rc, rt_last_error(ctx[r]));
+            const char* src = (const char*)slab[2 * r + b];
+            if (band) {  // packed band j of rank r -> frame rows (j n + r) band ...
+                const int q = (int)(img[r].size() / rowb) / band;
+                for (int j = 0; j < q; ++j) {
+                    const int y0 = (j * n + r) * band, rows = std::min(band, H - y0);
+                    if (rows > 0) ch.push_back({r, src + (size_t)j * band * rowb, (size_t)rows * rowb, (size_t)y0 * rowb});
+                }
+            } else {
+                ch.push_back({r, src, img[r].size(), (size_t)part[r].row_begin * rowb});
+            }
         }
-        if ((rc = rt_gather_sync(g))) return fail("rt_gather_sync", rc, rt_gather_error(g));
-        const auto t1 = std::chrono::steady_clock::now();
-        if ((rc = rt_gather_chunks(g, (int32_t)ch.size(), ch.data(), full)))
-            return fail("rt_gather_chunks", rc, rt_gather_error(g));
-        if ((rc = rt_gather_sync(g))) return fail("rt_gather_sync", rc, rt_gather_error(g));
-        const auto t2 = std::chrono::steady_clock::now();
-        total += std::chrono::duration<double>(t2 - t0).count();
-        gtotal += std::chrono::duration<double>(t2 - t1).count();
+        return ch;
+    };
+    const std::vector<rt_gather_chunk> ch[2] = {chunks_of(0), chunks_of(1)};
+    size_t gbytes = 0;
+    for (const auto& c : ch[0]) gbytes += c.bytes;
+    const int ver = G.version();
+    std::printf("[ETAT]: gather: RCCL %d.%d.%d, %d rank(s), %zu chunk(s), %.1f MB into GPU %d, pipelined (2 slabs)\n",
+                ver / 10000, (ver / 100) % 100, ver % 100, n, ch[0].size(), gbytes / 1e6, devs[0]);
+    std::printf("[ETAT]: Lancer de rayons...\n");
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int k = 0; k < frames; ++k) {
+        const int b = k & 1;
+        for (int r = 0; r < n; ++r) {
+            if (img[r].empty()) continue;
+            (void)hipSetDevice(devs[r]);
+            if (k >= 2 && hipStreamWaitEvent(rs[r], ev_g[2 * r + b], 0) != hipSuccess)  // gather k-2 read this slab
+                return fail("hipStreamWaitEvent", RT_E_HIP, "");
+            (void)hipEventRecord(t_r0[(size_t)r * frames + k], rs[r]);
+            if ((rc = rt_render_async(ctx[r], &part[r], (uint8_t*)slab[2 * r + b], nullptr, rs[r])))
+                return fail("LancerRayons", rc, rt_last_error(ctx[r]));
+            (void)hipEventRecord(t_r1[(size_t)r * frames + k], rs[r]);
+            (void)hipEventRecord(ev_r[2 * r + b], rs[r]);
+            if (hipStreamWaitEvent((hipStream_t)G.stream(g, r), ev_r[2 * r + b], 0) != hipSuccess)
+                return fail("hipStreamWaitEvent", RT_E_HIP, "");
+        }
+        (void)hipSetDevice(devs[0]);
+        (void)hipEventRecord(t_g0[k], (hipStream_t)G.stream(g, 0));
+        if ((rc = G.chunks(g, (int32_t)ch[b].size(), ch[b].data(), full)))
+            return fail("rt_gather_chunks", rc, G.error(g));
+        (void)hipEventRecord(t_g1[k], (hipStream_t)G.stream(g, 0));
+        for (int r = 0; r < n; ++r) {
+            if (img[r].empty()) continue;
+            (void)hipSetDevice(devs[r]);
+            (void)hipEventRecord(ev_g[2 * r + b], (hipStream_t)G.stream(g, r));
+        }
+    }
+    if ((rc = G.sync(g))) return fail("rt_gather_sync", rc, G.error(g));
+    for (int r = 0; r < n; ++r) {
+        (void)hipSetDevice(devs[r]);
+        (void)hipStreamSynchronize(rs[r]);
+    }
+    const double total = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    double rsum = 0.0, gsum = 0.0;
+    for (int k = 0; k < frames; ++k) {
+        float worst = 0.f, gm = 0.f;
+        for (int r = 0; r < n; ++r) {
+            if (img[r].empty()) continue;
+            float ms = 0.f;
+            if (hipEventElapsedTime(&ms, t_r0[(size_t)r * frames + k], t_r1[(size_t)r * frames + k]) == hipSuccess)
+                worst = std::max(worst, ms);
+        }
+        (void)hipEventElapsedTime(&gm, t_g0[k], t_g1[k]);
+        rsum += worst;
+        gsum += gm;
     }
     std::vector<uint8_t> host(rowb * H);
     (void)hipSetDevice(devs[0]);
     if (hipMemcpy(host.data(), full, host.size(), hipMemcpyDeviceToHost) != hipSuccess)
         return fail("hipMemcpy", RT_E_HIP, "frame to host");
-    std::printf("[ETAT]: gather: %.3f ms per frame (RCCL group of %zu send/recv pair(s))\n", gtotal * 1e3 / frames,
-                ch.size());
+    std::printf("[ETAT]: per frame: render %.3f ms (slowest rank), gather %.3f ms (RCCL group of %zu send/recv "
+                "pair(s)), wall %.3f ms\n",
+                rsum / frames, gsum / frames, ch[0].size(), total * 1e3 / frames);
     print_done(ctx[0], total, frames, n, band, stats);
     if (out && write_ppm(out, W, H, host)) return fail("fopen", -1, out);
     for (int r = 0; r < n; ++r) {
         (void)hipSetDevice(devs[r]);
-        (void)hipFree(slab[r]);
+        for (int b = 0; b < 2; ++b) {
+            (void)hipFree(slab[2 * r + b]);
+            (void)hipEventDestroy(ev_r[2 * r + b]);
+            (void)hipEventDestroy(ev_g[2 * r + b]);
+        }
+        for (int k = 0; k < frames; ++k) {
+            (void)hipEventDestroy(t_r0[(size_t)r * frames + k]);
+            (void)hipEventDestroy(t_r1[(size_t)r * frames + k]);
+        }
+        (void)hipStreamDestroy(rs[r]);
     }
     (void)hipSetDevice(devs[0]);
+    for (int k = 0; k < frames; ++k) {
+        (void)hipEventDestroy(t_g0[k]);
+        (void)hipEventDestroy(t_g1[k]);
+    }
     (void)hipFree(full);
-    rt_gather_destroy(g);
+    G.destroy(g);
     for (rt_ctx* c : ctx) rt_destroy(c);
     rt_scene_destroy(scene);
     return 0;

@@ -173,6 +173,7 @@ __device__ __forceinline__ int closest_hit(const SceneDev& S, const Vec3 O, cons
         }
         const TriRec tr = load_tri(S, k);
         ++cnt.tri;
+        if constexpr (!CAMERA) ++cnt.btri;  // bounce rays: every triangle
         const TriU r = tri_u(tr.p0, tr.e1, tr.e2, O, D);
         if (!__any(r.ok)) continue;
         float t;

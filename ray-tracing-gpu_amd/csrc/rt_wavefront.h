@@ -1,0 +1,211 @@
+// rt_wavefront.h — wavefront bounce levels for the BVH scenes: the
+// commented reflect/refract recursion (Scene.cpp:1779-1823) unrolled level
+// by level through queues in HBM instead of a per-lane DFS stack, so each
+// bounce level runs as its own launch over a COMPACTED queue of live rays
+// (ballot + prefix per wave, one atomic per wave) — full waves for the
+// BVH walk and the shading, whatever fraction of the pixels still bounces.
+// Part of the device code of rt_kernels.hip (one translation unit: the
+// kernels are templates instantiated by its host half); built with the
+// same exactness flags (no FMA contraction, IEEE div/sqrt).
+//
+// Level 0 is the depth-0 kernel (camera rays, camera buffer, light buffer)
+// with WAVE bit 512: a pixel whose hit spawns children writes a node record
+// instead of its colour.  Level L >= 1 (rt_wf_level): each queued ray is
+// traced through the BVH, shaded, and either spawns children into level
+// L + 1 (a node record) or writes its colour.  Then the levels fold from the
+// deepest up (rt_wf_fold): a node's colour is ((acc + C_refl * Kr) + C_refr
+// * Kt) — the reference's order, Scene.cpp:1787 then :1822 — from its
+// children's colours, and level 0's parents write their pixels.  Every ray
+// is the same ray the DFS traces (same origin P = O + t D, Reflect /
+// Refract of the same operands, same gates), and every fold one thread's
+// fixed-order sums, so the image is the DFS's bit for bit; the queue order
+// (atomic per wave) changes nothing but where records live.
+#ifndef RT_AMD_RT_WAVEFRONT_H
+#define RT_AMD_RT_WAVEFRONT_H
+
+#include "rt_bvh.h"
+
+#pragma clang fp contract(off)
+
+namespace rt {
+
+__device__ __forceinline__ unsigned lane_rank(unsigned long long m)
+{
+    return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+}
+
+// The children of a level-L node (act: a ray of level L that hit a surface
+// of material m at P with normal N, coming along D with ray IOR rior and
+// energy; acc its local colour; self its index — the pixel for level 0, the
+// ray for level L >= 1).  Gates of Scene.cpp:1780 / :1791 (bounces = L);
+// reflected rays keep CRayon's default IOR 0 (:1782-1788), refracted ones
+// Scene.cpp:1793-1822.  Returns true when the node spawned a child (its
+// colour then comes from rt_wf_fold).
+__device__ __forceinline__ bool wf_children(const FrameDev& F, int L, bool act, const Mat& m, const Vec3 P,
+                                            const Vec3 N, const Vec3 D, float rior, float energy, const Color acc,
+                                            unsigned self)
+{
+    const float er = m.kr * energy;
+    const float et = m.kt * energy;
+    const bool can = act & (L < F.max_bounces) & (L < F.wf.levels);
+    const bool doR = can & (er > F.min_energy);
+    const bool doT = can & (et > F.min_energy);
+    const unsigned long long bR = __ballot(doR), bT = __ballot(doT), bP = __ballot(doR | doT);
+    if (bP == 0ull) return false;
+    // one atomic per wave for the rays, one for the parents; slots in lane
+    // order, reflected children first
+    const int lead = (int)__builtin_ctzll(__ballot(true));
+    const int lane = (int)(threadIdx.x & 63);
+    unsigned base = 0u, pbase = 0u;
+    if (lane == lead) {
+        base = atomicAdd(&F.wf.count[L + 1], (unsigned)(__popcll(bR) + __popcll(bT)));
+        pbase = atomicAdd(&F.wf.count[kWfMaxLevels + 1 + L], (unsigned)__popcll(bP));
+    }
+    base = (unsigned)__builtin_amdgcn_readlane((int)base, lead);
+    pbase = (unsigned)__builtin_amdgcn_readlane((int)pbase, lead);
+    int cR = -1, cT = -1;
+    float4* const q = F.wf.ray[L + 1];
+    if (doR) {
+        cR = (int)(base + lane_rank(bR));
+        const Vec3 Dr = reflect(D, N);
+        q[2 * (size_t)cR] = make_float4(P.x, P.y, P.z, 0.0f);
+        q[2 * (size_t)cR + 1] = make_float4(Dr.x, Dr.y, Dr.z, er);
+    }
+    if (doT) {
+        cT = (int)(base + (unsigned)__popcll(bR) + lane_rank(bT));
+        Vec3 n = N;
+        float ratio, rior_t;
+        if (rior == m.ior) {  // Scene.cpp:1797-1803 inside -> out
+            rior_t = F.scene_ior;
+            ratio = m.ior / F.scene_ior;
+            n = -n;
+        } else {
+            rior_t = m.ior;
+            ratio = F.scene_ior / m.ior;
+        }
+        const Vec3 Dt = refract(D, n, ratio);
+        q[2 * (size_t)cT] = make_float4(P.x, P.y, P.z, rior_t);
+        q[2 * (size_t)cT + 1] = make_float4(Dt.x, Dt.y, Dt.z, et);
+    }
+    if (doR | doT) {
+        float4* nd = F.wf.node[L] + 2 * (size_t)self;
+        nd[0] = make_float4(acc.r, acc.g, acc.b, m.kr);
+        nd[1] = make_float4(m.kt, __int_as_float(cR), __int_as_float(cT), 0.0f);
+        F.wf.plist[L][pbase + lane_rank(bP)] = self;
+    }
+    return doR | doT;
+}
+
+// Bounce level L >= 1 runs as two launches over the level's queue (a
+// grid-stride loop over the count the previous launch left, 64 rays per
+// wave; every wave leaves when the queue is exhausted):
+//  * rt_wf_trace: each ray's closest hit, through the BVH (rt_bvh.h) —
+//    alone, so the walk's node and triangle records keep the L2 to
+//    themselves and its small register and LDS footprint (the stack only,
+//    depth x 256 bytes) keeps many waves in flight for its dependent loads;
+//  * rt_wf_shade: the hit's shading (light buffer) and its children.
+template <bool COUNT>
+__device__ __forceinline__ void wf_tally(const Counters& cnt, StatsDev* __restrict__ stats)
+{
+    unsigned long long v[9] = {cnt.primary, cnt.bounce, cnt.shadow, cnt.skipped, cnt.tri,
+                               cnt.pla,     cnt.qua,    cnt.btri,   cnt.bnode};
+    StatsDev* sl = stats + (blockIdx.x % kStatSlots);
+    unsigned long long* dst[9] = {&sl->primary, &sl->bounce, &sl->shadow, &sl->skipped, &sl->tri,
+                                  &sl->pla,     &sl->qua,    &sl->btri,   &sl->bnode};
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+        const unsigned long long w = wave_sum_u64(v[k]);
+        if ((threadIdx.x & 63) == 0) atomicAdd(dst[k], w);
+    }
+}
+
+template <bool COUNT>
+__global__ __launch_bounds__(64) void rt_wf_trace(const SceneDev S, const FrameDev F, int L,
+                                                  StatsDev* __restrict__ stats)
+{
+    const unsigned n = F.wf.count[L];
+    const float4* __restrict__ q = F.wf.ray[L];
+    Counters cnt;
+    for (unsigned base = blockIdx.x * 64u; base < n; base += gridDim.x * 64u) {
+        const unsigned i = base + (threadIdx.x & 63u);
+        if (i < n) {
+            const float4 r0 = q[2 * (size_t)i], r1 = q[2 * (size_t)i + 1];
+            ++cnt.bounce;
+            float t;
+            const int idx = closest_hit_bvh<0>(S, make3(r0.x, r0.y, r0.z), make3(r1.x, r1.y, r1.z), t, cnt);
+            F.wf.hit[i] = make_float2(__int_as_float(idx), t);
+        }
+    }
+    if (COUNT && (F.flags & RT_FLAG_STATS)) wf_tally<COUNT>(cnt, stats);
+}
+
+template <int WAVE, bool COUNT>
+__global__ __launch_bounds__(64) void rt_wf_shade(const SceneDev S, const FrameDev F, int L,
+                                                  StatsDev* __restrict__ stats)
+{
+    const unsigned n = F.wf.count[L];
+    const Color bg{F.bg[0], F.bg[1], F.bg[2]};
+    Counters cnt;
+    const float4* __restrict__ q = F.wf.ray[L];
+    for (unsigned base = blockIdx.x * 64u; base < n; base += gridDim.x * 64u) {
+        const unsigned i = base + (threadIdx.x & 63u);
+        if (i < n) {
+            const float2 h = F.wf.hit[i];
+            const int idx = __float_as_int(h.x);
+            Color res = bg;
+            bool parent = false;
+            if (idx >= 0) {
+                const float4 r0 = q[2 * (size_t)i], r1 = q[2 * (size_t)i + 1];
+                const Vec3 O = make3(r0.x, r0.y, r0.z), D = make3(r1.x, r1.y, r1.z);
+                const float t = h.y;
+                const Vec3 N = hit_normal(S, idx, O, D, t);
+                const Mat m = load_mat(S, idx);
+                const Vec3 P = O + t * D;
+#ifdef RT_WF_NO_SHADE  // timing experiment only (wrong images)
+                res = m.color;
+#else
+                res = shade_local<1, WAVE>(S, m, P, N, D, cnt);
+#endif
+                parent = wf_children(F, L, true, m, P, N, D, r0.w, r1.w, res, i);
+            }
+            if (!parent) F.wf.res[L][i] = make_float4(res.r, res.g, res.b, 0.0f);
+        }
+    }
+    if (COUNT && (F.flags & RT_FLAG_STATS)) wf_tally<COUNT>(cnt, stats);
+}
+
+// Fold level L (deepest first): each parent's colour from its children's,
+// in the reference's order; level 0 writes the parents' pixels.
+__global__ __launch_bounds__(256) void rt_wf_fold(const FrameDev F, int L, unsigned* __restrict__ rgba,
+                                                  float* __restrict__ rgbf)
+{
+    const unsigned n = F.wf.count[kWfMaxLevels + 1 + L];
+    const float4* __restrict__ child = F.wf.res[L + 1];
+    for (unsigned j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
+        const unsigned i = F.wf.plist[L][j];
+        const float4 a = F.wf.node[L][2 * (size_t)i], b = F.wf.node[L][2 * (size_t)i + 1];
+        Color c{a.x, a.y, a.z};
+        const int cR = __float_as_int(b.y), cT = __float_as_int(b.z);
+        if (cR >= 0) {
+            const float4 r = child[cR];
+            c += Color{r.x, r.y, r.z} * a.w;  // Scene.cpp:1787
+        }
+        if (cT >= 0) {
+            const float4 r = child[cT];
+            c += Color{r.x, r.y, r.z} * b.x;  // Scene.cpp:1822
+        }
+        if (L > 0) {
+            F.wf.res[L][i] = make_float4(c.r, c.g, c.b, 0.0f);
+        } else {
+            if (rgbf) {
+                rgbf[3 * (size_t)i] = c.r;
+                rgbf[3 * (size_t)i + 1] = c.g;
+                rgbf[3 * (size_t)i + 2] = c.b;
+            }
+            if (rgba) rgba[i] = unorm8(c.r) | (unorm8(c.g) << 8) | (unorm8(c.b) << 16) | 0xFF000000u;
+        }
+    }
+}
+
+}  // namespace rt
+#endif  // RT_AMD_RT_WAVEFRONT_H

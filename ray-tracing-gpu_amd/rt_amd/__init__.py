@@ -35,7 +35,7 @@ TRIANGLE, PLANE, QUADRIC = 0, 1, 2
 FLAG_STATS = 1
 # rt.h RT_OPT_* (ABI 5): A/B and test switches, none changes an image bit
 OPTIONS = {"light_buffer": 1, "camera_buffer": 2, "union_pretest": 3, "lb_scale": 4, "dcov_near": 5,
-           "cb_inline_max_mb": 6, "host_chunk_mb": 7, "cb_capacity": 8, "launch_camera": 12}
+           "cb_inline_max_mb": 6, "host_chunk_mb": 7, "cb_capacity": 8, "launch_camera": 12, "bvh": 13, "wavefront": 14}
 _ERRORS = {-1: "RT_E_ARG", -2: "RT_E_IO", -3: "RT_E_PARSE", -4: "RT_E_STATE", -5: "RT_E_HIP",
            -6: "RT_E_UNSUPPORTED"}
 
@@ -74,7 +74,14 @@ class Stats(ctypes.Structure):
                 ("shadow_rays", ctypes.c_uint64), ("shadow_tests_skipped", ctypes.c_uint64),
                 ("kernel_ms", ctypes.c_float), ("stack_depth", ctypes.c_int32),
                 ("light_batch", ctypes.c_int32), ("triangle_tests", ctypes.c_uint64),
-                ("plane_tests", ctypes.c_uint64), ("quadric_tests", ctypes.c_uint64)]
+                ("plane_tests", ctypes.c_uint64), ("quadric_tests", ctypes.c_uint64),
+                ("bounce_triangle_tests", ctypes.c_uint64), ("bvh_nodes_visited", ctypes.c_uint64),
+                ("kernel_name", ctypes.c_char * 48)]
+
+    @property
+    def kernel(self) -> str:
+        """The trace kernel that ran (rt_stats.kernel)."""
+        return self.kernel_name.decode()
 
 
 _lib: Optional[ctypes.CDLL] = None

@@ -130,6 +130,14 @@ def heightfield_path(tmp_path_factory):
     return synth.write_heightfield(str(tmp_path_factory.mktemp("hf") / "heightfield.dat"))
 
 
+@pytest.fixture(scope="session")
+def heightfield_r05_path(tmp_path_factory):
+    """The heightfield with `reflect: 0.5` on every triangle (bench c3r / c5r)."""
+    from rt_amd import synth
+
+    return synth.write_heightfield(str(tmp_path_factory.mktemp("hfr") / "heightfield_r05.dat"), reflect=0.5)
+
+
 def scene(i: int) -> str:
     return os.path.join(SCENES, f"scene{i}.dat")
 

@@ -62,10 +62,14 @@ def test_gather_library_exports_its_header():
     assert "librccl.so" in deps
     # the renderer itself never links RCCL (PyTorch brings its own)
     assert "librccl" not in subprocess.run(["objdump", "-p", rt_amd.LIB_PATH], capture_output=True, text=True).stdout
+    # rt_render loads librt_gather.so (and RCCL) only on its RCCL path (dlopen)
+    exe = os.path.join(REPO, "ray-tracing-gpu_amd", "lib", "rt_render")
+    needed = subprocess.run(["objdump", "-p", exe], capture_output=True, text=True).stdout
+    assert "librt_gather" not in needed and "librccl" not in needed
 
 
 def test_abi_version():
-    assert rt_amd.lib().rt_abi_version() == 6
+    assert rt_amd.lib().rt_abi_version() == 7
 
 
 def test_struct_layouts_match_header():
@@ -156,7 +160,7 @@ def test_option_enum_matches_binding_and_round_trips():
     h = ctypes.c_void_p()
     assert L.rt_create_cpu(1, ctypes.byref(h)) == 0
     values = {"light_buffer": 2, "camera_buffer": 2, "union_pretest": 0, "lb_scale": 8, "dcov_near": 1.5,
-              "cb_inline_max_mb": 64, "host_chunk_mb": 4, "cb_capacity": 1000, "launch_camera": 0}
+              "cb_inline_max_mb": 64, "host_chunk_mb": 4, "cb_capacity": 1000, "launch_camera": 0, "bvh": 0, "wavefront": 0}
     assert set(values) == set(enum)
     try:
         for name, v in values.items():

@@ -47,7 +47,8 @@ def test_scene2_1080p_matches_reference_digest(tmp_path, digests, extra):
     assert hashlib.sha256(tex.tobytes()).hexdigest() == digests["scene2_1920x1080_d0_rgba8_sha256"]
 
 
-@pytest.mark.parametrize("extra", [["-g", "1", "--gather", "rccl"], ["-g", "1", "--gather", "rccl", "-n", "3"]])
+@pytest.mark.parametrize("extra", [["-g", "1", "--gather", "rccl"], ["-g", "1", "--gather", "rccl", "-n", "3"],
+                                   ["-g", "1", "--gather", "rccl", "-n", "8", "--bands"]])
 def test_rccl_gather_matches_reference_digest(tmp_path, digests, extra):
     """rt_render's native RCCL path (librt_gather.so): the rank renders into
     device memory and ONE RCCL group (ncclSend / ncclRecv, here the root to
@@ -59,6 +60,8 @@ def test_rccl_gather_matches_reference_digest(tmp_path, digests, extra):
                        text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     assert "[ETAT]: gather: RCCL" in r.stdout and "send/recv pair(s)" in r.stdout, r.stdout
+    # pipelined: frame k + 1 renders while frame k's group runs; per-frame render and gather times
+    assert "pipelined (2 slabs)" in r.stdout and "per frame: render" in r.stdout, r.stdout
     tex = as_texture(read_ppm(out))
     assert hashlib.sha256(tex.tobytes()).hexdigest() == digests["scene2_1920x1080_d0_rgba8_sha256"]
 

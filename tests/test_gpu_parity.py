@@ -288,8 +288,22 @@ def test_launch_camera_equals_device_camera_state(i, w, h):
     frames.append(f)
     for k, f in enumerate(frames):
         want = p.render_float(f)
-        assert bits_equal(a.render_float(f), want), (i, w, h, k)
+        # three renders of each frame on the context's stream: the camera's
+        # first frame computes its tile masks, the second stores them, the
+        # third reads them back (off-grid slabs and bands included)
+        for rep in range(3):
+            assert bits_equal(a.render_float(f), want), (i, w, h, k, rep)
         assert bits_equal(b.render_float(f), want), (i, w, h, k)
+    # host output in row chunks (each chunk a launch of its own), three times
+    a.set_option("host_chunk_mb", max(1e-4, w * h * 12 / 8 / 1048576.0 / 1.01))
+    try:
+        f = s.frame.copy()
+        f.cam_pos[1] += 0.25  # a camera new to the stream
+        want = p.render_float(f)
+        for rep in range(3):
+            assert bits_equal(a.render_float(f), want), (i, w, h, "chunked", rep)
+    finally:
+        a.set_option("host_chunk_mb", 8)
 
 
 def test_camera_buffer_after_bounce_frame(tmp_path):
