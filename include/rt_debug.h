@@ -59,6 +59,13 @@ int rt_debug_bvh_info(rt_ctx*, double* out, int n);
  * tests and inner nodes visited, summed.  RT_E_STATE without a BVH. */
 int rt_debug_bvh_rays(rt_ctx*, const float* rays, int n, int* out_idx, float* out_t, unsigned long long* tally2);
 
+/* The same rays walked by the wavefront's straggler path — the budgeted
+ * serial walk stopped after one step, then the wave-cooperative walk (one
+ * wave per ray, a shared LDS stack) — winners into out_idx / out_t (one per
+ * ray); compare with rt_debug_bvh_rays' brute force.  RT_E_STATE without a
+ * BVH. */
+int rt_debug_bvh_rays_wave(rt_ctx*, const float* rays, int n, int* out_idx, float* out_t);
+
 /* Run the wave-primitive self-test (wave min / max / sum, wave cones) over
  * `blocks` workgroups on `device`; *failures = lanes that disagreed. */
 int rt_debug_selftest(int device, int blocks, unsigned* failures);

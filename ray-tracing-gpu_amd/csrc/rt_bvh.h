@@ -100,6 +100,11 @@ __device__ __forceinline__ bool bvh_box(const float4 lo, const float4 hi, const 
     return !(t0 > t1) & !(t1 < kEps) & !(have & (t0 > bt));
 }
 
+__device__ __forceinline__ unsigned lane_rank_u(unsigned long long m)
+{
+    return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+}
+
 __device__ __forceinline__ bool finite3(const Vec3 v)
 {
     return (fabsf(v.x) <= 3.4e38f) & (fabsf(v.y) <= 3.4e38f) & (fabsf(v.z) <= 3.4e38f);
@@ -109,9 +114,13 @@ __device__ __forceinline__ bool finite3(const Vec3 v)
 // triangles through the BVH.  Same winner as closest_hit<false>: the file
 // order's first minimum is the lexicographic (t, file index) minimum, which
 // does not depend on the order the candidates are tested in.
-template <size_t WIN = kLdsWaveBytes>
+// BUDGET > 0 (the wavefront's trace kernel): a walk still running after that
+// many steps (inner nodes + leaves) stops with *straggled set and its
+// partial minimum in best_t / the return value — a valid starting bound for
+// bvh_walk_wave, which finishes it with the whole wave.
+template <size_t WIN = kLdsWaveBytes, int BUDGET = 0>
 __device__ __forceinline__ int closest_hit_bvh(const SceneDev& S, const Vec3 O, const Vec3 D, float& best_t,
-                                               Counters& cnt)
+                                               Counters& cnt, bool* straggled = nullptr)
 {
     float bt = -1.0f;
     int bi = -1;
@@ -147,8 +156,14 @@ __device__ __forceinline__ int closest_hit_bvh(const SceneDev& S, const Vec3 O, 
     } else {
         const Vec3 inv = make3(__builtin_amdgcn_rcpf(D.x), __builtin_amdgcn_rcpf(D.y), __builtin_amdgcn_rcpf(D.z));
         int* const stk = bvh_stack<WIN>();
-        int node = 0, sp = 0;
+        int node = 0, sp = 0, steps = 0;
         for (;;) {
+            if constexpr (BUDGET > 0) {
+                if (++steps > BUDGET) {
+                    *straggled = true;
+                    break;
+                }
+            }
             if (node >= 0) {
                 const float4* n = S.bvh_node + 4 * (size_t)node;
                 const float4 a0 = n[0], a1 = n[1], b0 = n[2], b1 = n[3];
@@ -190,6 +205,96 @@ __device__ __forceinline__ int closest_hit_bvh(const SceneDev& S, const Vec3 O, 
     }
     best_t = bt;
     return bi;
+}
+
+// Lexicographic (t, file index) minimum of the wave's lanes' candidates
+// (bi < 0: none), combined with the running (bt, bi): every lane gets it.
+__device__ __forceinline__ void wave_take_min(float lt, int li, float& bt, int& bi)
+{
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const float ot = __shfl_xor(lt, off, 64);
+        const int oi = __shfl_xor(li, off, 64);
+        if ((oi >= 0) & ((li < 0) | (ot < lt) | ((ot == lt) & (oi < li)))) {
+            lt = ot;
+            li = oi;
+        }
+    }
+    if ((li >= 0) & ((bi < 0) | (lt < bt) | ((lt == bt) & (li < bi)))) {
+        bt = lt;
+        bi = li;
+    }
+}
+
+// One ray's BVH walk by the whole wave (the stragglers of the budgeted
+// walk: a ray skimming the mesh whose walk would hold its wave for
+// thousands of dependent steps).  A shared stack of node references in LDS
+// (cap entries at stk): each round the lanes take up to 64 references off
+// its top — an inner node's two child boxes are tested (against the
+// wave's current minimum), the ones that pass are pushed; a leaf's
+// triangles are tested exactly — then one wave reduction updates the
+// minimum.  The same boxes, the same exact tests and the same lexicographic
+// minimum as the serial walk: only the order differs, which the minimum
+// does not see.  The rounds take at most cap - 32 - sp references, so the
+// stack never overflows (with one reference per round it grows by at most
+// the tree's depth, <= kBvhStack).  Wave-uniform: every lane calls it with
+// the same ray; (bt, bi) in: the partial minimum (planes, quadrics and the
+// triangles tested so far), out: the ray's minimum.
+__device__ __forceinline__ void bvh_walk_wave(const SceneDev& S, const Vec3 O, const Vec3 D, float& bt, int& bi,
+                                              int* __restrict__ stk, int cap, Counters& cnt)
+{
+    const int lane = (int)(threadIdx.x & 63);
+    const Vec3 inv = make3(__builtin_amdgcn_rcpf(D.x), __builtin_amdgcn_rcpf(D.y), __builtin_amdgcn_rcpf(D.z));
+    int sp = 1;
+    if (lane == 0) stk[0] = 0;
+    for (;;) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (sp == 0) break;
+        int take = min(64, min(sp, cap - 32 - sp));
+        if (take < 1) take = 1;
+        const int ref = lane < take ? stk[sp - take + lane] : 0;
+        const bool mine = lane < take;
+        sp -= take;
+        float lt = -1.0f;
+        int li = -1;
+        bool p0 = false, p1 = false;
+        int r0 = 0, r1 = 0;
+        const bool have = bi >= 0;
+        if (mine && ref >= 0) {
+            const float4* n = S.bvh_node + 4 * (size_t)ref;
+            const float4 a0 = n[0], a1 = n[1], b0 = n[2], b1 = n[3];
+            ++cnt.bnode;
+            r0 = __float_as_int(a1.w);
+            r1 = __float_as_int(b1.w);
+            float t0, t1;
+            p0 = bvh_box(a0, a1, O, inv, have, bt, t0);
+            p1 = bvh_box(b0, b1, O, inv, have, bt, t1);
+        } else if (mine) {
+            const unsigned enc = ~(unsigned)ref;
+            const int first = (int)(enc >> 4), count = (int)(enc & 15u) + 1;
+            for (int k = first; k < first + count; ++k) {
+                const float4* r = S.bvh_tri + 3 * (size_t)k;
+                const float4 a = r[0], b = r[1], c = r[2];
+                ++cnt.tri;
+                ++cnt.btri;
+                float t;
+                const bool ok = hit_triangle(make_float4(0.f, a.x, a.y, a.z), make_float4(a.w, b.x, b.y, b.z),
+                                             make_float4(b.w, c.x, 0.f, 0.f), O, D, t);
+                take_min(ok, t, __float_as_int(c.y), lt, li);
+            }
+        }
+        // every lane has read its reference before the pushes overwrite them
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const unsigned long long m0 = __ballot(p0), m1 = __ballot(p1);
+        if (p0) stk[sp + (int)lane_rank_u(m0)] = r0;
+        if (p1) stk[sp + __popcll(m0) + (int)lane_rank_u(m1)] = r1;
+        sp += __popcll(m0) + __popcll(m1);
+        wave_take_min(lt, li, bt, bi);
+    }
 }
 
 }  // namespace rt

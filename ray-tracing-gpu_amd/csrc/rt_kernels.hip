@@ -96,8 +96,70 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
         }
         const Vec3 P = O + t * D;
         const Color c = shade_local<LB, WAVE>(S, m, P, N, D, cnt, hit & live);
-        if constexpr ((WAVE & 512) != 0) deferred = wf_children(F, 0, hit & live, m, P, N, D, 1.0f, 1.0f, c, pix);
+        if constexpr ((WAVE & 512) != 0)
+            deferred = wf_children(F, 0, hit & live, m, P, N, D, 1.0f, 1.0f, c, pix, blockIdx.x + blockIdx.y * gridDim.x);
         return hit ? c : bg;
+    } else if constexpr ((WAVE & 1024) != 0) {
+        // Reflect-only scenes (no Kt can pass the gate: the host's kt_max <= 0
+        // with min_energy >= 0): every node has at most one child, the
+        // reflected ray, and its colour is acc + C_child * Kr (Scene.cpp:1787).
+        // The chain's (acc, Kr) pairs live in registers — a shift stack with
+        // compile-time indices, top at [0] — instead of the DFS's scratch
+        // frames; the fold runs bottom-up in the same order.
+        Color accs[MAXD];
+        float krs[MAXD];
+#pragma unroll
+        for (int k = 0; k < MAXD; ++k) {
+            accs[k] = Color{0.f, 0.f, 0.f};
+            krs[k] = 0.f;
+        }
+        int d = 0;  // nodes on the chain (pushed)
+        float energy = 1.0f;
+        Color ret = bg;
+        for (int lv = 0;; ++lv) {
+            float t;
+            int idx;
+            if (lv == 0)
+                idx = closest_hit_primary<(WAVE & 107)>(S, O, D, t, cnt, tile, T);
+            else if constexpr ((WAVE & 256) != 0)  // bounce rays through the BVH (rt_bvh.h)
+                idx = closest_hit_bvh(S, O, D, t, cnt);
+            else
+                idx = closest_hit<false>(S, O, D, t, cnt);
+            ret = bg;
+            if (idx < 0) break;
+            const Vec3 N = hit_normal(S, idx, O, D, t);
+            const Mat m = load_mat(S, idx);
+            const Vec3 P = O + t * D;
+            const Color acc = shade_local<LB, WAVE>(S, m, P, N, D, cnt);
+            // Scene.cpp:1779-1781 gate; bounces == lv
+            const float er = m.kr * energy;
+            const bool doR = er > F.min_energy && lv < F.max_bounces && lv < MAXD;
+            if (!doR) {
+                ret = acc;
+                break;
+            }
+#pragma unroll
+            for (int k = MAXD - 1; k > 0; --k) {
+                accs[k] = accs[k - 1];
+                krs[k] = krs[k - 1];
+            }
+            accs[0] = acc;
+            krs[0] = m.kr;
+            ++d;
+            ++cnt.bounce;
+            O = P;
+            D = reflect(D, N);  // Scene.cpp:1782-1788
+            energy = er;
+        }
+#pragma unroll
+        for (int k = 0; k < MAXD; ++k) {
+            if (k < d) {
+                Color a = accs[k];
+                a += ret * krs[k];  // Scene.cpp:1787
+                ret = a;
+            }
+        }
+        return ret;
     } else {
         Frame stk[MAXD];
         Refr rf[MAXD];
@@ -473,6 +535,36 @@ __global__ __launch_bounds__(64) void rt_bvh_rays_kernel(const SceneDev S, const
     atomicAdd(&tally[1], (unsigned long long)nodes);
 }
 
+// The wave-cooperative walk (rt_debug_bvh_rays_wave): one ray per wave, its
+// planes and quadrics and first BVH step by the budgeted serial walk (budget
+// 1: every ray straggles), the rest by bvh_walk_wave — as the wavefront's
+// straggler kernel finishes a walk.
+__global__ __launch_bounds__(64) void rt_bvh_wave_kernel(const SceneDev S, const float* __restrict__ rays, int n,
+                                                           int* __restrict__ out_idx, float* __restrict__ out_t)
+{
+    extern __shared__ float4 rt_lds_dyn[];
+    int* const base = reinterpret_cast<int*>(rt_lds_dyn);
+    const int i = (int)blockIdx.x;
+    if (i >= n) return;
+    const float* r = rays + 6 * (size_t)i;
+    const Vec3 O = make3(r[0], r[1], r[2]), D = make3(r[3], r[4], r[5]);
+    Counters cnt;
+    float bt = -1.0f;
+    int bi = -1;
+    bool str = false;
+    if ((threadIdx.x & 63) == 0) {
+        bi = closest_hit_bvh<kWfStragCap * sizeof(int), 1>(S, O, D, bt, cnt, &str);
+    }
+    bt = readlanef(bt, 0);
+    bi = __builtin_amdgcn_readlane(bi, 0);
+    str = __builtin_amdgcn_readlane((int)str, 0) != 0;
+    if (str) bvh_walk_wave(S, O, D, bt, bi, base, kWfStragCap, cnt);
+    if ((threadIdx.x & 63) == 0) {
+        out_idx[i] = bi;
+        out_t[i] = bt;
+    }
+}
+
 }  // namespace rt
 
 // ===================================================================== host
@@ -658,7 +750,8 @@ struct rt_ctx {
         void* mem = nullptr;      // one allocation: counters, then every level's arrays
         size_t bytes = 0;
         size_t px = 0;            // pixel capacity (level-0 nodes)
-        size_t cap[kWfMaxLevels + 1] = {};  // ray capacity per level
+        size_t cap[kWfMaxLevels + 1] = {};   // ray slots per level (level 0: pixels)
+        size_t pcap[kWfMaxLevels + 1] = {};  // parent-list slots per level
         WfDev dev{};
         hipEvent_t ev = nullptr;  // after the last wavefront frame
         hipStream_t last = nullptr;
@@ -1778,8 +1871,11 @@ static KernelPick kpick(unsigned lds)
 // (camera buffer bit 8 — a no-op when S.cb_tiles_x is 0 —, light buffer bit
 // 4, wave culling 1 or clustered 2); its waves carry the traversal stacks in
 // LDS after the staging window.
+// chain: no refracted ray can pass its gate (reflect-only scenes): the
+// bounce kernels keep the chain in registers (WAVE bit 1024).
 template <bool COUNT>
-static KernelPick pick_kernel(int depth, int n_tri, int n_lights, bool lbuf, bool cbuf, int bvh_depth = 0)
+static KernelPick pick_kernel(int depth, int n_tri, int n_lights, bool lbuf, bool cbuf, int bvh_depth = 0,
+                              bool chain = false)
 {
     const bool bvh = bvh_depth > 0;
     const unsigned win = (unsigned)kLdsWaveBytes;
@@ -1795,14 +1891,17 @@ static KernelPick pick_kernel(int depth, int n_tri, int n_lights, bool lbuf, boo
     if (depth == 0 && n_lights > 1) return kpick<0, 3, 0, COUNT>(0);
     const unsigned bl = (unsigned)(kLdsWaveBytes + (size_t)bvh_depth * 64 * sizeof(int));
     if (bvh && lbuf && n_tri > 0) {
-#define RT_PICK_BVH(N)                                                                                   \
-    if (depth <= N)                                                                                      \
-        return n_tri > kClusterMinTriangles ? kpick<N, 1, 270, COUNT>(bl) : kpick<N, 1, 269, COUNT>(bl);
+#define RT_PICK_BVH(N)                                                                                     \
+    if (depth <= N) {                                                                                      \
+        if (chain)                                                                                         \
+            return n_tri > kClusterMinTriangles ? kpick<N, 1, 1294, COUNT>(bl) : kpick<N, 1, 1293, COUNT>(bl); \
+        return n_tri > kClusterMinTriangles ? kpick<N, 1, 270, COUNT>(bl) : kpick<N, 1, 269, COUNT>(bl);   \
+    }
         RT_STACK_DEPTHS(RT_PICK_BVH)
 #undef RT_PICK_BVH
     }
 #define RT_PICK(N) \
-    if (depth <= N) return kpick<N, 1, 0, COUNT>(0);
+    if (depth <= N) return chain ? kpick<N, 1, 1024, COUNT>(0) : kpick<N, 1, 0, COUNT>(0);
     RT_STACK_DEPTHS(RT_PICK)
 #undef RT_PICK
     KernelPick none;
@@ -1973,6 +2072,10 @@ static bool bvh_on(const rt_ctx* c, int depth, bool lbuf)
 {
     return depth > 0 && c->d_bvh_node && c->opt_bvh && lbuf && c->n_tri > 0;
 }
+// No refracted ray can pass its gate (Scene.cpp:1791: Kt * energy >
+// min_energy with every Kt <= 0 and min_energy >= 0): the bounce tree of
+// every pixel is a chain of reflections.
+static bool reflect_chain(const rt_ctx* c, const rt_frame* f) { return !(c->kt_max > 0.0f) && f->min_energy >= 0.0f; }
 // The frame's camera rays may walk a camera buffer: the depth-0 kernels and
 // the BVH kernels.
 static bool cam_lists(const rt_ctx* c, int depth, bool lbuf) { return depth == 0 || bvh_on(c, depth, lbuf); }
@@ -2058,24 +2161,48 @@ static int wf_branch(const rt_ctx* c) { return (c->kr_max > 0.0f ? 1 : 0) + (c->
 #ifndef RT_WF_MAX_GB
 #define RT_WF_MAX_GB 32.0
 #endif
-// Bytes of the queues for px pixels and `levels` bounce levels: level 0
-// node records (32 B) + parent list (4 B) per pixel; level L >= 1 per ray
-// (px * branch^L rays at most): the ray (32 B), its colour (16 B), and but
-// for the deepest level a node record (32 B) and a parent slot (4 B).
-static size_t wf_bytes(size_t px, int levels, int branch, size_t* cap)
+// The queues' layout for a frame of `tiles` level-0 tiles (one wave each)
+// over px pixels, `levels` bounce levels, `branch` children per node at most
+// (rt_layout.h WfDev): segment capacities that no wave's appends can
+// overflow — segment s of level L + 1 receives the children of level L's
+// chunks c = s (mod kWfSeg), at most 64 * branch each — then the bytes:
+// counters; level-0 node records (32 B) per pixel and its parent list;
+// per level L >= 1 the rays (32 B), colours (16 B) and, but for the deepest
+// level, node records (32 B) and the parent list; the hit records (8 B) and
+// straggler queue (16 B) of the largest level.
+struct WfLayout {
+    size_t cap[kWfMaxLevels + 1] = {}, pcap[kWfMaxLevels + 1] = {};
+    unsigned seg[kWfMaxLevels + 1] = {}, pseg[kWfMaxLevels + 1] = {};
+    size_t most = 0, bytes = 0;
+};
+static WfLayout wf_layout(size_t tiles, size_t px, int levels, int branch)
 {
-    size_t tot = 256, n = px, most = 0;
-    cap[0] = px;
-    tot += px * (32 + 4);
-    for (int L = 1; L <= levels; ++L) {
-        n *= (size_t)branch;
-        cap[L] = n;
-        most = std::max(most, n);
-        tot += n * (32 + 16) + (L < levels ? n * (32 + 4) : 0);
-        tot = (tot + 255) & ~(size_t)255;
+    WfLayout w;
+    auto up = [](size_t a, size_t b) { return (a + b - 1) / b; };
+    size_t chunks = tiles;
+    for (int L = 0; L <= levels; ++L) {
+        if (L > 0) {
+            w.seg[L] = (unsigned)(up(chunks, kWfSeg) * 64 * (size_t)branch);
+            w.cap[L] = (size_t)kWfSeg * w.seg[L];
+            chunks = up(w.cap[L], 64);
+            w.most = std::max(w.most, w.cap[L]);
+        }
+        if (L < levels) {
+            w.pseg[L] = (unsigned)(up(chunks, kWfSeg) * 64);
+            w.pcap[L] = (size_t)kWfSeg * w.pseg[L];
+        }
     }
-    return tot + most * 8;  // the hit records of the level being shaded
+    auto a = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    size_t tot = a(kWfCountBytes) + a(px * 32) + a(w.pcap[0] * 4);
+    for (int L = 1; L <= levels; ++L) {
+        tot += a(w.cap[L] * 32) + a(w.cap[L] * 16);
+        if (L < levels) tot += a(w.cap[L] * 32) + a(w.pcap[L] * 4);
+    }
+    w.bytes = tot + a(w.most * 8) + a(w.most * 16);
+    return w;
 }
+
+static size_t frame_tiles(const rt_frame* f, int rows) { return (size_t)((f->width + 7) / 8) * (size_t)((rows + 7) / 8); }
 
 // Would frame f (depth `depth`, its kernel a BVH kernel) render as a
 // wavefront?  RT_OPT_WAVEFRONT, at most kWfMaxLevels levels, a single
@@ -2083,57 +2210,56 @@ static size_t wf_bytes(size_t px, int levels, int branch, size_t* cap)
 static bool wf_fits(const rt_ctx* c, const rt_frame* f, int depth, int rows)
 {
     if (!c->opt_wavefront || depth < 1 || depth > kWfMaxLevels || wf_branch(c) == 0) return false;
-    size_t cap[kWfMaxLevels + 1];
-    return (double)wf_bytes((size_t)rows * f->width, depth, wf_branch(c), cap) <= RT_WF_MAX_GB * 1073741824.0;
+    const WfLayout w = wf_layout(frame_tiles(f, rows), (size_t)rows * f->width, depth, wf_branch(c));
+    return (double)w.bytes <= RT_WF_MAX_GB * 1073741824.0;
 }
 
-// The queues for px pixels / `levels` levels (grown, never shrunk; not
-// while capturing).  Fills c->wf.dev.
-static int wf_ensure(rt_ctx* c, size_t px, int levels, bool capturing, bool* ok)
+// The queues for frame f (grown, never shrunk; not while capturing).
+// Fills c->wf.dev.
+static int wf_ensure(rt_ctx* c, const rt_frame* f, int rows, int levels, bool capturing, bool* ok)
 {
     rt_ctx::WfBuf& W = c->wf;
-    size_t cap[kWfMaxLevels + 1] = {};
-    const int br = wf_branch(c);
-    const size_t bytes = wf_bytes(px, levels, br, cap);
+    const size_t px = (size_t)rows * f->width;
+    const WfLayout w = wf_layout(frame_tiles(f, rows), px, levels, wf_branch(c));
     *ok = false;
-    if (bytes > W.bytes) {
+    if (w.bytes > W.bytes) {
         if (capturing) return RT_OK;  // (the frame renders by the BVH megakernel)
         free_later(c, W.mem);  // an enqueued frame may still use the old queues
         W.mem = nullptr;
         W.bytes = 0;
-        HIP_TRY(c, hipMalloc(&W.mem, bytes));
-        W.bytes = bytes;
-        W.px = 0;
+        HIP_TRY(c, hipMalloc(&W.mem, w.bytes));
+        W.bytes = w.bytes;
     }
     if (!W.ev) HIP_TRY(c, hipEventCreateWithFlags(&W.ev, hipEventDisableTiming));
     char* p = (char*)W.mem;
+    auto take = [&](size_t bytes) {
+        char* q = p;
+        p += (bytes + 255) & ~(size_t)255;
+        return q;
+    };
     WfDev& d = W.dev;
     d = WfDev{};
-    d.count = (unsigned*)p;
-    p += 256;
-    d.node[0] = (float4*)p;
-    p += px * 32;
-    d.plist[0] = (unsigned*)p;
-    p += px * 4;
-    size_t off = (size_t)(p - (char*)W.mem);
-    off = (off + 255) & ~(size_t)255;
+    d.count = (unsigned*)take(kWfCountBytes);
+    d.node[0] = (float4*)take(px * 32);
+    d.plist[0] = (unsigned*)take(w.pcap[0] * 4);
+    d.pseg[0] = w.pseg[0];
     for (int L = 1; L <= levels; ++L) {
-        p = (char*)W.mem + off;
-        d.ray[L] = (float4*)p;
-        p += cap[L] * 32;
-        d.res[L] = (float4*)p;
-        p += cap[L] * 16;
+        d.ray[L] = (float4*)take(w.cap[L] * 32);
+        d.res[L] = (float4*)take(w.cap[L] * 16);
+        d.seg[L] = w.seg[L];
         if (L < levels) {
-            d.node[L] = (float4*)p;
-            p += cap[L] * 32;
-            d.plist[L] = (unsigned*)p;
-            p += cap[L] * 4;
+            d.node[L] = (float4*)take(w.cap[L] * 32);
+            d.plist[L] = (unsigned*)take(w.pcap[L] * 4);
+            d.pseg[L] = w.pseg[L];
         }
-        off = ((size_t)(p - (char*)W.mem) + 255) & ~(size_t)255;
     }
-    d.hit = (float2*)((char*)W.mem + off);
+    d.hit = (float2*)take(w.most * 8);
+    d.strag = (int4*)take(w.most * 16);
     d.levels = levels;
-    for (int L = 0; L <= levels; ++L) W.cap[L] = cap[L];
+    for (int L = 0; L <= levels; ++L) {
+        W.cap[L] = L == 0 ? px : w.cap[L];
+        W.pcap[L] = w.pcap[L];
+    }
     W.px = px;
     *ok = true;
     return RT_OK;
@@ -2157,6 +2283,7 @@ static int wf_levels(rt_ctx* c, const SceneDev& S, const FrameDev& F, int levels
 {
     const bool big = c->n_tri > kClusterMinTriangles;
     const void* kt = count ? (const void*)&rt_wf_trace<true> : (const void*)&rt_wf_trace<false>;
+    const void* kg = count ? (const void*)&rt_wf_straggle<true> : (const void*)&rt_wf_straggle<false>;
     const void* ks = big ? (count ? (const void*)&rt_wf_shade<6, true> : (const void*)&rt_wf_shade<6, false>)
                          : (count ? (const void*)&rt_wf_shade<5, true> : (const void*)&rt_wf_shade<5, false>);
     const unsigned lds_t = (unsigned)((size_t)c->bvh_depth * 64 * sizeof(int));
@@ -2170,10 +2297,12 @@ static int wf_levels(rt_ctx* c, const SceneDev& S, const FrameDev& F, int levels
         int Lv = L;
         void* args[] = {(void*)&S, (void*)&Fl, (void*)&Lv, (void*)&stats};
         HIP_TRY(c, hipLaunchKernel(kt, dim3(gt), dim3(64), args, lds_t, st));
+        HIP_TRY(c, hipLaunchKernel(kg, dim3((unsigned)c->n_cu * 4), dim3(64), args,
+                                   (unsigned)(kWfStragCap * sizeof(int)), st));
         HIP_TRY(c, hipLaunchKernel(ks, dim3(gs), dim3(64), args, lds_s, st));
     }
     for (int L = levels - 1; L >= 0; --L) {
-        const unsigned g = (unsigned)std::min<size_t>((c->wf.cap[L] + 255) / 256, (size_t)c->n_cu * 4);
+        const unsigned g = (unsigned)std::min<size_t>((c->wf.pcap[L] + 255) / 256, (size_t)c->n_cu * 4);
         hipLaunchKernelGGL(rt_wf_fold, dim3(std::max(1u, g)), dim3(256), 0, st, F, L, rgba, rgbf);
         HIP_TRY(c, hipGetLastError());
     }
@@ -2224,13 +2353,15 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
     bool wf = bvh && rows > 0 && !capturing && wf_fits(c, f, depth, rows);
     if (wf) {
         bool ok = false;
-        if (int rc = wf_ensure(c, (size_t)rows * f->width, depth, capturing, &ok)) return rc;
+        if (int rc = wf_ensure(c, f, rows, depth, capturing, &ok)) return rc;
         wf = ok;
     }
     const bool count = (f->flags & RT_FLAG_STATS) != 0;
     const KernelPick kp = wf ? (count ? pick_wf0<true>(c->n_tri, cbuf) : pick_wf0<false>(c->n_tri, cbuf))
-                             : (count ? pick_kernel<true>(depth, c->n_tri, c->n_lights, lbuf, cbuf, bvh ? c->bvh_depth : 0)
-                                      : pick_kernel<false>(depth, c->n_tri, c->n_lights, lbuf, cbuf, bvh ? c->bvh_depth : 0));
+                             : (count ? pick_kernel<true>(depth, c->n_tri, c->n_lights, lbuf, cbuf,
+                                                          bvh ? c->bvh_depth : 0, reflect_chain(c, f))
+                                      : pick_kernel<false>(depth, c->n_tri, c->n_lights, lbuf, cbuf,
+                                                           bvh ? c->bvh_depth : 0, reflect_chain(c, f)));
     if (!kp.k) {
         c->err = "reachable bounce depth " + std::to_string(depth) + " exceeds the compiled stack (32)";
         return RT_E_UNSUPPORTED;
@@ -2265,7 +2396,7 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
     if (wf) {
         rt_ctx::WfBuf& W = c->wf;
         if (W.pending && W.last != st) HIP_TRY(c, hipStreamWaitEvent(st, W.ev, 0));
-        HIP_TRY(c, hipMemsetAsync(W.dev.count, 0, 256, st));
+        HIP_TRY(c, hipMemsetAsync(W.dev.count, 0, kWfCountBytes, st));
     }
     if (nch <= 1) {
         if (int rc = launch_trace(c, kp, tiny, f->flags & RT_FLAG_STATS, S, F, f->width, rows, rgba_dev, rgb_dev, stats,
@@ -2494,7 +2625,8 @@ RT_EXPORT int rt_render_sequence_async(rt_ctx* c, const rt_frame* frames, int32_
         if (c->n_tri > 0 && !tiny) {
             if (int rc = camera_records(c, f->cam_pos, fs, cbuf, q.tricam, q.cone_cam, q.uni, q.clu_cam)) return rc;
         }
-        const KernelPick kp = pick_kernel<false>(depth, c->n_tri, c->n_lights, lbuf, cbuf, bvh ? c->bvh_depth : 0);
+        const KernelPick kp =
+            pick_kernel<false>(depth, c->n_tri, c->n_lights, lbuf, cbuf, bvh ? c->bvh_depth : 0, reflect_chain(c, f));
         SceneDev S = scene_dev(c, lbuf, false);
         S.tricam = q.tricam;
         S.cone_cam = q.cone_cam;
@@ -2822,6 +2954,43 @@ RT_EXPORT int rt_debug_bvh_rays(rt_ctx* c, const float* rays, int n, int* out_id
     hipFree(d_idx);
     hipFree(d_t);
     hipFree(d_tally);
+    return rc;
+}
+
+RT_EXPORT int rt_debug_bvh_rays_wave(rt_ctx* c, const float* rays, int n, int* out_idx, float* out_t)
+{
+    if (!c || !rays || n < 0 || !out_idx || !out_t) return RT_E_ARG;
+    if (c->cpu) return not_cpu(c);
+    if (!c->uploaded || !c->d_bvh_node) {
+        c->err = "no bounce-ray BVH";
+        return RT_E_STATE;
+    }
+    HIP_TRY(c, hipSetDevice(c->device));
+    if (int rc = sync_all(c)) return rc;
+    if (n == 0) return RT_OK;
+    float* d_rays = nullptr;
+    int* d_idx = nullptr;
+    float* d_t = nullptr;
+    int rc = RT_OK;
+    auto chk = [&](hipError_t e, const char* what) {
+        if (e != hipSuccess && rc == RT_OK) rc = hip_fail(c, e, what);
+        return rc == RT_OK;
+    };
+    if (chk(hipMalloc(&d_rays, (size_t)n * 6 * sizeof(float)), "hipMalloc") &&
+        chk(hipMalloc(&d_idx, (size_t)n * sizeof(int)), "hipMalloc") &&
+        chk(hipMalloc(&d_t, (size_t)n * sizeof(float)), "hipMalloc") &&
+        chk(hipMemcpy(d_rays, rays, (size_t)n * 6 * sizeof(float), hipMemcpyHostToDevice), "hipMemcpy")) {
+        const SceneDev S = scene_dev(c, false, false);
+        // the shared stack, then lane 0's serial stack (one step: a row)
+        const unsigned lds = (unsigned)(kWfStragCap * sizeof(int) + 64 * sizeof(int) * (size_t)c->bvh_depth);
+        hipLaunchKernelGGL(rt_bvh_wave_kernel, dim3((unsigned)n), dim3(64), lds, c->stream, S, d_rays, n, d_idx, d_t);
+        if (chk(hipGetLastError(), "rt_bvh_wave_kernel") && chk(hipStreamSynchronize(c->stream), "sync") &&
+            chk(hipMemcpy(out_idx, d_idx, (size_t)n * sizeof(int), hipMemcpyDeviceToHost), "hipMemcpy"))
+            chk(hipMemcpy(out_t, d_t, (size_t)n * sizeof(float), hipMemcpyDeviceToHost), "hipMemcpy");
+    }
+    hipFree(d_rays);
+    hipFree(d_idx);
+    hipFree(d_t);
     return rc;
 }
 

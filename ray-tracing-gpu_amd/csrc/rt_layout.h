@@ -133,18 +133,34 @@ struct SceneDev {
 // energy]) and their colours (1 float4); level L >= 0 the node records of
 // the rays (level 0: pixels) that spawned children (2 float4: [acc kr]
 // [kt cR cT -], by ray / pixel index) and the list of those parents.
-// count[L]: rays of level L; count[kWfMaxLevels + 1 + L]: parents of
-// level L.  levels = 0: not a wavefront frame.
+// Rays and parents are appended in kWfSeg segments, each with a counter of
+// its own on a 128-byte line of its own (one global counter serialised
+// every wave's atomic on one L2 line): a wave appends to segment chunk %
+// kWfSeg (chunk = its 64-ray chunk or tile), and segment s of level L
+// starts at s * seg[L] (rays) / s * pseg[L] (parents), capacities the host
+// sized so that no segment can overflow.  A consumer maps a compacted index
+// to its slot through the 16 counts' prefix sums (wf_slot).
+// levels = 0: not a wavefront frame.
 constexpr int kWfMaxLevels = 8;
+constexpr int kWfSeg = 16;
+constexpr int kWfCntStride = 32;  // u32 words between counters (128 bytes)
 struct WfDev {
     float4* ray[kWfMaxLevels + 1];
     float4* res[kWfMaxLevels + 1];
     float4* node[kWfMaxLevels + 1];
     unsigned* plist[kWfMaxLevels + 1];
-    float2* hit;      // the level being shaded: [file index (int bits), t] per ray
-    unsigned* count;
+    unsigned seg[kWfMaxLevels + 1];   // ray slots per segment, level L >= 1
+    unsigned pseg[kWfMaxLevels + 1];  // parent slots per segment, level L >= 0
+    float2* hit;      // the level being shaded: [file index (int bits), t] per ray slot
+    int4* strag;      // the level's straggling walks: [ray slot, partial t (bits), partial index, -]
+    unsigned* count;  // counters, kWfCntStride words apart: wf_rays / wf_pars / wf_strag
     int levels;
 };
+// counter of segment s of level L's rays / parents; level L's stragglers
+__host__ __device__ inline int wf_rays(int L, int s) { return (L * kWfSeg + s) * kWfCntStride; }
+__host__ __device__ inline int wf_pars(int L, int s) { return ((kWfMaxLevels + 1 + L) * kWfSeg + s) * kWfCntStride; }
+__host__ __device__ inline int wf_strag(int L) { return (2 * (kWfMaxLevels + 1) * kWfSeg + L) * kWfCntStride; }
+constexpr size_t kWfCountBytes = (size_t)(2 * (kWfMaxLevels + 1) * kWfSeg + kWfMaxLevels + 1) * kWfCntStride * 4;
 
 struct FrameDev {
     float cam[3];

@@ -27,11 +27,45 @@
 
 #pragma clang fp contract(off)
 
+// Steps (inner nodes + leaves) a lane's BVH walk may take in the trace
+// kernel before it is handed to the straggler kernel.
+#ifndef RT_WF_BUDGET
+#define RT_WF_BUDGET 256
+#endif
+
 namespace rt {
 
 __device__ __forceinline__ unsigned lane_rank(unsigned long long m)
 {
     return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+}
+
+// A segmented queue as the consumer sees it: the prefix sums of its
+// kWfSeg segment counts (wave-uniform: scalar loads of the counters the
+// previous launch left) and the slot of compacted index x.
+struct WfQueue {
+    unsigned pre[kWfSeg + 1];
+    unsigned seg;
+};
+__device__ __forceinline__ WfQueue wf_queue(const unsigned* count, int first_word, unsigned seg)
+{
+    WfQueue q;
+    q.seg = seg;
+    q.pre[0] = 0u;
+#pragma unroll
+    for (int k = 0; k < kWfSeg; ++k) q.pre[k + 1] = q.pre[k] + count[first_word + k * kWfCntStride];
+    return q;
+}
+__device__ __forceinline__ unsigned wf_slot(const WfQueue& q, unsigned x)
+{
+    unsigned p = 0u, s = 0u;
+#pragma unroll
+    for (int k = 1; k < kWfSeg; ++k) {
+        const bool ge = x >= q.pre[k];
+        p = ge ? q.pre[k] : p;
+        s = ge ? (unsigned)k : s;
+    }
+    return s * q.seg + (x - p);
 }
 
 // The children of a level-L node (act: a ray of level L that hit a surface
@@ -40,10 +74,11 @@ __device__ __forceinline__ unsigned lane_rank(unsigned long long m)
 // ray for level L >= 1).  Gates of Scene.cpp:1780 / :1791 (bounces = L);
 // reflected rays keep CRayon's default IOR 0 (:1782-1788), refracted ones
 // Scene.cpp:1793-1822.  Returns true when the node spawned a child (its
-// colour then comes from rt_wf_fold).
+// colour then comes from rt_wf_fold).  chunk: the wave's 64-ray chunk (or
+// tile) index, which picks its segments.
 __device__ __forceinline__ bool wf_children(const FrameDev& F, int L, bool act, const Mat& m, const Vec3 P,
                                             const Vec3 N, const Vec3 D, float rior, float energy, const Color acc,
-                                            unsigned self)
+                                            unsigned self, unsigned chunk)
 {
     const float er = m.kr * energy;
     const float et = m.kt * energy;
@@ -56,13 +91,14 @@ __device__ __forceinline__ bool wf_children(const FrameDev& F, int L, bool act, 
     // order, reflected children first
     const int lead = (int)__builtin_ctzll(__ballot(true));
     const int lane = (int)(threadIdx.x & 63);
+    const int sg = (int)(chunk % (unsigned)kWfSeg);
     unsigned base = 0u, pbase = 0u;
     if (lane == lead) {
-        base = atomicAdd(&F.wf.count[L + 1], (unsigned)(__popcll(bR) + __popcll(bT)));
-        pbase = atomicAdd(&F.wf.count[kWfMaxLevels + 1 + L], (unsigned)__popcll(bP));
+        base = atomicAdd(&F.wf.count[wf_rays(L + 1, sg)], (unsigned)(__popcll(bR) + __popcll(bT)));
+        pbase = atomicAdd(&F.wf.count[wf_pars(L, sg)], (unsigned)__popcll(bP));
     }
-    base = (unsigned)__builtin_amdgcn_readlane((int)base, lead);
-    pbase = (unsigned)__builtin_amdgcn_readlane((int)pbase, lead);
+    base = (unsigned)__builtin_amdgcn_readlane((int)base, lead) + (unsigned)sg * F.wf.seg[L + 1];
+    pbase = (unsigned)__builtin_amdgcn_readlane((int)pbase, lead) + (unsigned)sg * F.wf.pseg[L];
     int cR = -1, cT = -1;
     float4* const q = F.wf.ray[L + 1];
     if (doR) {
@@ -123,33 +159,77 @@ template <bool COUNT>
 __global__ __launch_bounds__(64) void rt_wf_trace(const SceneDev S, const FrameDev F, int L,
                                                   StatsDev* __restrict__ stats)
 {
-    const unsigned n = F.wf.count[L];
+    const WfQueue Q = wf_queue(F.wf.count, wf_rays(L, 0), F.wf.seg[L]);
+    const unsigned n = Q.pre[kWfSeg];
     const float4* __restrict__ q = F.wf.ray[L];
     Counters cnt;
     for (unsigned base = blockIdx.x * 64u; base < n; base += gridDim.x * 64u) {
-        const unsigned i = base + (threadIdx.x & 63u);
-        if (i < n) {
+        const unsigned x = base + (threadIdx.x & 63u);
+        if (x < n) {
+            const unsigned i = wf_slot(Q, x);
             const float4 r0 = q[2 * (size_t)i], r1 = q[2 * (size_t)i + 1];
             ++cnt.bounce;
             float t;
-            const int idx = closest_hit_bvh<0>(S, make3(r0.x, r0.y, r0.z), make3(r1.x, r1.y, r1.z), t, cnt);
-            F.wf.hit[i] = make_float2(__int_as_float(idx), t);
+            bool str = false;
+            const int idx =
+                closest_hit_bvh<0, RT_WF_BUDGET>(S, make3(r0.x, r0.y, r0.z), make3(r1.x, r1.y, r1.z), t, cnt, &str);
+            // a walk past the budget goes to the straggler queue with its
+            // partial minimum (rt_wf_straggle finishes it with a whole wave)
+            const unsigned long long bs = __ballot(str);
+            if (bs) {
+                const int lead = (int)__builtin_ctzll(__ballot(true));
+                unsigned sb = 0u;
+                if ((int)(threadIdx.x & 63) == lead) sb = atomicAdd(&F.wf.count[wf_strag(L)], (unsigned)__popcll(bs));
+                sb = (unsigned)__builtin_amdgcn_readlane((int)sb, lead);
+                if (str) F.wf.strag[sb + lane_rank(bs)] = make_int4((int)i, __float_as_int(t), idx, 0);
+            }
+            if (!str) F.wf.hit[i] = make_float2(__int_as_float(idx), t);
         }
     }
     if (COUNT && (F.flags & RT_FLAG_STATS)) wf_tally<COUNT>(cnt, stats);
+}
+
+// The straggling walks of level L, one ray per wave (bvh_walk_wave: the
+// wave's LDS stack of kWfStragCap references).
+constexpr int kWfStragCap = 4096;
+template <bool COUNT>
+__global__ __launch_bounds__(64) void rt_wf_straggle(const SceneDev S, const FrameDev F, int L,
+                                                     StatsDev* __restrict__ stats)
+{
+    extern __shared__ float4 rt_lds_dyn[];
+    int* const stk = reinterpret_cast<int*>(rt_lds_dyn);
+    const unsigned n = F.wf.count[wf_strag(L)];
+    const float4* __restrict__ q = F.wf.ray[L];
+    Counters cnt;
+    for (unsigned j = blockIdx.x; j < n; j += gridDim.x) {
+        const int4 rec = F.wf.strag[j];
+        const unsigned i = (unsigned)rec.x;
+        const float4 r0 = q[2 * (size_t)i], r1 = q[2 * (size_t)i + 1];
+        float bt = __int_as_float(rec.y);
+        int bi = rec.z;
+        bvh_walk_wave(S, make3(r0.x, r0.y, r0.z), make3(r1.x, r1.y, r1.z), bt, bi, stk, kWfStragCap, cnt);
+        if ((threadIdx.x & 63) == 0) F.wf.hit[i] = make_float2(__int_as_float(bi), bt);
+    }
+    if (COUNT && (F.flags & RT_FLAG_STATS)) {
+        // the lanes tally the work they did; the wave's one ray counts once
+        cnt.bounce = 0;
+        wf_tally<COUNT>(cnt, stats);
+    }
 }
 
 template <int WAVE, bool COUNT>
 __global__ __launch_bounds__(64) void rt_wf_shade(const SceneDev S, const FrameDev F, int L,
                                                   StatsDev* __restrict__ stats)
 {
-    const unsigned n = F.wf.count[L];
+    const WfQueue Q = wf_queue(F.wf.count, wf_rays(L, 0), F.wf.seg[L]);
+    const unsigned n = Q.pre[kWfSeg];
     const Color bg{F.bg[0], F.bg[1], F.bg[2]};
     Counters cnt;
     const float4* __restrict__ q = F.wf.ray[L];
     for (unsigned base = blockIdx.x * 64u; base < n; base += gridDim.x * 64u) {
-        const unsigned i = base + (threadIdx.x & 63u);
-        if (i < n) {
+        const unsigned x = base + (threadIdx.x & 63u);
+        if (x < n) {
+            const unsigned i = wf_slot(Q, x);
             const float2 h = F.wf.hit[i];
             const int idx = __float_as_int(h.x);
             Color res = bg;
@@ -166,7 +246,7 @@ __global__ __launch_bounds__(64) void rt_wf_shade(const SceneDev S, const FrameD
 #else
                 res = shade_local<1, WAVE>(S, m, P, N, D, cnt);
 #endif
-                parent = wf_children(F, L, true, m, P, N, D, r0.w, r1.w, res, i);
+                parent = wf_children(F, L, true, m, P, N, D, r0.w, r1.w, res, i, base / 64u);
             }
             if (!parent) F.wf.res[L][i] = make_float4(res.r, res.g, res.b, 0.0f);
         }
@@ -179,10 +259,11 @@ __global__ __launch_bounds__(64) void rt_wf_shade(const SceneDev S, const FrameD
 __global__ __launch_bounds__(256) void rt_wf_fold(const FrameDev F, int L, unsigned* __restrict__ rgba,
                                                   float* __restrict__ rgbf)
 {
-    const unsigned n = F.wf.count[kWfMaxLevels + 1 + L];
+    const WfQueue Q = wf_queue(F.wf.count, wf_pars(L, 0), F.wf.pseg[L]);
+    const unsigned n = Q.pre[kWfSeg];
     const float4* __restrict__ child = F.wf.res[L + 1];
     for (unsigned j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
-        const unsigned i = F.wf.plist[L][j];
+        const unsigned i = F.wf.plist[L][wf_slot(Q, j)];
         const float4 a = F.wf.node[L][2 * (size_t)i], b = F.wf.node[L][2 * (size_t)i + 1];
         Color c{a.x, a.y, a.z};
         const int cR = __float_as_int(b.y), cT = __float_as_int(b.z);

@@ -88,7 +88,8 @@ def test_reflective_heightfield_matches_reference(hfr, hfr_golden, size, wavefro
     if wavefront:  # level 0 = the big-list depth-0 kernel emitting children, then the levels
         assert st.kernel.startswith("wavefront rt_trace_kernel<0,1,526>"), st.kernel
     else:
-        assert st.kernel.endswith(",1,270>"), st.kernel  # the BVH megakernel ran
+        # the BVH megakernel ran (reflect-only: its chain variant, WAVE bit 1024)
+        assert st.kernel.endswith(",1,1294>"), st.kernel
     assert st.bounce_rays > 0
     # bounce rays test <= 1% of the 50,000 triangles each
     assert st.bounce_triangle_tests <= 0.01 * 50_000 * st.bounce_rays, (st.bounce_triangle_tests, st.bounce_rays)
@@ -190,7 +191,8 @@ def test_wavefront_stats_count_the_bounce_rays(hfr):
         out[wf] = (st.primary_rays, st.bounce_rays, st.shadow_rays, st.bounce_triangle_tests, st.bvh_nodes_visited)
     ctx.set_option("wavefront", 1)
     assert out[1][:3] == out[0][:3]  # the same rays, however scheduled
-    assert out[1][3] == out[0][3] and out[1][4] == out[0][4]  # the same walks, ray by ray
+    # the same walks but for the stragglers the wave finishes together
+    assert out[0][3] <= out[1][3] <= 1.5 * out[0][3], out
 
 
 def _rays_on_mesh(rng, s, n):
@@ -273,6 +275,18 @@ def _check_rays(ctx, O, D):
     return idx, t, tally
 
 
+def _check_rays_wave(ctx, O, D):
+    L = rt_amd.lib()
+    L.rt_debug_bvh_rays_wave.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                         ctypes.c_void_p]
+    rays = np.ascontiguousarray(np.concatenate([O, D], 1).astype(np.float32))
+    n = rays.shape[0]
+    idx = np.zeros(n, np.int32)
+    t = np.zeros(n, np.float32)
+    assert L.rt_debug_bvh_rays_wave(ctx._h, rays.ctypes.data, n, idx.ctypes.data, t.ctypes.data) == 0, ctx._err()
+    return idx, t
+
+
 def test_bvh_walk_equals_brute_force_on_adversarial_rays(hfr):
     ctx, get = hfr
     s = get(1920, 1080, 3)
@@ -281,6 +295,10 @@ def test_bvh_walk_equals_brute_force_on_adversarial_rays(hfr):
         same = (idx[:, 0] == idx[:, 1]) & (t[:, 0].view(np.uint32) == t[:, 1].view(np.uint32))
         bad = np.nonzero(~same)[0]
         assert bad.size == 0, (name, bad[:5], idx[bad[:5]], t[bad[:5]])
+        # the wave-cooperative walk (the wavefront's stragglers) on the first 4,096
+        wi, wt = _check_rays_wave(ctx, O[:4096], D[:4096])
+        same = (wi == idx[:4096, 1]) & (wt.view(np.uint32) == t[:4096, 1].view(np.uint32))
+        assert same.all(), (name, np.nonzero(~same)[0][:5])
         if name not in ("degenerate",):
             hits = int((idx[:, 1] >= 0).sum())
             assert hits > 0, name
