@@ -156,15 +156,19 @@ __device__ __forceinline__ int closest_hit_bvh(const SceneDev& S, const Vec3 O, 
     } else {
         const Vec3 inv = make3(__builtin_amdgcn_rcpf(D.x), __builtin_amdgcn_rcpf(D.y), __builtin_amdgcn_rcpf(D.z));
         int* const stk = bvh_stack<WIN>();
-        int node = 0, sp = 0, steps = 0;
+        // "while-while" (Aila & Laine): a lane walks inner nodes until it
+        // holds a leaf, postponing the first leaf it meets, and the wave
+        // leaves the inner loop once every lane still in it holds one; then
+        // the lanes test their leaves together — the inner steps (2 box
+        // tests) and the leaf steps (up to 4 exact triangle tests) no longer
+        // both run in every iteration of a wave with lanes of both kinds.
+        constexpr int kDone = 0x7fffffff;  // (never an inner node index)
+        int node = 0, leaf = 0, sp = 0, steps = 0;  // leaf: 0 = none, else a leaf reference (< 0)
         for (;;) {
-            if constexpr (BUDGET > 0) {
-                if (++steps > BUDGET) {
-                    *straggled = true;
-                    break;
+            while ((node >= 0) & (node != kDone)) {
+                if constexpr (BUDGET > 0) {
+                    if (++steps > BUDGET) break;
                 }
-            }
-            if (node >= 0) {
                 const float4* n = S.bvh_node + 4 * (size_t)node;
                 const float4 a0 = n[0], a1 = n[1], b0 = n[2], b1 = n[3];
                 ++cnt.bnode;
@@ -178,14 +182,25 @@ __device__ __forceinline__ int closest_hit_bvh(const SceneDev& S, const Vec3 O, 
                     stk[64 * sp] = near0 ? r1 : r0;
                     ++sp;
                     node = near0 ? r0 : r1;
-                    continue;
-                }
-                if (h0 | h1) {
+                } else if (h0 | h1) {
                     node = h0 ? r0 : r1;
-                    continue;
+                } else {
+                    node = sp > 0 ? stk[64 * --sp] : kDone;
                 }
-            } else {
-                const unsigned enc = ~(unsigned)node;
+                if ((node < 0) & (leaf == 0)) {  // postpone the first leaf, walk on
+                    leaf = node;
+                    node = sp > 0 ? stk[64 * --sp] : kDone;
+                }
+                if (__all(leaf != 0)) break;
+            }
+            if constexpr (BUDGET > 0) {
+                if (steps > BUDGET) {
+                    *straggled = true;
+                    break;
+                }
+            }
+            while (leaf != 0) {
+                const unsigned enc = ~(unsigned)leaf;
                 const int first = (int)(enc >> 4), count = (int)(enc & 15u) + 1;
                 for (int k = first; k < first + count; ++k) {
                     const float4* r = S.bvh_tri + 3 * (size_t)k;
@@ -197,10 +212,14 @@ __device__ __forceinline__ int closest_hit_bvh(const SceneDev& S, const Vec3 O, 
                                                  make_float4(b.w, c.x, 0.f, 0.f), O, D, t);
                     take_min(ok, t, __float_as_int(c.y), bt, bi);
                 }
+                leaf = 0;
+                if ((node < 0) & (node != kDone)) {  // the leaf that ended the inner loop
+                    leaf = node;
+                    node = sp > 0 ? stk[64 * --sp] : kDone;
+                }
+                if constexpr (BUDGET > 0) ++steps;
             }
-            if (sp == 0) break;
-            --sp;
-            node = stk[64 * sp];
+            if (node == kDone) break;
         }
     }
     best_t = bt;

@@ -39,6 +39,13 @@ for s in $STEPS; do
       run pmc_sq2_${CONFIG:-c2} 300 rocprofv3 --pmc SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM SQ_INSTS_LDS SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_SALU SQ_THREAD_CYCLES_VALU SQ_INSTS_BRANCH --output-format csv -d gpurun_out/pmc_${CONFIG:-c2} -o sq2 -- $B
       python tools/pmc_summary.py gpurun_out/pmc_${CONFIG:-c2} > gpurun_out/pmc_${CONFIG:-c2}/summary.json
       ;;
+    pmcx)  # cache and SQ counters per kernel of a config (every kernel kept: tools/pmc_kernels.py)
+      B="python bench.py --steps 5 --warmup 1 --settle-ms 0 --no-cpu-baseline --no-host-boundary --config ${CONFIG:-c2}"
+      run pmcx_l2_${CONFIG:-c2} 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum --output-format csv -d gpurun_out/pmcx_${CONFIG:-c2} -o l2 -- $B
+      run pmcx_sq_${CONFIG:-c2} 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VMEM SQ_THREAD_CYCLES_VALU --output-format csv -d gpurun_out/pmcx_${CONFIG:-c2} -o sq -- $B
+      run pmcx_wr_${CONFIG:-c2} 300 rocprofv3 --pmc WRITE_SIZE FETCH_SIZE --output-format csv -d gpurun_out/pmcx_${CONFIG:-c2} -o wr -- $B
+      python tools/pmc_kernels.py gpurun_out/pmcx_${CONFIG:-c2} > gpurun_out/pmcx_${CONFIG:-c2}/kernels.json
+      ;;
     ab) run ab_${CONFIG:-c2} 600 python tools/ab_variants.py --config ${CONFIG:-c2} ray-tracing-gpu_amd/lib/var/*.so ;;
     abenv) run abenv_${CONFIG:-c2} 600 python tools/ab_variants.py --config ${CONFIG:-c2} $AB_ARGS ;;
     pmcvar)
