@@ -56,6 +56,25 @@ def path(frame):
     return rt_amd.camera_path(frame, 6, yaw_deg=1.5, step=(0.6, 0.0, -0.4))
 
 
+def moving(frame, n=6):
+    """The bench's moving camera (bench.py frame_costs): translated by
+    (-0.29, 0, +0.17) more every frame, orientation and film unchanged — a
+    camera sliding sideways, the per-frame move of a display loop."""
+    out = []
+    for k in range(n):
+        f = frame.copy()
+        f.cam_pos[0] -= 0.29 * (k + 1)
+        f.cam_pos[2] += 0.17 * (k + 1)
+        out.append(f)
+    return out
+
+
+# Full-size moved frames of the 50k heightfield at C3 (1920x1080, depth 0):
+# frames of moving() pinned by whole-frame digests (cameras.json key
+# f"hf_1920x1080_d0_moving{i}")
+MOVING_FULL = ("hf", 1920, 1080, 0, (3, 6))
+
+
 def words(f) -> list:
     """The camera words of a frame, as the reference's pixel loop reads them."""
     return [*f.cam_pos, *f.orient, f.half_w, f.half_h, f.inv_w, f.inv_h]
@@ -77,4 +96,4 @@ def key(which, kind, i):
     return f"{which}_{w}x{h}_d{depth}_{kind}{i}"
 
 
-KINDS = {"cams": cameras, "path": path}
+KINDS = {"cams": cameras, "path": path, "moving": moving}

@@ -13,6 +13,8 @@ container:
   half extents, pixel reciprocals — what rt_frame carries), then runs the
   reference pixel loop (Scene.cpp:1538-1561) over the whole frame.
 * Big bounce frames: scene7 and scene9 at 3840x2160, depth 5, whole frame.
+* Moved C3 frames at full size: frames 3 and 6 of tests/cameras.py
+  moving() (the bench's translated camera) on the heightfield at 1920x1080.
 
 Output: tests/golden/cameras.json — per frame the SHA-256 of its camera
 words (tests/cameras.py words()), of the float32 RGB frame (row 0 = bottom)
@@ -93,9 +95,19 @@ def main():
             continue
         tasks = [(name, w, h, 5, None, r, min(h, r + 120)) for r in range(0, h, 120)]
         jobs.append((f"{name}_{w}x{h}_d5_full", None, w, h, tasks))
+    name, w, h, depth, idx = cameras.MOVING_FULL  # full-size moved C3 frames
+    mv = cameras.moving(rt_amd.Scene(scene_path(name), w, h, depth).frame, max(idx) + 1)
+    for i in idx:
+        k = f"{name}_{w}x{h}_d{depth}_moving{i}"
+        if k in out:
+            assert out[k]["camera_words_sha256"] == cameras.words_sha(mv[i])
+            continue
+        words = [float(x) for x in cameras.words(mv[i])]
+        tasks = [(name, w, h, depth, words, r, min(h, r + BAND)) for r in range(0, h, BAND)]
+        jobs.append((k, cameras.words_sha(mv[i]), w, h, tasks))
     flat = [t for j in jobs for t in j[4]]
     t0 = time.time()
-    with Pool(min(8, os.cpu_count() or 1)) as p:
+    with Pool(int(os.environ.get("GOLDEN_PROCS", min(8, os.cpu_count() or 1)))) as p:
         bands = p.map(render_band, flat, chunksize=1)
     k = 0
     for key, wsha, w, h, tasks in jobs:

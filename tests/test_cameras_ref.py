@@ -31,11 +31,13 @@ def test_fixture_keys_and_words(heightfield_path):
         CamRef(which, heightfield_path)  # asserts every frame's camera words
     keys = {cameras.key(w, k, i) for w, *_ in cameras.SETS for k in cameras.KINDS for i in range(6)}
     keys |= {"scene7_3840x2160_d5_full", "scene9_3840x2160_d5_full"}
+    name, w, h, d, idx = cameras.MOVING_FULL
+    keys |= {f"{name}_{w}x{h}_d{d}_moving{i}" for i in idx}
     assert keys == set(cam_golden())
 
 
 @pytest.mark.parametrize("which", CPU_SETS)
-@pytest.mark.parametrize("kind", ["cams", "path"])
+@pytest.mark.parametrize("kind", ["cams", "path", "moving"])
 def test_oracle_explicit_camera(oracle, heightfield_path, which, kind):
     r = CamRef(which, heightfield_path)
     L = oracle.L
