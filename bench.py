@@ -271,7 +271,7 @@ def progressive(ctx, frame, W, rows, n=60):
                     "replay per path"}
 
 
-def frame_costs(scene, frame, W, cold):
+def frame_costs(scene, frame, W, cold, opts=None):
     """What the drop-in pays beyond the steady-state kernel (never `value`):
     the reference renders ONE frame per process through LancerRayons
     (Main.cpp:181, Scene.cpp:672), paying the scene upload, the per-camera
@@ -295,7 +295,7 @@ def frame_costs(scene, frame, W, cold):
     rows = rt_amd.frame_rows(frame)
     pinned = torch.empty((rows, W, 4), dtype=torch.uint8).pin_memory()
     torch.cuda.synchronize()
-    ctx = rt_amd.Context(0)
+    ctx = rt_amd.Context(0, **(opts or {}))
     t0 = time.perf_counter()
     ctx.upload(scene)
     t1 = time.perf_counter()
@@ -772,7 +772,7 @@ def main():
             out["frame_rgba8_sha256"] = frame_sha
         if world == 1 and not args.no_host_boundary:
             out["host_boundary"] = host_boundary(ctx, frame, W)
-            fc = frame_costs(scene, frame, W, cold)
+            fc = frame_costs(scene, frame, W, cold, ctx_opts)
             out["first_frame_ms"] = fc.get("first_frame_ms")
             out["moving_camera_ms_per_frame"] = fc.get("moving_camera_ms_per_frame")
             mc = fc.get("moving_camera") or {}

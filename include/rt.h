@@ -259,14 +259,6 @@ enum {
                                    per level then a fold per level (up to 8 levels,
                                    not inside a hipGraph capture or a sequence): 1
                                    (default) / 0 (one kernel, a per-lane DFS stack) */
-    RT_OPT_CB_ENVELOPE = 15,    /* launch (ABI 7): a camera that moves by translation
-                                   (its previous render had the same view from another
-                                   position) walks envelope lists — per-tile lists valid
-                                   for every camera position in a ball, built once for
-                                   its next N frames at its current step and reused while
-                                   it stays inside (scenes above 1,024 triangles; a
-                                   repeated camera still builds its own lists): N =
-                                   the value, default 8; 0 = off */
     RT_OPT_LAUNCH_CAMERA = 12   /* launch (ABI 6): depth-0 frames of scenes of 1-20
                                    triangles with light-buffer shadows take their camera
                                    records with the kernel launch — per-triangle camera

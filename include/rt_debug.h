@@ -36,14 +36,6 @@ int rt_debug_cb_info(rt_ctx*, double* out, int n);
  * not exactly the triangles passing the camera wave test (or mis-keyed),
  * out[1] passing pairs, out[2] tiles with a list. */
 int rt_debug_cb_verify(rt_ctx*, unsigned long long* out3);
-/* Envelope lists (RT_OPT_CB_ENVELOPE): out[0] current, [1] entries of the
- * last build, [2] builds, [3] frames that walked them, [4] the ball's radius,
- * [5] entry capacity, [6] candidate pairs (n >= 4). */
-int rt_debug_env_info(rt_ctx*, double* out, int n);
-/* The envelope lists against the last prepared camera's own records: out[0]
- * tiles missing a triangle that camera's exact list holds (or keyed above its
- * dmin), out[1] its passing pairs, out[2] envelope entries.  Synchronous. */
-int rt_debug_env_verify(rt_ctx*, unsigned long long* out3);
 
 /* The last rt_upload_scene's host wall time by part (ms): out[0] records +
  * device copies, out[1] cone / cluster prepasses, out[2] light buffer,

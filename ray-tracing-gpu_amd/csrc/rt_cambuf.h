@@ -734,49 +734,5 @@ __global__ __launch_bounds__(256) void rt_cb_verify(const SceneDev S, const CbDe
     }
 }
 
-// Diagnostic (rt_debug_env_verify): envelope lists against the current
-// camera's own records (S.cone_cam): every triangle whose camera wave test
-// passes for a tile — what that camera's exact list would hold — must be in
-// the tile's envelope list, keyed at most its own dmin.  out[0] += tiles
-// missing one (or keyed above it), out[1] += passing pairs, out[2] += entries.
-__global__ __launch_bounds__(256) void rt_cb_env_verify(const SceneDev S, const CbDev B, unsigned* __restrict__ out)
-{
-    const int lane = (int)(threadIdx.x & 63);
-    const int t = (int)(blockIdx.x * 4 + (threadIdx.x >> 6));
-    if (t >= B.tiles_x * B.tiles_y || B.flag[t]) return;
-    const unsigned b = B.off[t], m = B.off[t + 1] - b;
-    unsigned n = 0;
-    bool bad = false;
-    for (int k0 = 0; k0 < S.n_tri; k0 += 64) {
-        const int k = k0 + lane;
-        bool pass = false;
-        float4 c1 = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (k < S.n_tri) {
-            c1 = S.cone_cam[2 * k + 1];
-            pass = cb_pair_test(B, t, S.cone_cam[2 * k], c1.w, S.cone_cam + 2 * (size_t)S.n_tri + 3 * (size_t)k);
-        }
-        const unsigned long long pm = __ballot(pass);
-        if (!pm) continue;
-        n += (unsigned)__popcll(pm);
-        bool ok = !pass;
-        if (pass) {
-            const float d = cb_dmin(make_int2(0, __float_as_int(c1.x)));
-            for (unsigned e = 0; e < m; ++e) {
-                const int2 en = B.ent[b + e];
-                if (en.x == k) {
-                    ok = cb_dmin(en) <= d;
-                    break;
-                }
-            }
-        }
-        bad |= __any(!ok);
-    }
-    if (lane == 0) {
-        atomicAdd(&out[1], n);
-        atomicAdd(&out[2], m);
-        if (bad) atomicAdd(&out[0], 1u);
-    }
-}
-
 }  // namespace rt
 #endif  // RT_AMD_RT_CAMBUF_H

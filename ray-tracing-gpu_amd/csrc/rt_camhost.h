@@ -546,57 +546,6 @@ static bool cb_matches(const rt_ctx::CamBuf& B, const rt_frame* f)
     return std::memcmp(key, B.key, sizeof key) == 0;
 }
 
-// ---- envelope lists (rt_cull.h cone_record_env)
-// Does the envelope buffer serve frame f: the same view (every key word
-// past the position) and a camera position inside the ball (in double: the
-// records hold for every position within env_r of env_c)?
-static bool env_contains(const rt_ctx* c, const rt_frame* f)
-{
-    const rt_ctx::CamBuf& B = c->cbe;
-    if (!B.valid || !c->d_cone_env) return false;
-    float key[30];
-    cb_key_of(f, key);
-    if (std::memcmp(key + 3, B.key + 3, sizeof key - 3 * sizeof(float)) != 0) return false;
-    double d2 = 0.0;
-    for (int i = 0; i < 3; ++i) {
-        const double d = (double)f->cam_pos[i] - c->env_c[i];
-        d2 += d * d;
-    }
-    return std::sqrt(d2) <= c->env_r;
-}
-
-// Build the envelope lists for a camera at f->cam_pos moving by `step` per
-// frame: the ball around the midpoint of its next K = RT_OPT_CB_ENVELOPE
-// positions (radius K |step| / 2, widened by 0.1% and by float rounding of
-// positions the caller will compute), its records (rt_cone_env_prepass) and
-// the usual build from them (no inline records: each frame walks its own
-// tricam records by index).  f's key is the buffer's key: env_contains
-// compares everything but the position.
-static int cb_envelope_build(rt_ctx* c, const rt_frame* f, const double* step, hipStream_t st, bool sync_path)
-{
-    const double K = (double)c->opt_cb_envelope;
-    double P[3], len2 = 0.0, p2 = 0.0;
-    for (int i = 0; i < 3; ++i) {
-        P[i] = (double)f->cam_pos[i] + 0.5 * K * step[i];
-        len2 += step[i] * step[i];
-        p2 += P[i] * P[i];
-    }
-    const double R = 0.5 * K * std::sqrt(len2) * 1.001 + 1e-6 * (std::sqrt(p2) + 1.0);
-    if (!(R > 0.0) || !std::isfinite(R)) return RT_OK;  // (no motion: nothing to build)
-    if (!c->d_cone_env) HIP_TRY(c, hipMalloc((void**)&c->d_cone_env, (size_t)c->n_tri * 5 * sizeof(float4)));
-    c->cbe.valid = false;
-    hipLaunchKernelGGL(rt_cone_env_prepass, dim3((c->n_tri + 255) / 256), dim3(256), 0, st, c->d_tri, c->d_trisph,
-                       c->d_trinrm, c->d_tricoef, c->n_tri, P[0], P[1], P[2], R, c->d_cone_env);
-    HIP_TRY(c, hipGetLastError());
-    SceneDev S = scene_dev(c, false, nullptr);
-    S.cone_cam = c->d_cone_env;
-    if (int rc = cb_build(c, c->cbe, f, S, st, sync_path, false, false)) return rc;
-    for (int i = 0; i < 3; ++i) c->env_c[i] = P[i];
-    c->env_r = R;
-    ++c->env_builds;
-    return RT_OK;
-}
-
 static bool frame_ok(const rt_frame* f)
 {
     return !(f->width <= 0 || f->height <= 0 || f->row_begin < 0 || f->row_end > f->height ||

@@ -775,126 +775,6 @@ __host__ __device__ inline void cone_record(const float4* __restrict__ tri, cons
     oe[1] = ce[1];
     oe[2] = ce[2];
 }
-// Envelope camera records: records for apex P that hold for EVERY camera
-// position A with |A - P| <= R (the camera buffer of a translating camera,
-// rt_camhost.h cb_envelope: lists built once for a ball of positions, walked
-// by the frames whose camera lies in it, each with its own tricam records).
-//
-// Why they hold.  For apex A the proof above gives: a reported hit of a ray
-// from A with direction d has its plane crossing X within m_A of the
-// triangle, i.e. X in the sphere (s, r0 + m_A), at distance >= dv_A - r0 -
-// m_A from A and t >= dnear_A - 4 m_A / 3 — provided A's conditions hold
-// (h_eff >= G phi, m <= 10 r0, ...).  Translate the ray by P - A (same
-// direction d): it meets Y = X + (P - A), |Y - X| <= R, so Y lies in the
-// sphere (s, r0 + m_A + R) and within m_A + R of the triangle, at distance
-// |X - A| from P.  So with every A-dependent quantity replaced by its bound
-// over the ball — dv in [dv_P - R, dv_P + R], h in [h_P - R, h_P + R]
-// (|n| = 1 to float rounding, so R (1 + 1e-4)), G and Rp at their maxima,
-// m between m_lo and m_hi, phi (decreasing in m) at m_lo — the conditions
-// hold for every A at once, and the records from P with
-//   cone radius  r0 + m_hi + R + 2e-5 (dv_P + R)
-//   dmin         (dnear_P - R - 4 m_hi / 3 - 2e-5 (dv_P + R)) (1 - 1e-5)
-//   edge lim     -(m_hi + R) / (dv_P - R - r0 - m_hi) - 1e-5
-// pass every (tile, triangle) pair that A's own records pass (the tiles'
-// ray directions do not depend on the position), and bound every hit A's
-// rays can report from below.  The "never reported" record likewise with
-// the worst case of its inequality.  Anything else: "always test".  R = 0
-// does not reproduce cone_record's bits (its margins differ slightly) and
-// is never used: the exact lists come from cone_record.
-__host__ __device__ inline void cone_record_env(const float4* __restrict__ tri, const float4* __restrict__ sph,
-                                                const float4* __restrict__ nrm, const float4* __restrict__ coef,
-                                                int n, double ax, double ay, double az, double R,
-                                                float4* __restrict__ out, int k)
-{
-    const float4 s = sph[k], nr = nrm[k], cf = coef[k], p0 = tri[3 * k];
-    const double vx = (double)s.x - ax, vy = (double)s.y - ay, vz = (double)s.z - az;
-    const double dv = sqrt(vx * vx + vy * vy + vz * vz);
-    const double r0 = s.w, L = nr.w, gS = cf.x, gL = cf.y, rho_cap = cf.z;
-    const double h = fabs(nr.x * (ax - p0.x) + nr.y * (ay - p0.y) + nr.z * (az - p0.z));
-    const double Rh = R * (1.0 + 1e-4);
-    const double dv_hi = dv + R, dv_lo = dv - R;
-    const double h_hi = h + Rh, h_lo = fmax(0.0, h - Rh);
-    const double tau = 18.0 * 0x1p-24 * L;
-    const double he_lo = 0.989 * h_lo - 1e-6 * (dv_hi + r0), he_hi = 0.989 * h_hi;
-    const double Rp_hi = 1.011 * h_hi + dv_hi + r0 + 1e-6 * dv_hi;
-    const double G_hi = gS * (dv_hi + r0) + gL;
-    float4 c0 = make_float4(0.f, 0.f, 0.f, -2.0f);
-    float4 c1 = make_float4(-INFINITY, 0.f, -INFINITY, 2.0f);
-    float4 ce[3];
-    for (int e = 0; e < 3; ++e) ce[e] = make_float4(0.f, 0.f, 0.f, -4.0f);
-    bool cone_ok = false;
-    double m_hi = 0.01 * r0;
-    if (rho_cap >= 0.0 && he_lo > 1.01 * G_hi && isfinite(dv) && isfinite(gS) && isfinite(gL)) {
-        m_hi = fmax(m_hi, 1.001 * (he_hi * tau + 1.01 * G_hi * Rp_hi) / (he_lo - 1.01 * G_hi));
-        const double m_lo = 0.01 * r0;  // every A's m is at least this
-        const double phi_hi = 1.01 * (m_lo + Rp_hi) / (m_lo - tau);
-        const double rc = r0 + m_hi + R + 2e-5 * dv_hi;
-        cone_ok = m_hi <= 10.0 * r0 && m_lo > 2.0 * tau && dv_lo - (r0 + m_hi + 2e-5 * dv_hi) > m_hi / 3.0 + 0.02 &&
-                  dv - rc > 0.02 && he_lo >= G_hi * phi_hi;
-        if (cone_ok) {
-            double dnear = dv - r0;
-            const float4 t1 = tri[3 * k + 1], t2 = tri[3 * k + 2];
-            const double Vt[3][3] = {{p0.x, p0.y, p0.z},
-                                     {(double)p0.x + p0.w, (double)p0.y + t1.x, (double)p0.z + t1.y},
-                                     {(double)p0.x + t1.z, (double)p0.y + t1.w, (double)p0.z + t2.x}};
-            const double Ap[3] = {ax, ay, az};
-            const double dt = point_triangle_dist(Ap, Vt);
-            if (dt == dt) dnear = fmax(dnear, dt * (1.0 - 1e-9));
-            const double cosT = sqrt(1.0 - (rc / dv) * (rc / dv)) - 2e-6;
-            c0 = make_float4((float)(vx / dv), (float)(vy / dv), (float)(vz / dv), (float)cosT);
-            const float sinT = (float)(sqrt(fmax(0.0, 1.0 - (double)c0.w * c0.w)) + 1e-7);
-            const double dmin = (dnear - R - 4.0 * m_hi / 3.0 - 2e-5 * dv_hi) * (1.0 - 1e-5);
-            c1 = make_float4((float)dmin, 0.f, 0.f, sinT);
-            const double smin = dv - R - r0 - m_hi;
-            const float lim = (float)(-(m_hi + R) / smin - 1e-5);
-            bool good = smin > 0.0;
-            for (int e = 0; e < 3 && good; ++e) {
-                const int i = e, j = (e + 1) % 3, q = (e + 2) % 3;
-                const double ax_ = Vt[i][0] - ax, ay_ = Vt[i][1] - ay, az_ = Vt[i][2] - az;
-                const double bx_ = Vt[j][0] - ax, by_ = Vt[j][1] - ay, bz_ = Vt[j][2] - az;
-                const double nx = ay_ * bz_ - az_ * by_, ny = az_ * bx_ - ax_ * bz_, nz = ax_ * by_ - ay_ * bx_;
-                const double nn = sqrt(nx * nx + ny * ny + nz * nz);
-                const double side = nx * (Vt[q][0] - ax) + ny * (Vt[q][1] - ay) + nz * (Vt[q][2] - az);
-                if (!(nn > 0.0) || !isfinite(nn) || side == 0.0) {
-                    good = false;
-                    break;
-                }
-                const double sg = side > 0.0 ? 1.0 : -1.0;
-                ce[e] = make_float4((float)(sg * nx / nn), (float)(sg * ny / nn), (float)(sg * nz / nn), lim);
-            }
-            if (!good)
-                for (int e = 0; e < 3; ++e) ce[e] = make_float4(0.f, 0.f, 0.f, -4.0f);
-        }
-    }
-    if (!cone_ok && rho_cap >= 0.0 && cf.w > 0.0f && isfinite(dv) && isfinite(gS) && isfinite(gL)) {
-        // never reported from any camera of the ball (cone_record's test at
-        // the worst case: the farthest h, the nearest centre, the largest |S|)
-        const double nn = cf.w;
-        const double amin = (0.0099999 - 7.07 * 0x1p-24 * L * L) / (nn * (1.0 + 1e-6));
-        if (amin > 0.0) {
-            const double M = 1.01 * ((gS * (dv_hi + r0) + gL) / amin + tau);
-            const double hup = 1.01 * h_hi + 1e-5 * (dv_hi + r0);
-            if (dv_lo - r0 - M - hup / amin > 1e-3 * dv_hi + 0.01) {
-                c0 = make_float4((float)(vx / dv), (float)(vy / dv), (float)(vz / dv), 2.0f);
-                c1 = make_float4(INFINITY, 0.f, 0.f, 0.f);
-            }
-        }
-    }
-    out[2 * k] = c0;
-    out[2 * k + 1] = c1;
-    float4* oe = out + 2 * (size_t)n + 3 * k;
-    oe[0] = ce[0];
-    oe[1] = ce[1];
-    oe[2] = ce[2];
-}
-__global__ void rt_cone_env_prepass(const float4* __restrict__ tri, const float4* __restrict__ sph,
-                                    const float4* __restrict__ nrm, const float4* __restrict__ coef, int n,
-                                    double ax, double ay, double az, double R, float4* __restrict__ out)
-{
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k < n) cone_record_env(tri, sph, nrm, coef, n, ax, ay, az, R, out, k);
-}
-
 __global__ void rt_cone_prepass(const float4* __restrict__ tri, const float4* __restrict__ sph,
                                 const float4* __restrict__ nrm, const float4* __restrict__ coef, int n, float ax,
                                 float ay, float az, int camera, float dtarget, float4* __restrict__ out,

@@ -649,18 +649,6 @@ struct rt_ctx {
     // the last async frame's camera (cb_key_of): a repeat builds the sorted lists
     float last_async_key[30] = {};
     bool last_async_valid = false;
-    // Envelope camera buffer (round 5, rt_camhost.h cb_envelope_build): the
-    // lists of every camera position within env_r of env_c (same view
-    // otherwise: the key words past the position), built from
-    // cone_record_env records for a camera that moves by translation, and
-    // walked by its frames while the camera stays in the ball.
-    CamBuf cbe;
-    float4* d_cone_env = nullptr;  // 5 float4 per triangle, cone_cam's layout
-    double env_c[3] = {0.0, 0.0, 0.0}, env_r = 0.0;
-    unsigned long long env_builds = 0, env_frames = 0;
-    // the previous render's camera (any path): motion detection
-    float mv_key[30] = {};
-    bool mv_valid = false;
     // Camera state of rt_render_sequence_async: kSeqSlots slots of the
     // per-camera records and camera buffers, apart from the state above;
     // frame i of a sequence uses slot i % kSeqSlots on internal stream
@@ -770,7 +758,6 @@ struct rt_ctx {
         bool pending = false;
     } wf;
     int opt_wavefront = 1;      // RT_OPT_WAVEFRONT
-    int opt_cb_envelope = 8;    // RT_OPT_CB_ENVELOPE: frames ahead an envelope covers (0 = off)
     float kr_max = 0.0f, kt_max = 0.0f;  // max Kr, max Kt over surfaces
     bool uploaded = false;
     rt_stats last{};
@@ -925,7 +912,7 @@ RT_EXPORT int rt_set_option(rt_ctx* c, int32_t opt, double v)
         return RT_OK;
     case RT_OPT_CAMERA_BUFFER:
         if (v != 0 && v != 1 && v != 2) return RT_E_ARG;
-        if ((int)v != c->opt_camera_buffer) c->cb.valid = c->cbe.valid = false;
+        if ((int)v != c->opt_camera_buffer) c->cb.valid = false;
         c->opt_camera_buffer = (int)v;
         return RT_OK;
     case RT_OPT_UNION_PRETEST: c->opt_union = v != 0; return RT_OK;
@@ -950,14 +937,9 @@ RT_EXPORT int rt_set_option(rt_ctx* c, int32_t opt, double v)
     case RT_OPT_LAUNCH_CAMERA: c->opt_launch_camera = v != 0; return RT_OK;
     case RT_OPT_BVH: c->opt_bvh = v != 0; return RT_OK;
     case RT_OPT_WAVEFRONT: c->opt_wavefront = v != 0; return RT_OK;
-    case RT_OPT_CB_ENVELOPE:
-        if (v < 0 || v > 1024 || v != std::floor(v)) return RT_E_ARG;
-        if ((int)v != c->opt_cb_envelope) c->cbe.valid = false;
-        c->opt_cb_envelope = (int)v;
-        return RT_OK;
     case RT_OPT_CB_CAPACITY:
         if (v < 0 || v > 4e9 || v != std::floor(v)) return RT_E_ARG;
-        if (v != c->opt_cb_capacity) c->cb.valid = c->cbe.valid = false;
+        if (v != c->opt_cb_capacity) c->cb.valid = false;
         c->opt_cb_capacity = v;
         return RT_OK;
     default: return RT_E_ARG;
@@ -979,7 +961,6 @@ RT_EXPORT int rt_get_option(rt_ctx* c, int32_t opt, double* v)
     case RT_OPT_LAUNCH_CAMERA: *v = c->opt_launch_camera ? 1 : 0; return RT_OK;
     case RT_OPT_BVH: *v = c->opt_bvh ? 1 : 0; return RT_OK;
     case RT_OPT_WAVEFRONT: *v = c->opt_wavefront; return RT_OK;
-    case RT_OPT_CB_ENVELOPE: *v = c->opt_cb_envelope; return RT_OK;
     default: return RT_E_ARG;
     }
 }
@@ -1059,8 +1040,6 @@ RT_EXPORT void rt_destroy(rt_ctx* c)
         if (q.ev) hipEventDestroy(q.ev);
     }
     cb_free(c->cb);
-    cb_free(c->cbe);
-    hipFree(c->d_cone_env);
     for (auto& q : c->seq) {
         hipFree(q.tricam);
         hipFree(q.cone_cam);
@@ -1597,10 +1576,6 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
     c->bvh_inner = c->bvh_leaves = c->bvh_depth = 0;
     c->bvh_build_ms = 0.0;
     c->cb.valid = false;  // buffers are kept (reallocated on demand)
-    c->cbe.valid = false;
-    hipFree(c->d_cone_env);
-    c->d_cone_env = nullptr;
-    c->mv_valid = false;
     c->cam_valid = false;
     c->lb_build_ms = 0.0;
     c->d_geom = c->d_mat = c->d_lights = c->d_tri = c->d_plane = c->d_quad = nullptr;
@@ -2072,9 +2047,8 @@ static int camera_prepass(rt_ctx* c, const rt_frame* f, hipStream_t st, bool all
     return RT_OK;
 }
 
-static SceneDev scene_dev(rt_ctx* c, bool lbuf, const rt_ctx::CamBuf* cb)
+static SceneDev scene_dev(rt_ctx* c, bool lbuf, bool cbuf)
 {
-    const rt_ctx::CamBuf& B = cb ? *cb : c->cb;
     const int use_tricam = c->n_tri > 0 && c->n_tri <= kTricamMaxTriangles;
     return SceneDev{c->d_geom, c->d_mat, c->d_lights, c->d_tri, c->d_plane, c->d_quad, c->d_translucent, c->d_tricam,
                     use_tricam, c->n_tri <= kEdgeMaxTriangles, c->d_cone_cam, c->d_cone_light, c->d_clu_cam,
@@ -2082,8 +2056,8 @@ static SceneDev scene_dev(rt_ctx* c, bool lbuf, const rt_ctx::CamBuf* cb)
                     c->n_tri_opaque, c->n_plane_opaque, c->n_quad_opaque, c->n_translucent, c->shadow_split,
                     lbuf ? c->lb_levels : 0, c->d_lb_off, c->d_lb_ent, c->d_lb_dcap, c->d_lb_meta,
                     (c->d_uni && c->opt_union) ? c->d_uni : nullptr,
-                    B.off, B.ent, B.flag, cb ? B.tiles_x : 0, B.inline_rec ? B.rec : nullptr, c->d_bvh_node,
-                    c->d_bvh_tri};
+                    c->cb.off, c->cb.ent, c->cb.flag, cbuf ? c->cb.tiles_x : 0,
+                    c->cb.inline_rec ? c->cb.rec : nullptr, c->d_bvh_node, c->d_bvh_tri};
 }
 
 // The light buffer serves this context's shadow rays (RT_OPT_LIGHT_BUFFER).
@@ -2142,24 +2116,7 @@ static int prepare_state(rt_ctx* c, const rt_frame* f, hipStream_t st, bool sync
         c->last_async_valid = true;
     }
     const bool current = cb_matches(c->cb, f) && !need_prep;
-    // A camera moving by translation (the previous render's camera differs
-    // from this one in position only) walks envelope lists: reused while it
-    // stays in their ball, built for the next RT_OPT_CB_ENVELOPE frames at
-    // its current step when it leaves it (big lists only).  A repeated
-    // camera builds its own sorted lists, as before.
-    double step[3] = {0.0, 0.0, 0.0};
-    const bool moved = c->mv_valid && std::memcmp(key + 3, c->mv_key + 3, sizeof key - 3 * sizeof(float)) == 0 &&
-                       std::memcmp(key, c->mv_key, 3 * sizeof(float)) != 0;
-    if (moved)
-        for (int i = 0; i < 3; ++i) step[i] = (double)key[i] - (double)c->mv_key[i];
-    if (!capturing) {
-        std::memcpy(c->mv_key, key, sizeof key);
-        c->mv_valid = true;
-    }
-    const bool env_use = cb_want && !current && !repeat && c->opt_cb_envelope > 0 && env_contains(c, f);
-    const bool env_build = cb_want && !current && !repeat && !env_use && moved && c->opt_cb_envelope > 0 &&
-                           c->n_tri > kClusterMinTriangles;
-    const bool need_cb = cb_want && !current && !env_use && !env_build && (sync_path || repeat || cb_async_pays(c, f));
+    const bool need_cb = cb_want && !current && (sync_path || repeat || cb_async_pays(c, f));
     if (capturing) {
         if (need_prep) {
             c->err = "hipGraph capture: the frame's camera is not prepared (rt_render or rt_prepare_camera first)";
@@ -2167,7 +2124,7 @@ static int prepare_state(rt_ctx* c, const rt_frame* f, hipStream_t st, bool sync
         }
         return RT_OK;
     }
-    if (!need_prep && !need_cb && !env_build) return RT_OK;
+    if (!need_prep && !need_cb) return RT_OK;
     if (!sync_path) {
         if (int rc = fence_async(c, st)) return rc;
     }
@@ -2175,11 +2132,8 @@ static int prepare_state(rt_ctx* c, const rt_frame* f, hipStream_t st, bool sync
         if (int rc = camera_prepass(c, f, st, cb_want)) return rc;
     }
     if (need_cb) {
-        const SceneDev S = scene_dev(c, false, nullptr);
+        const SceneDev S = scene_dev(c, false, false);
         if (int rc = cb_build(c, c->cb, f, S, st, sync_path, false, true)) return rc;
-    }
-    if (env_build) {
-        if (int rc = cb_envelope_build(c, f, step, st, sync_path)) return rc;
     }
     if (!sync_path) {
         HIP_TRY(c, hipEventRecord(c->ev_state, st));
@@ -2391,17 +2345,7 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
     if (rows > 0 && !tiny) {
         if (int rc = prepare_state(c, f, st, sync_path, capturing, cb_want)) return rc;
     }
-    // the frame's camera buffer: its own camera's lists, else the envelope
-    // lists of a ball holding its camera (not inside a capture)
-    const rt_ctx::CamBuf* cbp = nullptr;
-    if (!tiny && cb_want) {
-        if (cb_matches(c->cb, f))
-            cbp = &c->cb;
-        else if (!capturing && env_contains(c, f))
-            cbp = &c->cbe;
-    }
-    const bool cbuf = cbp != nullptr;
-    if (cbp == &c->cbe && rows > 0) ++c->env_frames;
+    const bool cbuf = !tiny && cb_want && cb_matches(c->cb, f);
     // Wavefront: a BVH frame's bounce levels as compacted queues (rt_wavefront.h);
     // its queues are shared by the context's streams: a frame on another
     // stream than the last wavefront frame waits for that one.  A captured
@@ -2422,7 +2366,7 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
         c->err = "reachable bounce depth " + std::to_string(depth) + " exceeds the compiled stack (32)";
         return RT_E_UNSUPPORTED;
     }
-    SceneDev S = scene_dev(c, lbuf, cbp);
+    SceneDev S = scene_dev(c, lbuf, cbuf);
     FrameDev F;
     frame_dev(f, F);
     if (wf) F.wf = c->wf.dev;
@@ -2683,7 +2627,7 @@ RT_EXPORT int rt_render_sequence_async(rt_ctx* c, const rt_frame* frames, int32_
         }
         const KernelPick kp =
             pick_kernel<false>(depth, c->n_tri, c->n_lights, lbuf, cbuf, bvh ? c->bvh_depth : 0, reflect_chain(c, f));
-        SceneDev S = scene_dev(c, lbuf, nullptr);
+        SceneDev S = scene_dev(c, lbuf, false);
         S.tricam = q.tricam;
         S.cone_cam = q.cone_cam;
         S.clu_cam = q.clu_cam;
@@ -2878,74 +2822,6 @@ RT_EXPORT int rt_debug_cb_info(rt_ctx* c, double* out, int n)
     return RT_OK;
 }
 
-// Diagnostic (include/rt_debug.h): envelope lists (RT_OPT_CB_ENVELOPE):
-// out[0] = current (0/1), out[1] = entries of the last build read back,
-// out[2] = builds, out[3] = frames that walked them, out[4] = the ball's
-// radius, out[5] = the entry capacity, out[6] = candidate pairs.
-RT_EXPORT int rt_debug_env_info(rt_ctx* c, double* out, int n)
-{
-    if (!c || !out || n < 4) return RT_E_ARG;
-    if (c->cpu) return not_cpu(c);
-    rt_ctx::CamBuf& B = c->cbe;
-    if (B.tot_pending) {
-        HIP_TRY(c, hipEventSynchronize(B.ev_tot));
-        cb_harvest(B);
-    }
-    out[0] = B.valid ? 1.0 : 0.0;
-    out[1] = (double)B.entries;
-    out[2] = (double)c->env_builds;
-    out[3] = (double)c->env_frames;
-    if (n > 4) out[4] = c->env_r;
-    if (n > 5) out[5] = (double)B.cap;
-    if (n > 6) out[6] = B.hstat[1];
-    return RT_OK;
-}
-
-// Diagnostic (include/rt_debug.h): the envelope lists against the camera
-// last prepared (its own camera records, rt_cb_env_verify): out[0] = tiles
-// whose list misses a triangle that camera's exact list holds (or keys it
-// above that camera's dmin), out[1] = that camera's passing pairs, out[2] =
-// envelope entries walked.  RT_E_STATE when the envelope lists are not
-// current or do not hold the prepared camera.  Synchronous.
-RT_EXPORT int rt_debug_env_verify(rt_ctx* c, unsigned long long* out)
-{
-    if (!c || !out) return RT_E_ARG;
-    if (c->cpu) return not_cpu(c);
-    HIP_TRY(c, hipSetDevice(c->device));
-    if (int rc = sync_all(c)) return rc;
-    rt_ctx::CamBuf& B = c->cbe;
-    if (!B.valid || !c->cam_valid) {
-        c->err = "no envelope lists, or no prepared camera";
-        return RT_E_STATE;
-    }
-    double d2 = 0.0;
-    for (int i = 0; i < 3; ++i) d2 += ((double)c->cam_key[i] - c->env_c[i]) * ((double)c->cam_key[i] - c->env_c[i]);
-    if (!(std::sqrt(d2) <= c->env_r)) {
-        c->err = "the prepared camera lies outside the envelope";
-        return RT_E_STATE;
-    }
-    unsigned* d = nullptr;
-    HIP_TRY(c, hipMalloc((void**)&d, 3 * sizeof(unsigned)));
-    HIP_TRY(c, hipMemsetAsync(d, 0, 3 * sizeof(unsigned), c->stream));
-    const SceneDev S = scene_dev(c, false, &B);
-    CbDev D{};
-    D.tcone = B.tcone;
-    D.off = B.off;
-    D.flag = B.flag;
-    D.ent = B.ent;
-    D.tiles_x = B.tiles_x;
-    D.tiles_y = B.tiles_x > 0 ? B.ntiles / B.tiles_x : 0;
-    hipLaunchKernelGGL(rt_cb_env_verify, dim3((unsigned)((B.ntiles + 3) / 4)), dim3(256), 0, c->stream, S, D, d);
-    unsigned h[3] = {0, 0, 0};
-    hipError_t e = hipGetLastError();
-    if (e == hipSuccess) e = hipMemcpyAsync(h, d, sizeof h, hipMemcpyDeviceToHost, c->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-    hipFree(d);
-    if (e != hipSuccess) return hip_fail(c, e, "rt_debug_env_verify");
-    for (int i = 0; i < 3; ++i) out[i] = h[i];
-    return RT_OK;
-}
-
 // Diagnostic (include/rt_debug.h): the current camera buffer against brute
 // force (rt_cb_verify): out[0] = tiles whose list is not exactly the
 // passing triangles (or mis-keyed), out[1] = passing pairs, out[2] = tiles
@@ -2974,7 +2850,7 @@ RT_EXPORT int rt_debug_cb_verify(rt_ctx* c, unsigned long long* out)
     D.cap = (unsigned)B.cap;
     D.tiles_x = B.tiles_x;
     D.tiles_y = B.ntiles / std::max(1, B.tiles_x);
-    const SceneDev S = scene_dev(c, false, &c->cb);
+    const SceneDev S = scene_dev(c, false, true);
     unsigned h[2] = {0, 0};
     std::vector<unsigned> flags((size_t)B.ntiles);
     if (rc == RT_OK) {
@@ -3066,7 +2942,7 @@ RT_EXPORT int rt_debug_bvh_rays(rt_ctx* c, const float* rays, int n, int* out_id
         chk(hipMalloc(&d_tally, 2 * sizeof(unsigned long long)), "hipMalloc") &&
         chk(hipMemcpy(d_rays, rays, (size_t)n * 6 * sizeof(float), hipMemcpyHostToDevice), "hipMemcpy") &&
         chk(hipMemset(d_tally, 0, 2 * sizeof(unsigned long long)), "hipMemset")) {
-        const SceneDev S = scene_dev(c, false, nullptr);
+        const SceneDev S = scene_dev(c, false, false);
         hipLaunchKernelGGL(rt_bvh_rays_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64),
                            (unsigned)(kLdsWaveBytes + kBvhLdsBytes), c->stream, S, d_rays, n, d_idx, d_t, d_tally);
         if (chk(hipGetLastError(), "rt_bvh_rays_kernel") && chk(hipStreamSynchronize(c->stream), "sync") &&
@@ -3104,7 +2980,7 @@ RT_EXPORT int rt_debug_bvh_rays_wave(rt_ctx* c, const float* rays, int n, int* o
         chk(hipMalloc(&d_idx, (size_t)n * sizeof(int)), "hipMalloc") &&
         chk(hipMalloc(&d_t, (size_t)n * sizeof(float)), "hipMalloc") &&
         chk(hipMemcpy(d_rays, rays, (size_t)n * 6 * sizeof(float), hipMemcpyHostToDevice), "hipMemcpy")) {
-        const SceneDev S = scene_dev(c, false, nullptr);
+        const SceneDev S = scene_dev(c, false, false);
         // the shared stack, then lane 0's serial stack (one step: a row)
         const unsigned lds = (unsigned)(kWfStragCap * sizeof(int) + 64 * sizeof(int) * (size_t)c->bvh_depth);
         hipLaunchKernelGGL(rt_bvh_wave_kernel, dim3((unsigned)n), dim3(64), lds, c->stream, S, d_rays, n, d_idx, d_t);

@@ -160,8 +160,7 @@ def test_option_enum_matches_binding_and_round_trips():
     h = ctypes.c_void_p()
     assert L.rt_create_cpu(1, ctypes.byref(h)) == 0
     values = {"light_buffer": 2, "camera_buffer": 2, "union_pretest": 0, "lb_scale": 8, "dcov_near": 1.5,
-              "cb_inline_max_mb": 64, "host_chunk_mb": 4, "cb_capacity": 1000, "launch_camera": 0, "bvh": 0, "wavefront": 0,
-              "cb_envelope": 4}
+              "cb_inline_max_mb": 64, "host_chunk_mb": 4, "cb_capacity": 1000, "launch_camera": 0, "bvh": 0, "wavefront": 0}
     assert set(values) == set(enum)
     try:
         for name, v in values.items():

@@ -80,7 +80,7 @@ def test_partial_frame_lists_equal_brute_force(heightfield_path, rows, bands):
 
 
 @pytest.mark.parametrize("which,lc", [("scene2", 1), ("scene2", 0), ("scene7", 1), ("scene9", 1), ("hf", 1)])
-@pytest.mark.parametrize("kind", ["cams", "path"])
+@pytest.mark.parametrize("kind", ["cams", "path", "moving"])
 def test_moved_cameras_equal_reference(heightfield_path, which, lc, kind):
     """Synchronous renders (float32 RGB and RGBA8) of every moved camera of
     the set, one context for all of them, against _ref's frames (scene2 with
@@ -96,13 +96,14 @@ def test_moved_cameras_equal_reference(heightfield_path, which, lc, kind):
 
 @pytest.mark.parametrize("which,cbopt,lc", [("scene2", 1, 1), ("scene2", 1, 0), ("scene2", 2, 0), ("hf", 2, 1),
                                            ("hf", 1, 1), ("scene7", 1, 1), ("scene9", 1, 1)])
-def test_async_moving_camera_matches_reference(heightfield_path, which, cbopt, lc):
+@pytest.mark.parametrize("kind", ["path", "moving"])
+def test_async_moving_camera_matches_reference(heightfield_path, which, cbopt, lc, kind):
     """rt_render_async of a camera path, no host sync between frames: each
     new camera's records travel with the launch (scene2, lc 1), or its device
     state (and, with camera_buffer 2 or where it pays, its camera buffer) is
     built on the caller's stream; every frame is the reference's."""
     r = CamRef(which, heightfield_path)
-    frames = r.frames["path"]
+    frames = r.frames[kind]
     ctx = rt_amd.Context(0, camera_buffer=cbopt, launch_camera=lc)
     ctx.upload(r.scene)
     st = torch.cuda.current_stream()
@@ -118,7 +119,64 @@ def test_async_moving_camera_matches_reference(heightfield_path, which, cbopt, l
         if info[0] == 1.0:
             assert _verify(ctx)[0] == 0
     for i, o in enumerate(outs):
-        assert r.matches(o.cpu().numpy(), "path", i), (which, i)
+        assert r.matches(o.cpu().numpy(), kind, i), (which, i)
+    ctx.close()
+
+
+def test_moving_c3_full_size_matches_reference(heightfield_path):
+    """C3 (the 50k heightfield at 1920x1080, depth 0) under the bench's
+    translated camera (tests/cameras.py moving(), the per-frame move of a
+    display loop, Main.cpp:229-250 -> LancerRayons, Scene.cpp:674): seven
+    frames through rt_render_async (new cameras below 4 Mpx: the per-wave
+    path; a camera repeated once builds its lists), through
+    rt_render_sequence_async (the slots' own state) and synchronously (the
+    camera buffer of each camera); frames 3 and 6 against _ref's whole-frame
+    digests (tests/golden/cameras.json)."""
+    import hashlib
+
+    import numpy as np
+
+    from conftest import cam_golden
+
+    name, w, h, d, idx = cameras.MOVING_FULL
+    s = rt_amd.Scene(heightfield_path, w, h, d)
+    frames = cameras.moving(s.frame, max(idx) + 1)
+    g = cam_golden()
+
+    def key(i):
+        return f"{name}_{w}x{h}_d{d}_moving{i}"
+
+    def sha(a):
+        return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+    for i in idx:
+        assert g[key(i)]["camera_words_sha256"] == cameras.words_sha(frames[i])
+    ctx = rt_amd.Context(0)
+    ctx.upload(s)
+    st = torch.cuda.current_stream().cuda_stream
+    outs = []
+    for i, f in enumerate(frames):
+        o = torch.empty((h, w, 3), dtype=torch.float32, device="cuda")
+        ctx.render_async(f, 0, o.data_ptr(), st)
+        outs.append(o)
+        if i in idx:  # the same camera again: its second frame builds and walks its lists
+            o2 = torch.empty((h, w, 3), dtype=torch.float32, device="cuda")
+            ctx.render_async(f, 0, o2.data_ptr(), st)
+            outs.append(o2)
+    torch.cuda.synchronize()
+    k = 0
+    for i in range(len(frames)):
+        reps = 2 if i in idx else 1
+        for r_ in range(reps):
+            if i in idx:
+                assert sha(outs[k].cpu().numpy()) == g[key(i)]["rgb_f32_sha256"], ("async", i, r_)
+            k += 1
+    ring = torch.empty((len(frames), h, w, 4), dtype=torch.uint8, device="cuda")
+    ctx.render_sequence_async(frames, ring.data_ptr(), h * w * 4, 0, 0, st)
+    torch.cuda.synchronize()
+    for i in idx:
+        assert sha(ring[i].cpu().numpy()) == g[key(i)]["rgba8_sha256"], ("sequence", i)
+        assert sha(ctx.render_float(frames[i])) == g[key(i)]["rgb_f32_sha256"], ("sync", i)
     ctx.close()
 
 

@@ -46,6 +46,12 @@ for s in $STEPS; do
       run pmcx_wr_${CONFIG:-c2} 300 rocprofv3 --pmc WRITE_SIZE FETCH_SIZE --output-format csv -d gpurun_out/pmcx_${CONFIG:-c2} -o wr -- $B
       python tools/pmc_kernels.py gpurun_out/pmcx_${CONFIG:-c2} > gpurun_out/pmcx_${CONFIG:-c2}/kernels.json
       ;;
+    valumix)  # dynamic VALU instruction mix of a config's kernels
+      B="python bench.py --steps 5 --warmup 1 --settle-ms 0 --no-cpu-baseline --no-host-boundary --config ${CONFIG:-c2}"
+      run valumix_${CONFIG:-c2} 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_CVT SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 --output-format csv -d gpurun_out/valumix_${CONFIG:-c2} -o mix -- $B
+      run valumix2_${CONFIG:-c2} 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_INSTS_VMEM SQ_INSTS_LDS SQ_INSTS_VALU_FLOPS_FP32 SQ_INSTS_VALU_IOPS --output-format csv -d gpurun_out/valumix_${CONFIG:-c2} -o mix2 -- $B
+      python tools/pmc_kernels.py gpurun_out/valumix_${CONFIG:-c2} > gpurun_out/valumix_${CONFIG:-c2}/kernels.json
+      ;;
     ab) run ab_${CONFIG:-c2} 600 python tools/ab_variants.py --config ${CONFIG:-c2} ray-tracing-gpu_amd/lib/var/*.so ;;
     abenv) run abenv_${CONFIG:-c2} 600 python tools/ab_variants.py --config ${CONFIG:-c2} $AB_ARGS ;;
     pmcvar)
