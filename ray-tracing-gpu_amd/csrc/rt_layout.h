@@ -160,7 +160,12 @@ struct WfDev {
 __host__ __device__ inline int wf_rays(int L, int s) { return (L * kWfSeg + s) * kWfCntStride; }
 __host__ __device__ inline int wf_pars(int L, int s) { return ((kWfMaxLevels + 1 + L) * kWfSeg + s) * kWfCntStride; }
 __host__ __device__ inline int wf_strag(int L) { return (2 * (kWfMaxLevels + 1) * kWfSeg + L) * kWfCntStride; }
-constexpr size_t kWfCountBytes = (size_t)(2 * (kWfMaxLevels + 1) * kWfSeg + kWfMaxLevels + 1) * kWfCntStride * 4;
+// the trace launch's fetch cursor of level L (rays handed to lanes so far)
+__host__ __device__ inline int wf_fetch(int L)
+{
+    return (2 * (kWfMaxLevels + 1) * kWfSeg + kWfMaxLevels + 1 + L) * kWfCntStride;
+}
+constexpr size_t kWfCountBytes = (size_t)(2 * (kWfMaxLevels + 1) * kWfSeg + 2 * (kWfMaxLevels + 1)) * kWfCntStride * 4;
 
 struct FrameDev {
     float cam[3];

@@ -155,6 +155,23 @@ __device__ __forceinline__ void wf_tally(const Counters& cnt, StatsDev* __restri
     }
 }
 
+// Persistent lanes (round 5): a lane whose walk ends takes the queue's next
+// ray instead of idling until its wave's longest walk ends (the level's rays
+// skim a rough mesh: walks of 10 to 200+ steps side by side, VALU lane
+// utilisation 0.28 with one ray per lane per wave round).  Each round the
+// free lanes refill from the level's fetch cursor — one atomic per wave,
+// only once at least kWfRefill lanes are free (or none is busy), so the
+// cursor sees a few atomics per 64 rays — then every busy lane takes one
+// while-while round of its walk (closest_hit_bvh's, step for step: inner
+// nodes until every busy lane holds a leaf, then the leaves).  A lane's
+// ray, its stack (its own LDS column), bounds and order are its walk alone,
+// so each ray's minimum is closest_hit_bvh's; the budget and the straggler
+// hand-off are unchanged.
+#ifndef RT_WF_REFILL
+#define RT_WF_REFILL 32
+#endif
+constexpr int kWfRefill = RT_WF_REFILL;
+
 template <bool COUNT>
 __global__ __launch_bounds__(64) void rt_wf_trace(const SceneDev S, const FrameDev F, int L,
                                                   StatsDev* __restrict__ stats)
@@ -162,29 +179,144 @@ __global__ __launch_bounds__(64) void rt_wf_trace(const SceneDev S, const FrameD
     const WfQueue Q = wf_queue(F.wf.count, wf_rays(L, 0), F.wf.seg[L]);
     const unsigned n = Q.pre[kWfSeg];
     const float4* __restrict__ q = F.wf.ray[L];
+    unsigned* const cursor = F.wf.count + wf_fetch(L);
+    int* const stk = bvh_stack<0>();
+    const int lane = (int)(threadIdx.x & 63);
+    constexpr int kDone = 0x7fffffff;
     Counters cnt;
-    for (unsigned base = blockIdx.x * 64u; base < n; base += gridDim.x * 64u) {
-        const unsigned x = base + (threadIdx.x & 63u);
-        if (x < n) {
-            const unsigned i = wf_slot(Q, x);
-            const float4 r0 = q[2 * (size_t)i], r1 = q[2 * (size_t)i + 1];
-            ++cnt.bounce;
-            float t;
-            bool str = false;
-            const int idx =
-                closest_hit_bvh<0, RT_WF_BUDGET>(S, make3(r0.x, r0.y, r0.z), make3(r1.x, r1.y, r1.z), t, cnt, &str);
-            // a walk past the budget goes to the straggler queue with its
-            // partial minimum (rt_wf_straggle finishes it with a whole wave)
-            const unsigned long long bs = __ballot(str);
-            if (bs) {
-                const int lead = (int)__builtin_ctzll(__ballot(true));
-                unsigned sb = 0u;
-                if ((int)(threadIdx.x & 63) == lead) sb = atomicAdd(&F.wf.count[wf_strag(L)], (unsigned)__popcll(bs));
-                sb = (unsigned)__builtin_amdgcn_readlane((int)sb, lead);
-                if (str) F.wf.strag[sb + lane_rank(bs)] = make_int4((int)i, __float_as_int(t), idx, 0);
+    bool busy = false, more = true;  // more: the cursor has not passed n (wave-uniform)
+    unsigned slot = 0u;
+    Vec3 O = make3(0.f, 0.f, 0.f), D = O, inv = O;
+    float bt = -1.0f;
+    int bi = -1, node = kDone, leaf = 0, sp = 0, steps = 0;
+    for (;;) {
+        const unsigned long long fm = __ballot(!busy);
+        if (more && fm && (__popcll(fm) >= kWfRefill || !__any(busy))) {
+            const int lead = (int)__builtin_ctzll(fm);
+            unsigned b = 0u;
+            if (lane == lead) b = atomicAdd(cursor, (unsigned)__popcll(fm));
+            b = (unsigned)__builtin_amdgcn_readlane((int)b, lead);
+            more = b + (unsigned)__popcll(fm) < n;
+            const unsigned x = b + lane_rank(fm);
+            if (!busy && x < n) {
+                slot = wf_slot(Q, x);
+                const float4 r0 = q[2 * (size_t)slot], r1 = q[2 * (size_t)slot + 1];
+                O = make3(r0.x, r0.y, r0.z);
+                D = make3(r1.x, r1.y, r1.z);
+                ++cnt.bounce;
+                // closest_hit_bvh's prologue: planes, quadrics, the walk test
+                bt = -1.0f;
+                bi = -1;
+                for (int k = 0; k < S.n_plane; ++k) {
+                    const float4 a = S.plane[2 * k], c = S.plane[2 * k + 1];
+                    float t;
+                    ++cnt.pla;
+                    const bool ok = hit_plane(make_float4(0.f, a.x, a.y, a.z), make_float4(a.w, 0.f, 0.f, 0.f), O, D, t);
+                    take_min(ok, t, __float_as_int(c.x), bt, bi);
+                }
+                for (int k = 0; k < S.n_quad; ++k) {
+                    const float4* r = S.quad + 3 * k;
+                    const float4 a = r[0], c = r[1], e = r[2];
+                    float t;
+                    ++cnt.qua;
+                    const bool ok = hit_quadric(make_float4(0.f, a.x, a.y, a.z), make_float4(a.w, c.x, c.y, c.z),
+                                                make_float4(c.w, e.x, e.y, 0.f), O, D, t);
+                    take_min(ok, t, __float_as_int(e.z), bt, bi);
+                }
+                const float dd = dot(D, D);
+                if (finite3(O) & finite3(D) & (dd >= 0.98f) & (dd <= 1.02f)) {
+                    inv = make3(__builtin_amdgcn_rcpf(D.x), __builtin_amdgcn_rcpf(D.y), __builtin_amdgcn_rcpf(D.z));
+                    node = 0;
+                    leaf = 0;
+                    sp = 0;
+                    steps = 0;
+                    busy = true;
+                } else {  // every triangle (closest_hit_bvh's non-walk branch)
+                    for (int k = 0; k < S.n_tri; ++k) {
+                        const TriRec tr = load_tri(S, k);
+                        ++cnt.tri;
+                        ++cnt.btri;
+                        float t;
+                        const bool ok = hit_triangle(make_float4(0.f, tr.p0.x, tr.p0.y, tr.p0.z),
+                                                     make_float4(tr.e1.x, tr.e1.y, tr.e1.z, tr.e2.x),
+                                                     make_float4(tr.e2.y, tr.e2.z, 0.f, 0.f), O, D, t);
+                        take_min(ok, t, tr.idx, bt, bi);
+                    }
+                    F.wf.hit[slot] = make_float2(__int_as_float(bi), bt);
+                }
             }
-            if (!str) F.wf.hit[i] = make_float2(__int_as_float(idx), t);
         }
+        if (!__any(busy)) {
+            if (!more) break;
+            continue;
+        }
+        // one while-while round of every busy lane's walk
+        bool fin = false, str = false;
+        if (busy) {
+            while ((node >= 0) & (node != kDone)) {
+                if (++steps > RT_WF_BUDGET) break;
+                const float4* nd = S.bvh_node + 4 * (size_t)node;
+                const float4 a0 = nd[0], a1 = nd[1], b0 = nd[2], b1 = nd[3];
+                ++cnt.bnode;
+                const int r0 = __float_as_int(a1.w), r1 = __float_as_int(b1.w);
+                float t0, t1;
+                const bool have = bi >= 0;
+                const bool h0 = bvh_box(a0, a1, O, inv, have, bt, t0);
+                const bool h1 = bvh_box(b0, b1, O, inv, have, bt, t1);
+                if (h0 & h1) {
+                    const bool near0 = !(t1 < t0);
+                    stk[64 * sp] = near0 ? r1 : r0;
+                    ++sp;
+                    node = near0 ? r0 : r1;
+                } else if (h0 | h1) {
+                    node = h0 ? r0 : r1;
+                } else {
+                    node = sp > 0 ? stk[64 * --sp] : kDone;
+                }
+                if ((node < 0) & (leaf == 0)) {  // postpone the first leaf, walk on
+                    leaf = node;
+                    node = sp > 0 ? stk[64 * --sp] : kDone;
+                }
+                if (__all(leaf != 0)) break;
+            }
+            if (steps > RT_WF_BUDGET) {
+                str = true;
+            } else {
+                while (leaf != 0) {
+                    const unsigned enc = ~(unsigned)leaf;
+                    const int first = (int)(enc >> 4), count = (int)(enc & 15u) + 1;
+                    for (int k = first; k < first + count; ++k) {
+                        const float4* r = S.bvh_tri + 3 * (size_t)k;
+                        const float4 a = r[0], c = r[1], e = r[2];
+                        ++cnt.tri;
+                        ++cnt.btri;
+                        float t;
+                        const bool ok = hit_triangle(make_float4(0.f, a.x, a.y, a.z), make_float4(a.w, c.x, c.y, c.z),
+                                                     make_float4(c.w, e.x, 0.f, 0.f), O, D, t);
+                        take_min(ok, t, __float_as_int(e.y), bt, bi);
+                    }
+                    leaf = 0;
+                    if ((node < 0) & (node != kDone)) {  // the leaf that ended the inner loop
+                        leaf = node;
+                        node = sp > 0 ? stk[64 * --sp] : kDone;
+                    }
+                    ++steps;
+                }
+                fin = node == kDone;
+            }
+        }
+        // a walk past the budget goes to the straggler queue with its partial
+        // minimum (rt_wf_straggle finishes it with a whole wave)
+        const unsigned long long bs = __ballot(str);
+        if (bs) {
+            const int lead = (int)__builtin_ctzll(bs);
+            unsigned sb = 0u;
+            if (lane == lead) sb = atomicAdd(&F.wf.count[wf_strag(L)], (unsigned)__popcll(bs));
+            sb = (unsigned)__builtin_amdgcn_readlane((int)sb, lead);
+            if (str) F.wf.strag[sb + lane_rank(bs)] = make_int4((int)slot, __float_as_int(bt), bi, 0);
+        }
+        if (fin) F.wf.hit[slot] = make_float2(__int_as_float(bi), bt);
+        if (fin | str) busy = false;
     }
     if (COUNT && (F.flags & RT_FLAG_STATS)) wf_tally<COUNT>(cnt, stats);
 }

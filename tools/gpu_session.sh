@@ -25,7 +25,7 @@ for s in $STEPS; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 400 python bench.py ;;
     bench_all)
-      for c in c1 c2 c3 c4 c4s7 c4s9 c5; do run bench_$c 400 python bench.py --config $c --cpu-seconds 5; done ;;
+      for c in ${CONFIGS:-c1 c2 c3 c4 c4s7 c4s9 c5 c3r c5r}; do run bench_$c 400 python bench.py --config $c --cpu-seconds 5; done ;;
     bench_big)
       for c in ${CONFIGS:-c3 c5}; do run bench_$c 400 python bench.py --config $c --steps 10 --no-cpu-baseline; done ;;
     bench_one) run bench_${CONFIG:-c2} 400 python bench.py --config ${CONFIG:-c2} --steps 20 --no-cpu-baseline ;;
@@ -43,7 +43,8 @@ for s in $STEPS; do
       B="python bench.py --steps 5 --warmup 1 --settle-ms 0 --no-cpu-baseline --no-host-boundary --config ${CONFIG:-c2}"
       run pmcx_l2_${CONFIG:-c2} 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum --output-format csv -d gpurun_out/pmcx_${CONFIG:-c2} -o l2 -- $B
       run pmcx_sq_${CONFIG:-c2} 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VMEM SQ_THREAD_CYCLES_VALU --output-format csv -d gpurun_out/pmcx_${CONFIG:-c2} -o sq -- $B
-      run pmcx_wr_${CONFIG:-c2} 300 rocprofv3 --pmc WRITE_SIZE FETCH_SIZE --output-format csv -d gpurun_out/pmcx_${CONFIG:-c2} -o wr -- $B
+      run pmcx_wr_${CONFIG:-c2} 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcx_${CONFIG:-c2} -o wr -- $B
+      run pmcx_fe_${CONFIG:-c2} 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcx_${CONFIG:-c2} -o fe -- $B
       python tools/pmc_kernels.py gpurun_out/pmcx_${CONFIG:-c2} > gpurun_out/pmcx_${CONFIG:-c2}/kernels.json
       ;;
     valumix)  # dynamic VALU instruction mix of a config's kernels
