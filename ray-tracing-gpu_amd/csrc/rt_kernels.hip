@@ -26,6 +26,7 @@
 //    bottom-up in the reference's order: ((local + C_refl*Kr) + C_refr*Kt);
 //  * no FMA contraction, IEEE f32 division and sqrt.
 #include <hip/hip_runtime.h>
+#include <hipcub/device/device_radix_sort.hpp>
 
 #include <algorithm>
 #include <chrono>
@@ -97,7 +98,8 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
         const Vec3 P = O + t * D;
         const Color c = shade_local<LB, WAVE>(S, m, P, N, D, cnt, hit & live);
         if constexpr ((WAVE & 512) != 0)
-            deferred = wf_children(F, 0, hit & live, m, P, N, D, 1.0f, 1.0f, c, pix, blockIdx.x + blockIdx.y * gridDim.x);
+            deferred = wf_children(F, 0, hit & live, m, P, N, D, 1.0f, 1.0f, c, pix, blockIdx.x + blockIdx.y * gridDim.x,
+                                   sidx);
         return hit ? c : bg;
     } else if constexpr ((WAVE & 1024) != 0) {
         // Reflect-only scenes (no Kt can pass the gate: the host's kt_max <= 0
@@ -753,6 +755,12 @@ struct rt_ctx {
         size_t cap[kWfMaxLevels + 1] = {};   // ray slots per level (level 0: pixels)
         size_t pcap[kWfMaxLevels + 1] = {};  // parent-list slots per level
         WfDev dev{};
+        // coherence sort (RT_WF_SORT): key buffers of `kcap` rays, the
+        // radix sort's scratch
+        unsigned long long *kin = nullptr, *kout = nullptr;
+        size_t kcap = 0;
+        void* stemp = nullptr;
+        size_t stemp_bytes = 0;
         hipEvent_t ev = nullptr;  // after the last wavefront frame
         hipStream_t last = nullptr;
         bool pending = false;
@@ -1034,6 +1042,9 @@ RT_EXPORT void rt_destroy(rt_ctx* c)
     hipFree(c->d_bvh_node);
     hipFree(c->d_bvh_tri);
     hipFree(c->wf.mem);
+    hipFree(c->wf.kin);
+    hipFree(c->wf.kout);
+    hipFree(c->wf.stemp);
     if (c->wf.ev) hipEventDestroy(c->wf.ev);
     for (auto& q : c->tiny_masks) {
         hipFree(q.d);
@@ -2158,6 +2169,14 @@ static int wf_branch(const rt_ctx* c) { return (c->kr_max > 0.0f ? 1 : 0) + (c->
 #ifndef RT_WF_TRACE_WAVES
 #define RT_WF_TRACE_WAVES 32  // trace launch: workgroups (one wave each) per CU
 #endif
+#ifndef RT_WF_SORT
+// each level's rays sorted by (parent surface, branch) before its trace,
+// for frames whose level queues hold at least this many ray slots: the
+// sort runs over the queue's capacity (the host never reads the count),
+// which at c3r (2.1 M slots) costs more than the coherence returns (+6%),
+// at c5r (33 M) less (-6%) — tools/ab_variants.py, profiles/r05/wfsort/
+#define RT_WF_SORT (6u << 20)
+#endif
 #ifndef RT_WF_MAX_GB
 #define RT_WF_MAX_GB 32.0
 #endif
@@ -2256,6 +2275,27 @@ static int wf_ensure(rt_ctx* c, const rt_frame* f, int rows, int levels, bool ca
     d.hit = (float2*)take(w.most * 8);
     d.strag = (int4*)take(w.most * 16);
     d.levels = levels;
+    d.kin = nullptr;
+    d.kout = nullptr;
+    if (RT_WF_SORT && levels >= 1 && w.cap[1] >= (size_t)RT_WF_SORT) {
+        if (w.most > W.kcap) {
+            free_later(c, W.kin);
+            free_later(c, W.kout);
+            free_later(c, W.stemp);
+            W.kin = W.kout = nullptr;
+            W.stemp = nullptr;
+            W.kcap = 0;
+            HIP_TRY(c, hipMalloc((void**)&W.kin, w.most * sizeof(unsigned long long)));
+            HIP_TRY(c, hipMalloc((void**)&W.kout, w.most * sizeof(unsigned long long)));
+            size_t tb = 0;
+            HIP_TRY(c, hipcub::DeviceRadixSort::SortKeys(nullptr, tb, (const unsigned long long*)nullptr,
+                                                          (unsigned long long*)nullptr, (int)w.most, 32, 64));
+            HIP_TRY(c, hipMalloc(&W.stemp, std::max<size_t>(tb, 16)));
+            W.stemp_bytes = std::max<size_t>(tb, 16);
+            W.kcap = w.most;
+        }
+        d.kin = W.kin;
+    }
     for (int L = 0; L <= levels; ++L) {
         W.cap[L] = L == 0 ? px : w.cap[L];
         W.pcap[L] = w.pcap[L];
@@ -2288,17 +2328,32 @@ static int wf_levels(rt_ctx* c, const SceneDev& S, const FrameDev& F, int levels
                          : (count ? (const void*)&rt_wf_shade<5, true> : (const void*)&rt_wf_shade<5, false>);
     const unsigned lds_t = (unsigned)((size_t)c->bvh_depth * 64 * sizeof(int));
     const unsigned lds_s = big ? (unsigned)kLdsWaveBytes : 0u;
+    rt_ctx::WfBuf& W = c->wf;
+    // the sort keys' significant bits: (surface x 2 + 1) < 2^bits - 1, so an
+    // empty slot's all-ones key sorts after every ray
+    int bits = 1;
+    while (((size_t)1 << bits) < 2 * (size_t)c->n_surf + 3) ++bits;
     for (int L = 1; L <= levels; ++L) {
         // enough waves to fill the chip; each strides over the level's queue
-        const size_t waves = (c->wf.cap[L] + 63) / 64;
+        const size_t waves = (W.cap[L] + 63) / 64;
         const unsigned gt = (unsigned)std::max<size_t>(1, std::min<size_t>(waves, (size_t)c->n_cu * RT_WF_TRACE_WAVES));
         const unsigned gs = (unsigned)std::max<size_t>(1, std::min<size_t>(waves, (size_t)c->n_cu * 16));
         FrameDev Fl = F;
+        if (W.dev.kin) {
+            // the level's rays by (parent surface, branch): rays leaving one
+            // triangle share its normal, so their walks and hits stay together
+            size_t tb = W.stemp_bytes;
+            HIP_TRY(c, hipcub::DeviceRadixSort::SortKeys(W.stemp, tb, (const unsigned long long*)W.kin, W.kout,
+                                                          (int)W.cap[L], 32, 32 + bits, st));
+            Fl.wf.kout = W.kout;
+        }
         int Lv = L;
         void* args[] = {(void*)&S, (void*)&Fl, (void*)&Lv, (void*)&stats};
         HIP_TRY(c, hipLaunchKernel(kt, dim3(gt), dim3(64), args, lds_t, st));
         HIP_TRY(c, hipLaunchKernel(kg, dim3((unsigned)c->n_cu * 4), dim3(64), args,
                                    (unsigned)(kWfStragCap * sizeof(int)), st));
+        if (W.dev.kin && L < levels)  // the next level's keys, written by the shade launch
+            HIP_TRY(c, hipMemsetAsync(W.kin, 0xFF, W.cap[L + 1] * sizeof(unsigned long long), st));
         HIP_TRY(c, hipLaunchKernel(ks, dim3(gs), dim3(64), args, lds_s, st));
     }
     for (int L = levels - 1; L >= 0; --L) {
@@ -2397,6 +2452,8 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
         rt_ctx::WfBuf& W = c->wf;
         if (W.pending && W.last != st) HIP_TRY(c, hipStreamWaitEvent(st, W.ev, 0));
         HIP_TRY(c, hipMemsetAsync(W.dev.count, 0, kWfCountBytes, st));
+        if (W.dev.kin)  // level 1's keys: empty slots sort last
+            HIP_TRY(c, hipMemsetAsync(W.dev.kin, 0xFF, W.cap[1] * sizeof(unsigned long long), st));
     }
     if (nch <= 1) {
         if (int rc = launch_trace(c, kp, tiny, f->flags & RT_FLAG_STATS, S, F, f->width, rows, rgba_dev, rgb_dev, stats,

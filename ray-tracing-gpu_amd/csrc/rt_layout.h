@@ -154,6 +154,12 @@ struct WfDev {
     float2* hit;      // the level being shaded: [file index (int bits), t] per ray slot
     int4* strag;      // the level's straggling walks: [ray slot, partial t (bits), partial index, -]
     unsigned* count;  // counters, kWfCntStride words apart: wf_rays / wf_pars / wf_strag
+    // Coherence sort (RT_WF_SORT): the rays being appended write sort keys
+    // (parent surface x 2 + refracted) << 32 | slot into kin (empty slots all
+    // ones); the host sorts them into kout before the level's trace, and the
+    // trace and shade launches take rays in kout's order (null: queue order).
+    unsigned long long* kin;
+    const unsigned long long* kout;
     int levels;
 };
 // counter of segment s of level L's rays / parents; level L's stragglers

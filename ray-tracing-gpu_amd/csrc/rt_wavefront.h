@@ -78,7 +78,7 @@ __device__ __forceinline__ unsigned wf_slot(const WfQueue& q, unsigned x)
 // tile) index, which picks its segments.
 __device__ __forceinline__ bool wf_children(const FrameDev& F, int L, bool act, const Mat& m, const Vec3 P,
                                             const Vec3 N, const Vec3 D, float rior, float energy, const Color acc,
-                                            unsigned self, unsigned chunk)
+                                            unsigned self, unsigned chunk, int surf)
 {
     const float er = m.kr * energy;
     const float et = m.kt * energy;
@@ -106,6 +106,7 @@ __device__ __forceinline__ bool wf_children(const FrameDev& F, int L, bool act, 
         const Vec3 Dr = reflect(D, N);
         q[2 * (size_t)cR] = make_float4(P.x, P.y, P.z, 0.0f);
         q[2 * (size_t)cR + 1] = make_float4(Dr.x, Dr.y, Dr.z, er);
+        if (F.wf.kin) F.wf.kin[cR] = ((unsigned long long)(2u * (unsigned)surf) << 32) | (unsigned)cR;
     }
     if (doT) {
         cT = (int)(base + (unsigned)__popcll(bR) + lane_rank(bT));
@@ -122,6 +123,7 @@ __device__ __forceinline__ bool wf_children(const FrameDev& F, int L, bool act, 
         const Vec3 Dt = refract(D, n, ratio);
         q[2 * (size_t)cT] = make_float4(P.x, P.y, P.z, rior_t);
         q[2 * (size_t)cT + 1] = make_float4(Dt.x, Dt.y, Dt.z, et);
+        if (F.wf.kin) F.wf.kin[cT] = ((unsigned long long)(2u * (unsigned)surf + 1u) << 32) | (unsigned)cT;
     }
     if (doR | doT) {
         float4* nd = F.wf.node[L] + 2 * (size_t)self;
@@ -199,7 +201,7 @@ __global__ __launch_bounds__(64) void rt_wf_trace(const SceneDev S, const FrameD
             more = b + (unsigned)__popcll(fm) < n;
             const unsigned x = b + lane_rank(fm);
             if (!busy && x < n) {
-                slot = wf_slot(Q, x);
+                slot = F.wf.kout ? (unsigned)F.wf.kout[x] : wf_slot(Q, x);
                 const float4 r0 = q[2 * (size_t)slot], r1 = q[2 * (size_t)slot + 1];
                 O = make3(r0.x, r0.y, r0.z);
                 D = make3(r1.x, r1.y, r1.z);
@@ -361,7 +363,7 @@ __global__ __launch_bounds__(64) void rt_wf_shade(const SceneDev S, const FrameD
     for (unsigned base = blockIdx.x * 64u; base < n; base += gridDim.x * 64u) {
         const unsigned x = base + (threadIdx.x & 63u);
         if (x < n) {
-            const unsigned i = wf_slot(Q, x);
+            const unsigned i = F.wf.kout ? (unsigned)F.wf.kout[x] : wf_slot(Q, x);
             const float2 h = F.wf.hit[i];
             const int idx = __float_as_int(h.x);
             Color res = bg;
@@ -378,7 +380,7 @@ __global__ __launch_bounds__(64) void rt_wf_shade(const SceneDev S, const FrameD
 #else
                 res = shade_local<1, WAVE>(S, m, P, N, D, cnt);
 #endif
-                parent = wf_children(F, L, true, m, P, N, D, r0.w, r1.w, res, i, base / 64u);
+                parent = wf_children(F, L, true, m, P, N, D, r0.w, r1.w, res, i, base / 64u, idx);
             }
             if (!parent) F.wf.res[L][i] = make_float4(res.r, res.g, res.b, 0.0f);
         }
