@@ -1090,7 +1090,10 @@ static bool nonneg_finite(float v) { return std::isfinite(v) && !std::signbit(v)
 
 // 256 camera records = 16 KB, the scalar data cache.
 static constexpr int kTricamMaxTriangles = 256;
-static constexpr int kEdgeMaxTriangles = 1024;
+#ifndef RT_EDGE_MAX_TRIANGLES
+#define RT_EDGE_MAX_TRIANGLES 0x7fffffff  // every list size (SceneDev::use_edges)
+#endif
+static constexpr int kEdgeMaxTriangles = RT_EDGE_MAX_TRIANGLES;
 // two-level (clustered) culling above this many triangles
 static constexpr int kClusterMinTriangles = 1024;
 

@@ -59,9 +59,12 @@ struct SceneDev {
     // scalar cache they win (C2: -3%), past it the extra misses lose (C3: +10%,
     // tools/ab_variants.py), so the host enables them for small lists only.
     int use_tricam;
-    // wave-level edge-plane test on sphere survivors (small triangle lists:
-    // loose spheres of large triangles; on big lists it costs more than it
-    // culls — C2 -22%, C3 +14%, tools/ab_variants.py)
+    // wave-level edge-plane test on sphere survivors: small triangle lists
+    // (loose spheres of large triangles, C2 -22%, round 1) and, since round
+    // 5, big lists too — the clustered per-wave path of a new camera stages
+    // its survivors, so every survivor the edges reject saves a wave-serial
+    // exact test: C3 moving camera 0.386 -> 0.334 ms, static frames flat
+    // (round 1 measured C3 +14% before the staged batches)
     int use_edges;
     // Bounding-cone culling (exact: it only skips triangles no lane's ray can
     // reach).  Per (apex, triangle), 2 float4: [dir-to-sphere-centre, cosT]
