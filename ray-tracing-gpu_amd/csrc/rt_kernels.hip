@@ -2170,7 +2170,38 @@ static int prepare_state(rt_ctx* c, const rt_frame* f, hipStream_t st, bool sync
 static int wf_branch(const rt_ctx* c) { return (c->kr_max > 0.0f ? 1 : 0) + (c->kt_max > 0.0f ? 1 : 0); }
 
 #ifndef RT_WF_TRACE_WAVES
-#define RT_WF_TRACE_WAVES 32  // trace launch: workgroups (one wave each) per CU
+// trace launch: workgroups (one wave each) per CU.  Fewer than the 32 that
+// fit (59 VGPRs, depth x 256 B of LDS) run faster: c3r 3.447 / 3.359 / 3.355
+// / 3.338 ms at 32 / 24 / 20 / 16, c5r 21.23 / 21.16 / 21.26 / 21.59
+// (profiles/r05/sorder/ab_trace_waves.log)
+#define RT_WF_TRACE_WAVES 24
+#endif
+// Steps a lane's walk may take in the trace launch before the straggler
+// launch finishes it with a whole wave.  Small levels (under
+// RT_WF_BUDGET_SPLIT ray slots, ~2 rays per lane) are dominated by the trace
+// launch's tail of long walks and hand off early; big ones (tens of rays
+// per lane) hide that tail and keep more walks on the lanes.  Measured
+// (profiles/r05/sorder/ab_budget.log): c3r (2.1 M slots) 2.944 / 2.973 /
+// 2.983 ms at 128 / 112 / 160; c5r (33 M) 19.17 / 18.97 / 18.97 at 256 /
+// 320 / 384.
+#ifndef RT_WF_BUDGET_SMALL
+#define RT_WF_BUDGET_SMALL 128
+#endif
+#ifndef RT_WF_BUDGET_BIG
+#define RT_WF_BUDGET_BIG 320
+#endif
+#ifndef RT_WF_BUDGET_SPLIT
+#define RT_WF_BUDGET_SPLIT (6u << 20)
+#endif
+#ifndef RT_WF_STRAG_WAVES
+// straggler launch: workgroups (one wave, one straggling ray at a time, its
+// kWfStragCap-entry LDS stack) per CU: 4 / 8 / 16 waves of 16 / 16 / 8 KB,
+// c3r 3.359 / 3.273 / 3.249 ms, c5r 21.13 / 19.80 / 19.19
+// (profiles/r05/sorder/ab_straggle*.log)
+#define RT_WF_STRAG_WAVES 16
+#endif
+#ifndef RT_WF_SHADE_WAVES
+#define RT_WF_SHADE_WAVES 24  // shade launch: workgroups (one wave each) per CU (= its occupancy)
 #endif
 #ifndef RT_WF_SORT
 // each level's rays sorted by (parent surface, branch) before its trace,
@@ -2340,8 +2371,9 @@ static int wf_levels(rt_ctx* c, const SceneDev& S, const FrameDev& F, int levels
         // enough waves to fill the chip; each strides over the level's queue
         const size_t waves = (W.cap[L] + 63) / 64;
         const unsigned gt = (unsigned)std::max<size_t>(1, std::min<size_t>(waves, (size_t)c->n_cu * RT_WF_TRACE_WAVES));
-        const unsigned gs = (unsigned)std::max<size_t>(1, std::min<size_t>(waves, (size_t)c->n_cu * 16));
+        const unsigned gs = (unsigned)std::max<size_t>(1, std::min<size_t>(waves, (size_t)c->n_cu * RT_WF_SHADE_WAVES));
         FrameDev Fl = F;
+        Fl.wf.budget = W.cap[L] >= (size_t)RT_WF_BUDGET_SPLIT ? RT_WF_BUDGET_BIG : RT_WF_BUDGET_SMALL;
         if (W.dev.kin) {
             // the level's rays by (parent surface, branch): rays leaving one
             // triangle share its normal, so their walks and hits stay together
@@ -2353,7 +2385,7 @@ static int wf_levels(rt_ctx* c, const SceneDev& S, const FrameDev& F, int levels
         int Lv = L;
         void* args[] = {(void*)&S, (void*)&Fl, (void*)&Lv, (void*)&stats};
         HIP_TRY(c, hipLaunchKernel(kt, dim3(gt), dim3(64), args, lds_t, st));
-        HIP_TRY(c, hipLaunchKernel(kg, dim3((unsigned)c->n_cu * 4), dim3(64), args,
+        HIP_TRY(c, hipLaunchKernel(kg, dim3((unsigned)c->n_cu * RT_WF_STRAG_WAVES), dim3(64), args,
                                    (unsigned)(kWfStragCap * sizeof(int)), st));
         if (W.dev.kin && L < levels)  // the next level's keys, written by the shade launch
             HIP_TRY(c, hipMemsetAsync(W.kin, 0xFF, W.cap[L + 1] * sizeof(unsigned long long), st));

@@ -164,6 +164,7 @@ struct WfDev {
     unsigned long long* kin;
     const unsigned long long* kout;
     int levels;
+    int budget;  // steps (inner nodes + leaves) a trace-launch walk takes before the straggler hand-off
 };
 // counter of segment s of level L's rays / parents; level L's stragglers
 __host__ __device__ inline int wf_rays(int L, int s) { return (L * kWfSeg + s) * kWfCntStride; }

@@ -27,11 +27,6 @@
 
 #pragma clang fp contract(off)
 
-// Steps (inner nodes + leaves) a lane's BVH walk may take in the trace
-// kernel before it is handed to the straggler kernel.
-#ifndef RT_WF_BUDGET
-#define RT_WF_BUDGET 256
-#endif
 
 namespace rt {
 
@@ -256,7 +251,7 @@ __global__ __launch_bounds__(64) void rt_wf_trace(const SceneDev S, const FrameD
         bool fin = false, str = false;
         if (busy) {
             while ((node >= 0) & (node != kDone)) {
-                if (++steps > RT_WF_BUDGET) break;
+                if (++steps > F.wf.budget) break;
                 const float4* nd = S.bvh_node + 4 * (size_t)node;
                 const float4 a0 = nd[0], a1 = nd[1], b0 = nd[2], b1 = nd[3];
                 ++cnt.bnode;
@@ -281,7 +276,7 @@ __global__ __launch_bounds__(64) void rt_wf_trace(const SceneDev S, const FrameD
                 }
                 if (__all(leaf != 0)) break;
             }
-            if (steps > RT_WF_BUDGET) {
+            if (steps > F.wf.budget) {
                 str = true;
             } else {
                 while (leaf != 0) {
@@ -325,7 +320,10 @@ __global__ __launch_bounds__(64) void rt_wf_trace(const SceneDev S, const FrameD
 
 // The straggling walks of level L, one ray per wave (bvh_walk_wave: the
 // wave's LDS stack of kWfStragCap references).
-constexpr int kWfStragCap = 4096;
+#ifndef RT_WF_STRAG_CAP
+#define RT_WF_STRAG_CAP 2048
+#endif
+constexpr int kWfStragCap = RT_WF_STRAG_CAP;
 template <bool COUNT>
 __global__ __launch_bounds__(64) void rt_wf_straggle(const SceneDev S, const FrameDev F, int L,
                                                      StatsDev* __restrict__ stats)
@@ -351,8 +349,16 @@ __global__ __launch_bounds__(64) void rt_wf_straggle(const SceneDev S, const Fra
     }
 }
 
+// Occupancy: at the compiler's free choice the shade kernel takes 87 VGPRs
+// (5 waves per SIMD) and its light-buffer walks are latency-bound (L2 hit
+// rate 0.29 on scattered hit points); bounded to 6 waves per SIMD it fits
+// 80 VGPRs without spilling: c3r -5.8%, c5r -6.3% with a grid of 24 waves
+// per CU (profiles/r05/sorder/ab_shade_occupancy*.log).
+#ifndef RT_WF_SHADE_EU
+#define RT_WF_SHADE_EU 6
+#endif
 template <int WAVE, bool COUNT>
-__global__ __launch_bounds__(64) void rt_wf_shade(const SceneDev S, const FrameDev F, int L,
+__global__ __launch_bounds__(64, RT_WF_SHADE_EU) void rt_wf_shade(const SceneDev S, const FrameDev F, int L,
                                                   StatsDev* __restrict__ stats)
 {
     const WfQueue Q = wf_queue(F.wf.count, wf_rays(L, 0), F.wf.seg[L]);
