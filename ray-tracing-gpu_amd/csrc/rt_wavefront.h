@@ -164,8 +164,11 @@ __device__ __forceinline__ void wf_tally(const Counters& cnt, StatsDev* __restri
 // ray, its stack (its own LDS column), bounds and order are its walk alone,
 // so each ray's minimum is closest_hit_bvh's; the budget and the straggler
 // hand-off are unchanged.
+// (refill at 16 / 32 / 48 free lanes, with the launch shapes of
+// profiles/r05/sorder/: c3r 3.110 / 2.945 / 2.933 ms, c5r 23.06 / 19.00 /
+// 18.32 — ab_knobs.log)
 #ifndef RT_WF_REFILL
-#define RT_WF_REFILL 32
+#define RT_WF_REFILL 48
 #endif
 constexpr int kWfRefill = RT_WF_REFILL;
 
