@@ -398,7 +398,12 @@ def spawn_ranks(n: int) -> int:
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
     env = dict(os.environ)
     env.setdefault("OMP_NUM_THREADS", "1")  # the launcher's default; silences its warning
-    return subprocess.run(cmd, env=env).returncode
+    rc = subprocess.run(cmd, env=env).returncode
+    if rc != 0:
+        # a rank failed (its own message is above): the launcher stopped the
+        # others, or they failed at their collective deadline
+        print(f"bench.py: the {n}-rank run exited with status {rc}", file=sys.stderr, flush=True)
+    return rc
 
 
 def main():
@@ -428,6 +433,9 @@ def main():
     ap.add_argument("--force-dist", action="store_true",
                     help="create the process group and run the gather path even with WORLD_SIZE=1 (exercises "
                          "RCCL's init, all-reduce and gather on a 1-GPU box)")
+    ap.add_argument("--rank-timeout", type=float, default=180.0,
+                    help="N>1: seconds any rank waits at the rendezvous or in a collective for a peer before it "
+                         "fails (a dead or hung rank ends the run with a message instead of holding the node)")
     ap.add_argument("--frame-sha", action="store_true",
                     help="rank 0 adds the SHA-256 of the last assembled RGBA8 frame (bottom row first)")
     ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
@@ -454,7 +462,6 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    import numpy as np
     import torch
 
     if world > 1 and args.dist_backend == "nccl" and world > torch.cuda.device_count():
@@ -463,33 +470,49 @@ def main():
               f"--dist-backend gloo to share GPUs", file=sys.stderr, flush=True)
         sys.exit(2)
 
+    from rt_amd.dist import rank_guard
+
+    with rank_guard(rank):
+        run_rank(args, ctx_opts, world, rank, local)
+
+
+def dist_setup(backend: str, device: int, world: int, timeout_s: float):
+    """The process group (RCCL, or gloo), with a deadline on the rendezvous and
+    on every collective (rt_amd.dist.init_ranks), and the check that every
+    rank joined: returns (dist, ranks_seen, gpus_used)."""
+    import torch
+    import torch.distributed as dist
+
+    from rt_amd.dist import init_ranks
+
+    init_ranks(dist, backend, torch.device("cuda", device) if backend == "nccl" else None, timeout_s)
+    # the ranks that joined the collective: one all-reduce of a 1 per rank
+    one = torch.ones(1, dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
+    dist.all_reduce(one)
+    ranks_seen = int(one.item())
+    if ranks_seen != world or dist.get_world_size() != world:
+        print(f"bench.py: {ranks_seen} ranks joined the all-reduce, WORLD_SIZE={world}", file=sys.stderr,
+              flush=True)
+        sys.exit(2)
+    # distinct GPUs the ranks render on (gloo ranks may share one)
+    used = torch.zeros(max(1, torch.cuda.device_count()), dtype=torch.float64, device=one.device)
+    used[device] = 1.0
+    dist.all_reduce(used, op=dist.ReduceOp.MAX)
+    return dist, ranks_seen, int(used.sum().item())
+
+
+def run_rank(args, ctx_opts, world, rank, local):
+    import numpy as np
+    import torch
+
     # one GPU per rank (ranks beyond the visible GPUs share them: gloo only)
     device = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(device)
     dist = None
     use_dist = world > 1 or args.force_dist
-    if use_dist:
-        import torch.distributed as dist
-
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
-        else:
-            dist.init_process_group("gloo")
     ranks_seen, gpus_used = 1, 1
     if use_dist:
-        # the ranks that joined the collective: one all-reduce of a 1 per rank
-        one = torch.ones(1, dtype=torch.float64, device="cuda" if args.dist_backend == "nccl" else "cpu")
-        dist.all_reduce(one)
-        ranks_seen = int(one.item())
-        if ranks_seen != world or dist.get_world_size() != world:
-            print(f"bench.py: {ranks_seen} ranks joined the all-reduce, WORLD_SIZE={world}", file=sys.stderr,
-                  flush=True)
-            sys.exit(2)
-        # distinct GPUs the ranks render on (gloo ranks may share one)
-        used = torch.zeros(max(1, torch.cuda.device_count()), dtype=torch.float64, device=one.device)
-        used[device] = 1.0
-        dist.all_reduce(used, op=dist.ReduceOp.MAX)
-        gpus_used = int(used.sum().item())
+        dist, ranks_seen, gpus_used = dist_setup(args.dist_backend, device, world, args.rank_timeout)
     import rt_amd
 
     name, W, H, depth = CONFIGS[args.config]
@@ -580,12 +603,6 @@ def main():
                       "inline_records": bool(ci[4]), "build_host_ms": round(ci[5], 3),
                       "binning": {"candidate_pairs": int(ci[6]), "lists_over_256": int(ci[7]),
                                   "longest_list": int(ci[8]), "capacity": int(ci[9])}}
-    # the timed kernel: a later frame of the same camera on the bench's stream
-    # (the counted render above may be a camera's first frame)
-    ctx.render_async(frame, single.data_ptr(), 0, stream)
-    ctx.render_async(frame, single.data_ptr(), 0, stream)
-    torch.cuda.synchronize()
-    timed_kernel = ctx.stats().kernel
     brute = algorithmic_flops(types, st.primary_rays, st.bounce_rays, st.shadow_rays)
     flops = executed_flops(st)
     brute_tests = (st.primary_rays + st.bounce_rays + st.shadow_rays) * int(types.shape[0])
@@ -647,6 +664,10 @@ def main():
     if use_dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    # the kernel the timed launches ran: rt_stats.kernel of the timed loop's
+    # last launch (a camera's first frames compute, then store, its tile
+    # masks; the timed frames read them: rt_trace_tiny<0,1,37> at C2)
+    timed_kernel = ctx.stats().kernel
     frame_sha = None
     if args.frame_sha and rank == 0:
         import hashlib
@@ -667,6 +688,7 @@ def main():
         b.record()
     torch.cuda.synchronize()
     per_frame = sorted(a.elapsed_time(b) for a, b in frame_ev)
+    ranks_info = None
     if use_dist:
         cdev = "cuda" if args.dist_backend == "nccl" else "cpu"
         t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
@@ -675,6 +697,34 @@ def main():
         c = torch.tensor([st.primary_rays, st.bounce_rays, st.shadow_rays], dtype=torch.float64, device=cdev)
         dist.all_reduce(c)
         tot_primary, tot_bounce, tot_shadow = (float(x) for x in c.tolist())
+        # The N>1 model's terms: each rank's slab render (median
+        # of its per-frame event pairs above) and the gather alone — batches
+        # of already-rendered slabs posted back to back after a barrier, with
+        # no render beside them, per batch of gather_batch frames.
+        nb = 4
+        dist.barrier()
+        torch.cuda.synchronize()
+        tg = time.perf_counter()
+        for j in range(nb):
+            for i in range(args.gather_batch):
+                k = counter[0]
+                counter[0] += 1
+                gather.target(k)
+                gather.submit(k)
+        gather.finish()
+        torch.cuda.synchronize()
+        gather_ms = (time.perf_counter() - tg) * 1e3 / nb
+        rmed = per_frame[len(per_frame) // 2]
+        v = torch.tensor([rmed, -rmed, gather_ms], dtype=torch.float64, device=cdev)
+        dist.all_reduce(v, op=dist.ReduceOp.MAX)
+        mx, mn, gmax = (float(x) for x in v.tolist())
+        ranks_info = {"render_ms_slowest": round(mx, 4), "render_ms_fastest": round(-mn, 4),
+                      "gather_ms_per_batch": round(gmax, 4), "gather_batch": args.gather_batch,
+                      "bytes_per_link_per_frame": int(rows * W * args.gather_channels),
+                      "note": "render: median per-frame launch time of a rank's slab (event pairs), slowest and "
+                              "fastest rank; gather: batches of gather_batch already-rendered slabs gathered to "
+                              "rank 0 back to back with no render beside them (max over ranks, per batch); bytes: "
+                              "one non-root rank's slab per frame over its link to rank 0"}
     else:
         tot_primary, tot_bounce, tot_shadow = float(st.primary_rays), float(st.bounce_rays), float(st.shadow_rays)
 
@@ -760,14 +810,15 @@ def main():
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
                          "frac_vs_nofma_issue_peak": round(achieved / PEAK_NOFMA_TOPS, 4),
                          "flops_per_launch": int(flops),
-                         # the kernel the library reports it ran (rt_stats.kernel, ABI 7) for
-                         # the counted render; the timed launches run its COUNT=false twin
-                         # (the launch-camera kernel's later frames on a stream: <0,1,37>)
+                         # the kernel the library reports for the timed loop's last launch
+                         # (rt_stats.kernel, ABI 7): the name rocprof's dominant kernel carries
                          "kernel": timed_kernel,
                          "work": "exact ray-primitive tests executed (after culling) x SURVEY 8(d) ops + set-up + shading",
                          "tests_executed": int(run_tests), "tests_brute_force": int(brute_tests),
                          "brute_force_equiv_tflops": round(brute / (kernel_ms * 1e-3) / 1e12, 3)},
         }
+        if ranks_info:
+            out["ranks"] = ranks_info
         if frame_sha:
             out["frame_rgba8_sha256"] = frame_sha
         if world == 1 and not args.no_host_boundary:

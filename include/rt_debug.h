@@ -52,6 +52,18 @@ int rt_debug_scan(int device, const unsigned* in, unsigned n, unsigned* out, uns
  * inner-node path), out[4] host build ms. */
 int rt_debug_bvh_info(rt_ctx*, double* out, int n);
 
+/* The last wavefront frame's queue counts (round 6; synchronous): per level
+ * L = 0 .. 8, out[3 L] its rays (L >= 1), out[3 L + 1] its parents (nodes
+ * that spawned children), out[3 L + 2] its walks finished by the straggler
+ * launch.  RT_E_STATE before any wavefront frame. */
+int rt_debug_wf_counts(rt_ctx*, unsigned* out, int n);
+
+/* The host BVH build alone, no device (round 6): n triangles of 12 floats
+ * (p0, e1, e2, normal); out3 = {depth, inner nodes, leaves}.  The depth is
+ * at most 24 (the walk's stack) for every input; RT_E_UNSUPPORTED above
+ * 4 x 2^24 triangles (bounce rays then test every triangle). */
+int rt_debug_bvh_build(const float* tri12, long long n, int* out3);
+
 /* Bounce-ray closest hits of n arbitrary rays (rays: O.xyz D.xyz per ray),
  * each through the BVH and through every triangle (planes and quadrics
  * too, both ways; synchronous): out_idx / out_t (2 per ray) = [BVH, brute

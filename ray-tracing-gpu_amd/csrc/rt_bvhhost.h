@@ -18,7 +18,15 @@
 namespace rt {
 
 constexpr int kBvhLeafMax = 4;
-constexpr int kBvhMedianDepth = 20;  // past this depth: median splits (bounded depth)
+constexpr int kBvhMedianDepth = 20;  // past this depth: median splits
+
+// Levels of median splits below a node of m triangles: ceil(log2(ceil(m / 4))).
+inline int bvh_median_levels(size_t m)
+{
+    int k = 0;
+    for (size_t cap = kBvhLeafMax; cap < m; cap *= 2) ++k;
+    return k;
+}
 
 struct BvhPrim {
     float lo[3], hi[3];
@@ -194,11 +202,22 @@ class BvhBuilder {
         const auto it = std::partition(ord.begin() + b, ord.begin() + e, [&](int k) { return bin_of(k) < cut; });
         const size_t mid = (size_t)(it - ord.begin());
         if (mid == b || mid == e) return median();
+        // Depth bound: every node keeps depth + bvh_median_levels(count) <=
+        // kBvhStack (the root does for up to 4 x 2^24 triangles); an SAH cut
+        // whose larger side would break it is replaced by the median cut,
+        // which keeps it — so the tree always fits the walk's stack.
+        if (depth + 1 + bvh_median_levels(std::max(mid - b, e - mid)) > kBvhStack) return median();
         return mid;
     }
 };
 
-// The BVH over tri[] (12 floats per triangle, n > kBvhLeafMax).
+// Largest triangle count the leaf encoding ~((first << 4) | (count - 1))
+// keeps negative (first < 2^27) and the median-split bound keeps within
+// kBvhStack levels (4 x 2^24): larger scenes trace bounce rays without a BVH.
+constexpr size_t kBvhMaxTriangles = (size_t)kBvhLeafMax << kBvhStack;
+static_assert(kBvhMaxTriangles <= ((size_t)1 << 27), "leaf encoding");
+
+// The BVH over tri[] (12 floats per triangle, kBvhLeafMax < n <= kBvhMaxTriangles).
 inline void bvh_build(const std::vector<float>& tri, size_t n, BvhBuilt& out)
 {
     std::vector<BvhPrim> P(n);

@@ -1607,7 +1607,7 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
     HIP_TRY(c, hipMalloc((void**)&c->d_tricam, (tri.size() / 12) * 16 * sizeof(float)));
     // the bounce-ray BVH: only a scene with a reflective or refractive
     // surface has bounce rays (Scene.cpp:1779-1823 gate on Kr, Kt > 0)
-    if (kmax > 0.0f && cnt_tri >= RT_BVH_MIN_TRIANGLES) {
+    if (kmax > 0.0f && cnt_tri >= RT_BVH_MIN_TRIANGLES && (size_t)cnt_tri <= kBvhMaxTriangles) {
         const auto tb = std::chrono::steady_clock::now();
         BvhBuilt B;
         bvh_build(tri, (size_t)cnt_tri, B);
@@ -2165,9 +2165,15 @@ static int prepare_state(rt_ctx* c, const rt_frame* f, hipStream_t st, bool sync
 // overlapping chunk i + 1's kernel (the same pixels: every pixel is independent, and the chunks keep
 // the unchunked launch's 8-row wave rows).
 // ---- wavefront bounce levels (rt_wavefront.h)
-// Children one node can spawn: a reflected ray needs some Kr > 0, a
-// refracted one some Kt > 0 (the gates compare K * energy > min_energy >= 0).
-static int wf_branch(const rt_ctx* c) { return (c->kr_max > 0.0f ? 1 : 0) + (c->kt_max > 0.0f ? 1 : 0); }
+// Children one node can spawn (the gates compare K * energy > min_energy,
+// Scene.cpp:1780,1791): with min_energy >= 0 a reflected ray needs some
+// Kr > 0 and a refracted one some Kt > 0; a negative (or NaN) threshold is
+// passed by K = 0 too, so every node may spawn both.
+static int wf_branch(const rt_ctx* c, const rt_frame* f)
+{
+    if (!(f->min_energy >= 0.0f)) return 2;
+    return (c->kr_max > 0.0f ? 1 : 0) + (c->kt_max > 0.0f ? 1 : 0);
+}
 
 #ifndef RT_WF_TRACE_WAVES
 // trace launch: workgroups (one wave each) per CU.  Fewer than the 32 that
@@ -2262,8 +2268,8 @@ static size_t frame_tiles(const rt_frame* f, int rows) { return (size_t)((f->wid
 // output chunk, queues within RT_WF_MAX_GB.
 static bool wf_fits(const rt_ctx* c, const rt_frame* f, int depth, int rows)
 {
-    if (!c->opt_wavefront || depth < 1 || depth > kWfMaxLevels || wf_branch(c) == 0) return false;
-    const WfLayout w = wf_layout(frame_tiles(f, rows), (size_t)rows * f->width, depth, wf_branch(c));
+    if (!c->opt_wavefront || depth < 1 || depth > kWfMaxLevels || wf_branch(c, f) == 0) return false;
+    const WfLayout w = wf_layout(frame_tiles(f, rows), (size_t)rows * f->width, depth, wf_branch(c, f));
     return (double)w.bytes <= RT_WF_MAX_GB * 1073741824.0;
 }
 
@@ -2273,7 +2279,7 @@ static int wf_ensure(rt_ctx* c, const rt_frame* f, int rows, int levels, bool ca
 {
     rt_ctx::WfBuf& W = c->wf;
     const size_t px = (size_t)rows * f->width;
-    const WfLayout w = wf_layout(frame_tiles(f, rows), px, levels, wf_branch(c));
+    const WfLayout w = wf_layout(frame_tiles(f, rows), px, levels, wf_branch(c, f));
     *ok = false;
     if (w.bytes > W.bytes) {
         if (capturing) return RT_OK;  // (the frame renders by the BVH megakernel)
@@ -3004,6 +3010,51 @@ RT_EXPORT int rt_debug_bvh_info(rt_ctx* c, double* out, int n)
     const double v[5] = {c->d_bvh_node ? 1.0 : 0.0, (double)c->bvh_inner, (double)c->bvh_leaves, (double)c->bvh_depth,
                          c->bvh_build_ms};
     for (int i = 0; i < n; ++i) out[i] = i < 5 ? v[i] : 0.0;
+    return RT_OK;
+}
+
+// Diagnostic (include/rt_debug.h): the last wavefront frame's queue counts,
+// per level L = 0 .. kWfMaxLevels: out[3 L] rays of level L (L >= 1), out[3 L
+// + 1] parents of level L, out[3 L + 2] straggling walks of level L.
+RT_EXPORT int rt_debug_wf_counts(rt_ctx* c, unsigned* out, int n)
+{
+    if (!c || !out || n <= 0) return RT_E_ARG;
+    if (c->cpu) return not_cpu(c);
+    if (!c->wf.mem) {
+        c->err = "no wavefront frame rendered";
+        return RT_E_STATE;
+    }
+    if (int rc = sync_all(c)) return rc;
+    std::vector<unsigned> w(kWfCountBytes / 4);
+    HIP_TRY(c, hipMemcpy(w.data(), c->wf.dev.count, kWfCountBytes, hipMemcpyDeviceToHost));
+    for (int i = 0; i < n; ++i) {
+        const int L = i / 3, k = i % 3;
+        unsigned v = 0;
+        if (L <= kWfMaxLevels) {
+            if (k == 2) {
+                v = w[wf_strag(L)];
+            } else {
+                for (int s = 0; s < kWfSeg; ++s) v += w[k == 0 ? wf_rays(L, s) : wf_pars(L, s)];
+            }
+        }
+        out[i] = v;
+    }
+    return RT_OK;
+}
+
+// Diagnostic (include/rt_debug.h): the host BVH build alone (no device) over
+// n triangles of 12 floats (p0, e1, e2, normal: the upload's tri[] records);
+// out3 = {depth, inner nodes, leaves}.  RT_E_UNSUPPORTED past kBvhMaxTriangles.
+RT_EXPORT int rt_debug_bvh_build(const float* tri12, long long n, int* out3)
+{
+    if (!tri12 || !out3 || n <= kBvhLeafMax) return RT_E_ARG;
+    if ((size_t)n > kBvhMaxTriangles) return RT_E_UNSUPPORTED;
+    std::vector<float> tri(tri12, tri12 + 12 * (size_t)n);
+    BvhBuilt B;
+    bvh_build(tri, (size_t)n, B);
+    out3[0] = B.depth;
+    out3[1] = B.inner;
+    out3[2] = B.leaves;
     return RT_OK;
 }
 

@@ -27,7 +27,44 @@ backend the benchmark's numbers are quoted on.
 """
 from __future__ import annotations
 
+import contextlib
+import os
+import sys
 from typing import List, Optional, Tuple
+
+# Collective deadline of the benchmark's process group: a rank that dies or
+# hangs makes every other rank's pending rendezvous or collective fail after
+# this long (gloo raises; RCCL's watchdog aborts the communicator), instead
+# of holding the node until an outer kill.
+RANK_TIMEOUT_S = 180.0
+
+
+def init_ranks(dist, backend: str, device=None, timeout_s: float = RANK_TIMEOUT_S):
+    """init_process_group with a deadline (env:// rendezvous from the
+    launcher).  backend "nccl" (RCCL) binds the rank's device."""
+    import datetime
+
+    kw = {"timeout": datetime.timedelta(seconds=timeout_s)}
+    if backend == "nccl":
+        kw["device_id"] = device
+    dist.init_process_group(backend, **kw)
+
+
+@contextlib.contextmanager
+def rank_guard(rank: int, what: str = "bench.py"):
+    """Any exception on a rank ends that process at once with status 1 and a
+    one-line message naming the rank (no interpreter teardown, which could
+    block in a collective's destructor): the launcher then stops the other
+    ranks and exits non-zero, and a rank still waiting on this one fails at
+    its collective deadline."""
+    try:
+        yield
+    except SystemExit:
+        raise
+    except BaseException as e:  # noqa: BLE001 — report any failure, then end the rank
+        print(f"{what}: rank {rank} failed: {type(e).__name__}: {e}", file=sys.stderr, flush=True)
+        sys.stdout.flush()
+        os._exit(1)
 
 
 def slab_rows(height: int, world: int, rank: int) -> Tuple[int, int, int]:

@@ -53,3 +53,68 @@ def test_oracle_matches_reference_reflective_heightfield(oracle, heightfield_r05
         # the mirrors change the picture: the same window of the plain mesh differs
         with np.load(os.path.join(GOLDEN, "c3_column.npz")) as p:
             assert not np.array_equal(p["hf_1080p_d1_win_400_408_944_976"], z["hfr_1920x1080_d1_win_400_408_944_976"])
+
+
+# ---- the host build's depth bound: every tree fits the walk's
+# 24-entry stack, whatever the triangle distribution
+def _build(tri):
+    import ctypes
+
+    import rt_amd
+
+    L = rt_amd.lib()
+    L.rt_debug_bvh_build.argtypes = [ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p]
+    tri = np.ascontiguousarray(tri, np.float32)
+    out = np.zeros(3, np.int32)
+    rc = L.rt_debug_bvh_build(tri.ctypes.data, tri.shape[0], out.ctypes.data)
+    return rc, out
+
+
+def _tris(p0, size):
+    n = p0.shape[0]
+    t = np.zeros((n, 12), np.float32)
+    t[:, 0:3] = p0
+    t[:, 3] = size
+    t[:, 7] = size
+    t[:, 11] = 1.0
+    return t
+
+
+@pytest.mark.parametrize("kind", ["grid", "geometric", "clustered"])
+def test_bvh_depth_fits_the_stack_on_big_meshes(kind):
+    n = 1_200_000
+    rng = np.random.default_rng(5)
+    if kind == "grid":
+        k = np.arange(n)
+        p0 = np.stack([(k % 1000).astype(np.float32), np.zeros(n, np.float32), (k // 1000).astype(np.float32)], 1)
+        size = np.ones(n, np.float32)
+    elif kind == "geometric":
+        # centroids spread over ~34 decades: SAH's 16 bins over the widest
+        # extent split off a few triangles per level (the round-5 build
+        # reached depth 20 with ~1M triangles left, then 38 levels)
+        x = np.power(np.float64(1.00006), np.arange(n)).astype(np.float32)
+        p0 = np.stack([x, np.zeros(n, np.float32), np.zeros(n, np.float32)], 1)
+        size = np.maximum(x * np.float32(1e-3), np.float32(1e-3))
+    else:
+        c = rng.integers(0, 8, n)
+        p0 = (rng.normal(size=(n, 3)) * np.power(10.0, c)[:, None]).astype(np.float32)
+        size = np.power(10.0, c - 3).astype(np.float32)
+    rc, (depth, inner, leaves) = _build(_tris(p0, size))
+    assert rc == 0
+    assert 1 <= depth <= 24, depth
+    assert leaves == inner + 1
+    assert leaves >= n // 4
+
+
+def test_bvh_build_refuses_what_the_leaf_encoding_cannot_hold():
+    import ctypes
+
+    import rt_amd
+
+    L = rt_amd.lib()
+    L.rt_debug_bvh_build.argtypes = [ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p]
+    out = np.zeros(3, np.int32)
+    dummy = np.zeros(12, np.float32)
+    # (the size check comes before any read of the triangles)
+    assert L.rt_debug_bvh_build(dummy.ctypes.data, (4 << 24) + 1, out.ctypes.data) == -6
+    assert L.rt_debug_bvh_build(dummy.ctypes.data, 4, out.ctypes.data) == -1

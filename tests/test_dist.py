@@ -182,3 +182,29 @@ def test_bench_refuses_world_size_other_than_gpus():
 def test_bench_refuses_zero_gpus():
     r = _bench_rc(["--gpus", "0"], {})
     assert r.returncode == 2
+
+
+# ---- the N>1 failure bound: bench.py's own dist_setup
+# under rank_guard, two gloo ranks, rank 1 misbehaving
+@pytest.mark.parametrize("mode", ["before_init", "after_init", "raise"])
+def test_rank_failure_ends_the_run(mode):
+    import subprocess
+    import sys
+    import time
+
+    from conftest import REPO
+
+    deadline = 10.0
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(REPO, "tests", "dist_fail_worker.py"), "--mode", mode, "--timeout", str(deadline)]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    t0 = time.perf_counter()
+    r = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=120, env=env)
+    took = time.perf_counter() - t0
+    assert r.returncode != 0, (r.stdout, r.stderr[-2000:])
+    assert "ok" not in r.stdout.split()
+    # rank 0 itself failed with a message naming it (or was stopped by the
+    # launcher after rank 1's failure), well inside the deadline + start-up
+    assert "rank 0 failed" in r.stderr or "rank 1 failed" in r.stderr, r.stderr[-2000:]
+    assert took < deadline + 60, took

@@ -346,3 +346,70 @@ def test_bvh_walk_equals_brute_force_on_random_meshes(tmp_path, seed):
     assert same.all(), np.nonzero(~same)[0][:5]
     assert (idx[:, 1] >= 0).sum() > m // 4
     ctx.close()
+
+
+# ---- the wavefront levels' 2-child segments: refraction, and a
+# negative min_energy (every node spawns both children, Kt = 0 included)
+def _oracle_windows(oracle, path, w, h, depth, min_energy, wins, threads=8):
+    out = []
+    for (r0, r1, c0, c1) in wins:
+        rc, p = oracle.load(path, w, h, depth)
+        assert rc == 0
+        oracle.L.oracle_set_params(p, depth, min_energy, 1.0)
+        img = np.zeros((r1 - r0, c1 - c0, 3), np.float32)
+        oracle.L.oracle_render_window(p, r0, r1, c0, c1, img.ctypes.data, threads)
+        oracle.L.oracle_free(p)
+        out.append(img)
+    return out
+
+
+_WINS = [(0, 8, 0, 64), (300, 308, 900, 964), (500, 508, 1200, 1264), (700, 716, 400, 432), (1072, 1080, 1856, 1920),
+         (540, 548, 0, 1920)]
+
+
+def _three_ways(path, w, h, depth, min_energy, oracle):
+    s = rt_amd.Scene(path, w, h, depth, min_energy=min_energy)
+    got = {}
+    for wf in (1, 0):
+        c = rt_amd.Context(0, wavefront=wf)
+        c.upload(s)
+        f = s.frame.copy()
+        f.flags = rt_amd.FLAG_STATS
+        got[wf] = c.render_float(f)
+        st = c.stats()
+        assert st.kernel.startswith("wavefront") == bool(wf), st.kernel
+        assert st.bounce_rays > 0
+        c.close()
+    assert bits_equal(got[1], got[0])
+    for (r0, r1, c0, c1), want in zip(_WINS, _oracle_windows(oracle, path, w, h, depth, min_energy, _WINS)):
+        assert bits_equal(got[1][r0:r1, c0:c1], want), (r0, r1, c0, c1)
+
+
+@pytest.mark.parametrize("depth", [3, 5])
+def test_refractive_mesh_wavefront_megakernel_oracle(tmp_path, oracle, depth):
+    """Every triangle reflects, every other one also refracts (Kt 0.4, ior
+    1.5; the opaque half keeps the light buffer, which the BVH kernels need):
+    2-child nodes, inside/out IOR flips, the refracted branch's sort key — at
+    1920 x 1080."""
+    from rt_amd import synth
+
+    lines, k = [], 0
+    for line in synth.heightfield_dat(cols=40, rows=20, reflect=0.3).split("\n"):
+        lines.append(line)
+        if line.startswith("        reflect:"):
+            if k % 2 == 0:
+                lines.append("        refract: 0.4 1.5")
+            k += 1
+    path = tmp_path / "hf_refr.dat"
+    path.write_text("\n".join(lines))
+    _three_ways(str(path), 1920, 1080, depth, 0.01, oracle)
+
+
+def test_negative_min_energy_spawns_both_children(tmp_path, oracle):
+    """A reflect-only mesh with min_energy < 0: K * energy > min_energy holds
+    for Kt = 0 too, so every hit spawns two children (the queues must be
+    sized for 2 per node, not 1)."""
+    from rt_amd import synth
+
+    path = synth.write_heightfield(str(tmp_path / "hf_neg.dat"), cols=12, rows=6, reflect=0.5)
+    _three_ways(path, 1920, 1080, 3, -1.0, oracle)

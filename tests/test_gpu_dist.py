@@ -61,6 +61,11 @@ def test_scene2_ranks_match_reference_digest(one_rank, digests, n, partition, ga
     out = _bench(n, "c2", partition, gather_batch, gather_channels)
     assert out["n_gpus"] == out["ranks_seen"] == n
     assert out["frame_rgba8_sha256"] == one_rank["c2"]["frame_rgba8_sha256"]
+    # the N>1 model's terms
+    rk = out["ranks"]
+    assert 0 < rk["render_ms_fastest"] <= rk["render_ms_slowest"]
+    assert rk["gather_ms_per_batch"] > 0 and rk["gather_batch"] == gather_batch
+    assert rk["bytes_per_link_per_frame"] > 0
     # scene2 has no reflective/refractive surface: depth 3 renders the depth-0 image
     assert out["frame_rgba8_sha256"] == digests["scene2_1920x1080_d0_rgba8_sha256"]
     assert out["rays_per_frame"]["primary"] == 1920 * 1080
@@ -196,4 +201,5 @@ def test_bench_nccl_one_rank_runs_the_rccl_path(one_rank):
     assert len(lines) == 1, r.stdout[-2000:]
     out = json.loads(lines[0])
     assert "RCCL gather" in out["config"]["parallelism"]
+    assert out["ranks"]["bytes_per_link_per_frame"] == 1920 * 1080 * 3
     assert out["frame_rgba8_sha256"] == one_rank["c2"]["frame_rgba8_sha256"]

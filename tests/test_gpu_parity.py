@@ -158,6 +158,26 @@ def test_scene2_1080p_digest_and_counts(ctx, digests):
     assert st.bounce_rays == 0
 
 
+def test_timed_kernel_label_after_three_renders():
+    """bench.py's roofline.kernel is rt_stats.kernel of a timed launch: for
+    the C2 camera on one stream the first frame computes the tile masks
+    (<0,1,101>), the second stores them (<0,1,229>), every later frame reads
+    them (<0,1,37>, the kernel rocprof times in the bench's loop)."""
+    torch = pytest.importorskip("torch")
+    s = rt_amd.Scene(scene(2), 1920, 1080, 3)
+    c = rt_amd.Context(0)
+    c.upload(s)
+    out = torch.empty((1080, 1920, 4), dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    labels = []
+    for _ in range(4):
+        c.render_async(s.frame, out.data_ptr(), 0, stream)
+        labels.append(c.stats().kernel)
+    torch.cuda.synchronize()
+    assert labels == ["rt_trace_tiny<0,1,101>", "rt_trace_tiny<0,1,229>",
+                      "rt_trace_tiny<0,1,37>", "rt_trace_tiny<0,1,37>"], labels
+
+
 @pytest.mark.parametrize("i,depth", [(2, 0), (7, 3), (1, 0)])
 def test_counted_kernel_renders_the_same(ctx, i, depth):
     """The RT_FLAG_STATS launch runs the COUNT kernel variant: same image, and
