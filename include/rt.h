@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 7
+#define RT_ABI_VERSION 8
 
 enum {
     RT_OK = 0,
@@ -259,6 +259,20 @@ enum {
                                    per level then a fold per level (up to 8 levels,
                                    not inside a hipGraph capture or a sequence): 1
                                    (default) / 0 (one kernel, a per-lane DFS stack) */
+    RT_OPT_WF_SORT = 15,        /* launch (ABI 8): such wavefront frames order each level's
+                                   live rays by counting sorts on the device: bit 0 by
+                                   their parent surface's bin (BVH leaf order) and branch
+                                   before the BVH walk, bit 1 by their hit surface's bin
+                                   before the shading; 0 queue order; default 1; never
+                                   changes an image */
+    RT_OPT_XCD_DEAL = 16,       /* launch (ABI 8): how the big-list kernels (more than
+                                   1,024 triangles) deal 8 x 8 tiles to the 8 XCDs: 1
+                                   (default) runs of 8 along a tile row, 2 column stripes
+                                   (each XCD walks its own 1/8 of the columns row by row),
+                                   3 4 x 2 super-tiles round-robin, 0 hardware order;
+                                   never changes an image */
+    RT_OPT_XCD_STRIPE = 17,     /* launch (ABI 8): RT_OPT_XCD_DEAL 2's stripe width in tiles,
+                                   stripe s on XCD s % 8; 0 (default) one stripe per XCD */
     RT_OPT_LAUNCH_CAMERA = 12   /* launch (ABI 6): depth-0 frames of scenes of 1-20
                                    triangles with light-buffer shadows take their camera
                                    records with the kernel launch — per-triangle camera

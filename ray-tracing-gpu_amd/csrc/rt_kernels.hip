@@ -26,7 +26,6 @@
 //    bottom-up in the reference's order: ((local + C_refl*Kr) + C_refr*Kt);
 //  * no FMA contraction, IEEE f32 division and sqrt.
 #include <hip/hip_runtime.h>
-#include <hipcub/device/device_radix_sort.hpp>
 
 #include <algorithm>
 #include <chrono>
@@ -70,7 +69,7 @@ struct Refr {
 // its colour (deferred: rt_wf_fold writes the pixel).
 template <int MAXD, int LB, int WAVE>
 __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, Counters& cnt, bool live, int tile,
-                          const TinyCam* T, unsigned tmask, unsigned pix, bool& deferred)
+                          const TinyCam* T, unsigned tmask, unsigned pix, bool& deferred, unsigned chunk)
 {
     const Color bg{F.bg[0], F.bg[1], F.bg[2]};
     if constexpr (MAXD == 0) {
@@ -98,8 +97,7 @@ __device__ Color radiance(const SceneDev& S, const FrameDev& F, Vec3 O, Vec3 D, 
         const Vec3 P = O + t * D;
         const Color c = shade_local<LB, WAVE>(S, m, P, N, D, cnt, hit & live);
         if constexpr ((WAVE & 512) != 0)
-            deferred = wf_children(F, 0, hit & live, m, P, N, D, 1.0f, 1.0f, c, pix, blockIdx.x + blockIdx.y * gridDim.x,
-                                   sidx);
+            deferred = wf_children(F, 0, hit & live, m, P, N, D, 1.0f, 1.0f, c, pix, chunk, sidx);
         return hit ? c : bg;
     } else if constexpr ((WAVE & 1024) != 0) {
         // Reflect-only scenes (no Kt can pass the gate: the host's kt_max <= 0
@@ -352,7 +350,8 @@ __device__ __forceinline__ void trace_tile(const SceneDev& S, const FrameDev& F,
         if constexpr ((WAVE & 64) != 0) tmask = tiny_tile_mask(*T, tl, D);
         const size_t o = (size_t)ly * F.width + px;
         bool deferred = false;
-        c = radiance<MAXD, LB, WAVE>(S, F, O, D, cnt, valid, tile, T, tmask, (unsigned)o, deferred);
+        c = radiance<MAXD, LB, WAVE>(S, F, O, D, cnt, valid, tile, T, tmask, (unsigned)o, deferred,
+                                     (unsigned)(by * F.tiles_x + bx));
         if (valid & !deferred) {
             if (rgbf) {
                 rgbf[3 * o] = c.r;
@@ -425,18 +424,45 @@ __device__ __forceinline__ void trace_tile(const SceneDev& S, const FrameDev& F,
 // -1.4%, C2 -0.8%; declaring 64 threads: C5 -1.1%).
 // XCD-aware block order: the dispatcher deals workgroups round-robin over
 // the 8 XCDs (each with its own L2), so workgroup w runs on XCD w % 8 as
-// that XCD's (w / 8)-th; chunks of K consecutive blocks go to one XCD, when
-// the grid divides evenly, so neighbouring tiles — which read the same
-// cells, tile lists and records — share an L2 (whole-region runs per XCD
-// were 1.8x slower on C3: the mesh rows then pile onto a few XCDs).  Per
-// kernel (A/B): the big-list kernel K = 8 (C5 -1.4% against 4), the
-// small-list kernels none (C2 -2.5% against 4; the remap's code alone costs it).
+// that XCD's (w / 8)-th.  Big-list kernels (RT_OPT_XCD_DEAL, F.xcd_mode):
+//  1: chunks of K consecutive blocks of a tile row go to one XCD, when the
+//     grid divides evenly (C5 -1.4% against K = 4; C3's 240 x 135 tiles do
+//     not divide: hardware order) — horizontal neighbours share an L2;
+//  2: column stripes of xcd_w tiles, stripe s on XCD s % 8 (one stripe per
+//     XCD by default, RT_OPT_XCD_STRIPE): XCD x walks its stripes' tiles row
+//     by row, so a tile's horizontal AND vertical neighbours — which read
+//     the same light-buffer cells, tile lists and records — share its L2,
+//     while at any moment all XCDs work on the same frame rows (whole-region
+//     runs per XCD were 1.8x slower on C3: the mesh rows piled onto a few
+//     XCDs);
+//  3: 4 x 2 super-tiles dealt round-robin over the XCDs;
+//  0: hardware order.
+// Modes 2 and 3 launch a padded grid (xcd_grid); its blocks past the frame's
+// tiles return at once.  The small-list kernels: hardware order (C2 -2.5%
+// against K = 4; the remap's code alone costs it).
 template <int WAVE>
-__device__ __forceinline__ void tile_of_block(int& bx, int& by)
+__device__ __forceinline__ bool tile_of_block(const FrameDev& F, int& bx, int& by)
 {
     bx = (int)blockIdx.x;
     by = (int)blockIdx.y;
     constexpr unsigned K = (WAVE & 2) ? RT_XCD_CHUNK_BIG : RT_XCD_CHUNK_SMALL;
+    if constexpr ((WAVE & 2) != 0) {
+        const unsigned w = blockIdx.y * gridDim.x + blockIdx.x;
+        const unsigned x = w % kXcds, i = w / kXcds;
+        if (F.xcd_mode == 2) {
+            const unsigned sw = (unsigned)F.xcd_w, m = (unsigned)F.xcd_m, j = i % m;
+            bx = (int)((j / sw) * (kXcds * sw) + x * sw + j % sw);
+            by = (int)(i / m);
+            return bx < F.tiles_x && by < F.tiles_y;
+        }
+        if (F.xcd_mode == 3) {
+            const unsigned st = (i / 8u) * kXcds + x, p = i % 8u, gx = (unsigned)F.xcd_w;
+            bx = (int)((st % gx) * 4u + p % 4u);
+            by = (int)((st / gx) * 2u + p / 4u);
+            return bx < F.tiles_x && by < F.tiles_y;
+        }
+        if (F.xcd_mode == 0) return true;
+    }
     if constexpr (K > 0) {
         const unsigned nb = gridDim.x * gridDim.y, w = blockIdx.y * gridDim.x + blockIdx.x;
         const unsigned x = w % kXcds, i = w / kXcds;
@@ -446,6 +472,7 @@ __device__ __forceinline__ void tile_of_block(int& bx, int& by)
             by = (int)(lw / gridDim.x);
         }
     }
+    return true;
 }
 
 template <int MAXD, int LB, int WAVE, bool COUNT>
@@ -454,7 +481,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(waves_per_eu
     StatsDev* __restrict__ stats)
 {
     int bx, by;
-    tile_of_block<WAVE>(bx, by);
+    if (!tile_of_block<WAVE>(F, bx, by)) return;
     trace_tile<MAXD, LB, WAVE, COUNT>(S, F, rgba, rgbf, stats, nullptr, bx, by);
 }
 
@@ -466,7 +493,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(waves_per_eu
     StatsDev* __restrict__ stats)
 {
     int bx, by;
-    tile_of_block<WAVE>(bx, by);
+    if (!tile_of_block<WAVE>(F, bx, by)) return;
     trace_tile<MAXD, LB, WAVE, COUNT>(S, F, rgba, rgbf, stats, &T, bx, by);
 }
 
@@ -742,6 +769,10 @@ struct rt_ctx {
     // bounce-ray BVH (rt_bvh.h, built at upload for scenes that can bounce)
     float4* d_bvh_node = nullptr;
     float4* d_bvh_tri = nullptr;
+    // per surface: its coherence-sort bin (WfDev::skey; triangles in the
+    // BVH's leaf order, two per bin), and the bins per branch
+    unsigned* d_skey = nullptr;
+    unsigned nbin_half = 0;
     int bvh_inner = 0, bvh_leaves = 0, bvh_depth = 0;
     double bvh_build_ms = 0.0;
     bool opt_bvh = true;        // RT_OPT_BVH
@@ -755,17 +786,21 @@ struct rt_ctx {
         size_t cap[kWfMaxLevels + 1] = {};   // ray slots per level (level 0: pixels)
         size_t pcap[kWfMaxLevels + 1] = {};  // parent-list slots per level
         WfDev dev{};
-        // coherence sort (RT_WF_SORT): key buffers of `kcap` rays, the
-        // radix sort's scratch
-        unsigned long long *kin = nullptr, *kout = nullptr;
-        size_t kcap = 0;
-        void* stemp = nullptr;
-        size_t stemp_bytes = 0;
+        // coherence sort (WfDev::kin): bins of `kcap` ray slots, sorted
+        // slots, the bin counts / positions (hcap words) and their scan's
+        // scratch
+        unsigned *kin = nullptr, *kout = nullptr, *kout2 = nullptr, *hist = nullptr;
+        unsigned long long* bsum = nullptr;
+        size_t kcap = 0, hcap = 0;
+        int sort = 0;  // this frame's RT_OPT_WF_SORT: bit 0 parent sort, bit 1 hit sort
         hipEvent_t ev = nullptr;  // after the last wavefront frame
         hipStream_t last = nullptr;
         bool pending = false;
     } wf;
     int opt_wavefront = 1;      // RT_OPT_WAVEFRONT
+    int opt_wf_sort = 1;        // RT_OPT_WF_SORT
+    int opt_xcd_deal = 1;       // RT_OPT_XCD_DEAL
+    int opt_xcd_stripe = 0;     // RT_OPT_XCD_STRIPE
     float kr_max = 0.0f, kt_max = 0.0f;  // max Kr, max Kt over surfaces
     bool uploaded = false;
     rt_stats last{};
@@ -945,6 +980,18 @@ RT_EXPORT int rt_set_option(rt_ctx* c, int32_t opt, double v)
     case RT_OPT_LAUNCH_CAMERA: c->opt_launch_camera = v != 0; return RT_OK;
     case RT_OPT_BVH: c->opt_bvh = v != 0; return RT_OK;
     case RT_OPT_WAVEFRONT: c->opt_wavefront = v != 0; return RT_OK;
+    case RT_OPT_WF_SORT:
+        if (v != 0 && v != 1 && v != 2 && v != 3) return RT_E_ARG;
+        c->opt_wf_sort = (int)v;
+        return RT_OK;
+    case RT_OPT_XCD_DEAL:
+        if (v != 0 && v != 1 && v != 2 && v != 3) return RT_E_ARG;
+        c->opt_xcd_deal = (int)v;
+        return RT_OK;
+    case RT_OPT_XCD_STRIPE:
+        if (v < 0 || v > 4096 || v != std::floor(v)) return RT_E_ARG;
+        c->opt_xcd_stripe = (int)v;
+        return RT_OK;
     case RT_OPT_CB_CAPACITY:
         if (v < 0 || v > 4e9 || v != std::floor(v)) return RT_E_ARG;
         if (v != c->opt_cb_capacity) c->cb.valid = false;
@@ -969,6 +1016,9 @@ RT_EXPORT int rt_get_option(rt_ctx* c, int32_t opt, double* v)
     case RT_OPT_LAUNCH_CAMERA: *v = c->opt_launch_camera ? 1 : 0; return RT_OK;
     case RT_OPT_BVH: *v = c->opt_bvh ? 1 : 0; return RT_OK;
     case RT_OPT_WAVEFRONT: *v = c->opt_wavefront; return RT_OK;
+    case RT_OPT_WF_SORT: *v = c->opt_wf_sort; return RT_OK;
+    case RT_OPT_XCD_DEAL: *v = c->opt_xcd_deal; return RT_OK;
+    case RT_OPT_XCD_STRIPE: *v = c->opt_xcd_stripe; return RT_OK;
     default: return RT_E_ARG;
     }
 }
@@ -1044,7 +1094,10 @@ RT_EXPORT void rt_destroy(rt_ctx* c)
     hipFree(c->wf.mem);
     hipFree(c->wf.kin);
     hipFree(c->wf.kout);
-    hipFree(c->wf.stemp);
+    hipFree(c->wf.kout2);
+    hipFree(c->wf.hist);
+    hipFree(c->wf.bsum);
+    hipFree(c->d_skey);
     if (c->wf.ev) hipEventDestroy(c->wf.ev);
     for (auto& q : c->tiny_masks) {
         hipFree(q.d);
@@ -1586,7 +1639,10 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
     c->d_uni = nullptr;
     hipFree(c->d_bvh_node);
     hipFree(c->d_bvh_tri);
+    hipFree(c->d_skey);
     c->d_bvh_node = c->d_bvh_tri = nullptr;
+    c->d_skey = nullptr;
+    c->nbin_half = 0;
     c->bvh_inner = c->bvh_leaves = c->bvh_depth = 0;
     c->bvh_build_ms = 0.0;
     c->cb.valid = false;  // buffers are kept (reallocated on demand)
@@ -1614,6 +1670,24 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
         if (B.depth <= kBvhStack) {
             HIP_TRY(c, up((void**)&c->d_bvh_node, B.nodes.data(), B.nodes.size() * sizeof(float4)));
             HIP_TRY(c, up((void**)&c->d_bvh_tri, B.tris.data(), B.tris.size() * sizeof(float4)));
+            // the sort bins: triangle at leaf position p -> p / 2 (its
+            // file index is the leaf record's third float4 .y), every other
+            // surface a bin of its own after them
+            std::vector<unsigned> skey((size_t)n, 0u);
+            std::vector<char> is_tri((size_t)n, 0);
+            for (int i = 0; i < cnt_tri; ++i) {
+                int fi;
+                std::memcpy(&fi, &B.tris[3 * (size_t)i + 2].y, sizeof fi);
+                if (fi >= 0 && fi < n) {
+                    skey[(size_t)fi] = (unsigned)i >> 1;
+                    is_tri[(size_t)fi] = 1;
+                }
+            }
+            unsigned nb = ((unsigned)cnt_tri + 1u) >> 1;
+            for (int i = 0; i < n; ++i)
+                if (!is_tri[(size_t)i]) skey[(size_t)i] = nb++;
+            HIP_TRY(c, up((void**)&c->d_skey, skey.data(), skey.size() * sizeof(unsigned)));
+            c->nbin_half = nb;
             c->bvh_inner = B.inner;
             c->bvh_leaves = B.leaves;
             c->bvh_depth = B.depth;
@@ -1865,7 +1939,7 @@ typedef void (*kernel_fn)(const SceneDev, const FrameDev, unsigned*, float*, Sta
 // name (rt_stats.kernel).
 struct KernelPick {
     kernel_fn k = nullptr;
-    int cap = 0, lb = 1;
+    int cap = 0, lb = 1, wave = 0;
     unsigned lds = 0;
     char name[48] = {};
 };
@@ -1876,6 +1950,7 @@ static KernelPick kpick(unsigned lds)
     p.k = (kernel_fn)&rt_trace_kernel<MAXD, LB, WAVE, COUNT>;
     p.cap = MAXD;
     p.lb = LB;
+    p.wave = WAVE;
     p.lds = lds;
     std::snprintf(p.name, sizeof p.name, "rt_trace_kernel<%d,%d,%d>", MAXD, LB, WAVE);
     return p;
@@ -1950,6 +2025,26 @@ static int launch_trace(rt_ctx* c, const KernelPick& kp, const TinyCam* T, bool 
 {
     dim3 grid, block;
     trace_dims(width, rows, grid, block);
+    F.tiles_x = (int)grid.x;
+    F.tiles_y = (int)grid.y;
+    F.xcd_mode = 1;
+    F.xcd_w = 0;
+    F.xcd_m = 0;
+    if (!T && (kp.wave & 2) && c->opt_xcd_deal != 1) {
+        // the big-list kernels' padded grids (tile_of_block)
+        F.xcd_mode = c->opt_xcd_deal;
+        if (c->opt_xcd_deal == 2) {
+            const unsigned sw = c->opt_xcd_stripe > 0 ? (unsigned)c->opt_xcd_stripe : (grid.x + kXcds - 1) / kXcds;
+            F.xcd_w = (int)sw;
+            F.xcd_m = (int)((grid.x + kXcds * sw - 1) / (kXcds * sw) * sw);
+            grid = dim3(kXcds * (unsigned)F.xcd_m, grid.y);
+        } else if (c->opt_xcd_deal == 3) {
+            const unsigned gx = (grid.x + 3) / 4, gy = (grid.y + 1) / 2;
+            const unsigned nst = (gx * gy + kXcds - 1) / kXcds * kXcds;  // super-tiles, a multiple of 8
+            F.xcd_w = (int)gx;
+            grid = dim3(8, nst);
+        }
+    }
     if (T) {
         TinyCam Tv = *T;
         void* args[] = {&S, &F, &Tv, &oa, &ob, &stats};
@@ -2210,12 +2305,13 @@ static int wf_branch(const rt_ctx* c, const rt_frame* f)
 #define RT_WF_SHADE_WAVES 24  // shade launch: workgroups (one wave each) per CU (= its occupancy)
 #endif
 #ifndef RT_WF_SORT
-// each level's rays sorted by (parent surface, branch) before its trace,
-// for frames whose level queues hold at least this many ray slots: the
-// sort runs over the queue's capacity (the host never reads the count),
-// which at c3r (2.1 M slots) costs more than the coherence returns (+6%),
-// at c5r (33 M) less (-6%) — tools/ab_variants.py, profiles/r05/wfsort/
-#define RT_WF_SORT (6u << 20)
+// each level's rays sorted by their parent surface's bin (BVH leaf order)
+// and branch before its trace (rt_wf_sort_*), for frames whose level-1
+// queue holds at least this many ray slots (0: every wavefront frame).
+// Round 5's hipcub radix sort ran over the queue's capacity (+6% at c3r,
+// -6% at c5r, profiles/r05/wfsort/); the counting sort reads only the
+// level's live rays.
+#define RT_WF_SORT 0
 #endif
 #ifndef RT_WF_MAX_GB
 #define RT_WF_MAX_GB 32.0
@@ -2317,24 +2413,39 @@ static int wf_ensure(rt_ctx* c, const rt_frame* f, int rows, int levels, bool ca
     d.levels = levels;
     d.kin = nullptr;
     d.kout = nullptr;
-    if (RT_WF_SORT && levels >= 1 && w.cap[1] >= (size_t)RT_WF_SORT) {
+    d.skey = c->d_skey;
+    d.hist = nullptr;
+    d.nbin_half = c->nbin_half;
+    W.sort = 0;
+    if (c->d_skey && c->opt_wf_sort && levels >= 1 && w.cap[1] >= (size_t)RT_WF_SORT) {
         if (w.most > W.kcap) {
             free_later(c, W.kin);
             free_later(c, W.kout);
-            free_later(c, W.stemp);
-            W.kin = W.kout = nullptr;
-            W.stemp = nullptr;
+            free_later(c, W.kout2);
+            W.kin = W.kout = W.kout2 = nullptr;
             W.kcap = 0;
-            HIP_TRY(c, hipMalloc((void**)&W.kin, w.most * sizeof(unsigned long long)));
-            HIP_TRY(c, hipMalloc((void**)&W.kout, w.most * sizeof(unsigned long long)));
-            size_t tb = 0;
-            HIP_TRY(c, hipcub::DeviceRadixSort::SortKeys(nullptr, tb, (const unsigned long long*)nullptr,
-                                                          (unsigned long long*)nullptr, (int)w.most, 32, 64));
-            HIP_TRY(c, hipMalloc(&W.stemp, std::max<size_t>(tb, 16)));
-            W.stemp_bytes = std::max<size_t>(tb, 16);
+            HIP_TRY(c, hipMalloc((void**)&W.kin, w.most * sizeof(unsigned)));
+            HIP_TRY(c, hipMalloc((void**)&W.kout, w.most * sizeof(unsigned)));
+            HIP_TRY(c, hipMalloc((void**)&W.kout2, w.most * sizeof(unsigned)));
             W.kcap = w.most;
         }
-        d.kin = W.kin;
+        // (the hit sort's bins: nbin_half + kWfMissBins)
+        const size_t bins = std::max(2 * (size_t)c->nbin_half, (size_t)c->nbin_half + kWfMissBins);
+        if (bins + 1 > W.hcap) {
+            free_later(c, W.hist);
+            free_later(c, W.bsum);
+            W.hist = nullptr;
+            W.bsum = nullptr;
+            W.hcap = 0;
+            // the parent counts (hist), the hit counts, the scan's positions
+            // (next): bins + 1 words each
+            HIP_TRY(c, hipMalloc((void**)&W.hist, 3 * (bins + 1) * sizeof(unsigned)));
+            HIP_TRY(c, hipMalloc((void**)&W.bsum, scan_scratch(bins) * sizeof(unsigned long long)));
+            W.hcap = bins + 1;
+        }
+        W.sort = c->opt_wf_sort;
+        if (W.sort & 1) d.kin = W.kin;
+        d.hist = W.hist;
     }
     for (int L = 0; L <= levels; ++L) {
         W.cap[L] = L == 0 ? px : w.cap[L];
@@ -2369,10 +2480,6 @@ static int wf_levels(rt_ctx* c, const SceneDev& S, const FrameDev& F, int levels
     const unsigned lds_t = (unsigned)((size_t)c->bvh_depth * 64 * sizeof(int));
     const unsigned lds_s = big ? (unsigned)kLdsWaveBytes : 0u;
     rt_ctx::WfBuf& W = c->wf;
-    // the sort keys' significant bits: (surface x 2 + 1) < 2^bits - 1, so an
-    // empty slot's all-ones key sorts after every ray
-    int bits = 1;
-    while (((size_t)1 << bits) < 2 * (size_t)c->n_surf + 3) ++bits;
     for (int L = 1; L <= levels; ++L) {
         // enough waves to fill the chip; each strides over the level's queue
         const size_t waves = (W.cap[L] + 63) / 64;
@@ -2380,12 +2487,20 @@ static int wf_levels(rt_ctx* c, const SceneDev& S, const FrameDev& F, int levels
         const unsigned gs = (unsigned)std::max<size_t>(1, std::min<size_t>(waves, (size_t)c->n_cu * RT_WF_SHADE_WAVES));
         FrameDev Fl = F;
         Fl.wf.budget = W.cap[L] >= (size_t)RT_WF_BUDGET_SPLIT ? RT_WF_BUDGET_BIG : RT_WF_BUDGET_SMALL;
+        const unsigned gq = (unsigned)std::max<size_t>(1, std::min<size_t>(waves, (size_t)c->n_cu * 32));
         if (W.dev.kin) {
-            // the level's rays by (parent surface, branch): rays leaving one
-            // triangle share its normal, so their walks and hits stay together
-            size_t tb = W.stemp_bytes;
-            HIP_TRY(c, hipcub::DeviceRadixSort::SortKeys(W.stemp, tb, (const unsigned long long*)W.kin, W.kout,
-                                                          (int)W.cap[L], 32, 32 + bits, st));
+            // the level's live rays by bin (parent surface in BVH leaf order,
+            // branch): rays leaving one triangle share its normal, rays of
+            // neighbouring triangles their subtree, so their walks and hits
+            // stay together
+            // (the counts came with the appends; the scan leaves them zero
+            // for the next level's)
+            const unsigned bins = 2u * c->nbin_half;
+            unsigned* next = W.hist + 2 * W.hcap;
+            HIP_TRY(c, scan_u32(W.hist, bins, next, W.bsum, st, nullptr, true));
+            hipLaunchKernelGGL(rt_wf_sort_place<0>, dim3(gq), dim3(64), 0, st, F, L, (const unsigned*)nullptr, next,
+                               W.kout);
+            HIP_TRY(c, hipGetLastError());
             Fl.wf.kout = W.kout;
         }
         int Lv = L;
@@ -2393,9 +2508,22 @@ static int wf_levels(rt_ctx* c, const SceneDev& S, const FrameDev& F, int levels
         HIP_TRY(c, hipLaunchKernel(kt, dim3(gt), dim3(64), args, lds_t, st));
         HIP_TRY(c, hipLaunchKernel(kg, dim3((unsigned)c->n_cu * RT_WF_STRAG_WAVES), dim3(64), args,
                                    (unsigned)(kWfStragCap * sizeof(int)), st));
-        if (W.dev.kin && L < levels)  // the next level's keys, written by the shade launch
-            HIP_TRY(c, hipMemsetAsync(W.kin, 0xFF, W.cap[L + 1] * sizeof(unsigned long long), st));
-        HIP_TRY(c, hipLaunchKernel(ks, dim3(gs), dim3(64), args, lds_s, st));
+        FrameDev Fs = Fl;
+        if (W.sort & 2) {
+            // the level's rays by hit surface's bin for the shading (whose
+            // children, appended in that order, then sit by parent bin)
+            const unsigned hb = c->nbin_half + kWfMissBins;
+            unsigned *hist2 = W.hist + W.hcap, *next = W.hist + 2 * W.hcap;
+            hipLaunchKernelGGL(rt_wf_hit_count, dim3(gq), dim3(64), 0, st, F, L, (const unsigned*)Fl.wf.kout, hist2);
+            HIP_TRY(c, hipGetLastError());
+            HIP_TRY(c, scan_u32(hist2, hb, next, W.bsum, st, nullptr, true));
+            hipLaunchKernelGGL(rt_wf_sort_place<1>, dim3(gq), dim3(64), 0, st, F, L, (const unsigned*)Fl.wf.kout, next,
+                               W.kout2);
+            HIP_TRY(c, hipGetLastError());
+            Fs.wf.kout = W.kout2;
+        }
+        void* sargs[] = {(void*)&S, (void*)&Fs, (void*)&Lv, (void*)&stats};
+        HIP_TRY(c, hipLaunchKernel(ks, dim3(gs), dim3(64), sargs, lds_s, st));
     }
     for (int L = levels - 1; L >= 0; --L) {
         const unsigned g = (unsigned)std::min<size_t>((c->wf.pcap[L] + 255) / 256, (size_t)c->n_cu * 4);
@@ -2493,8 +2621,8 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
         rt_ctx::WfBuf& W = c->wf;
         if (W.pending && W.last != st) HIP_TRY(c, hipStreamWaitEvent(st, W.ev, 0));
         HIP_TRY(c, hipMemsetAsync(W.dev.count, 0, kWfCountBytes, st));
-        if (W.dev.kin)  // level 1's keys: empty slots sort last
-            HIP_TRY(c, hipMemsetAsync(W.dev.kin, 0xFF, W.cap[1] * sizeof(unsigned long long), st));
+        if (W.sort)  // the bin counts (level 1's: the level-0 kernel's appends)
+            HIP_TRY(c, hipMemsetAsync(W.dev.hist, 0, 2 * W.hcap * sizeof(unsigned), st));
     }
     if (nch <= 1) {
         if (int rc = launch_trace(c, kp, tiny, f->flags & RT_FLAG_STATS, S, F, f->width, rows, rgba_dev, rgb_dev, stats,

@@ -157,12 +157,18 @@ struct WfDev {
     float2* hit;      // the level being shaded: [file index (int bits), t] per ray slot
     int4* strag;      // the level's straggling walks: [ray slot, partial t (bits), partial index, -]
     unsigned* count;  // counters, kWfCntStride words apart: wf_rays / wf_pars / wf_strag
-    // Coherence sort (RT_WF_SORT): the rays being appended write sort keys
-    // (parent surface x 2 + refracted) << 32 | slot into kin (empty slots all
-    // ones); the host sorts them into kout before the level's trace, and the
-    // trace and shade launches take rays in kout's order (null: queue order).
-    unsigned long long* kin;
-    const unsigned long long* kout;
+    // Coherence sort (round 6): a ray being appended writes its bin into
+    // kin[slot] — its parent surface's spatial bin skey[surf] (triangles in
+    // the BVH's leaf order), + nbin_half for a refracted ray — and before the
+    // level's trace a counting sort over the level's LIVE rays (rt_wf_sort_*:
+    // histogram, scan, scatter) writes the level's slots in bin order into
+    // kout; the trace and shade launches take rays in kout's order (null:
+    // queue order).
+    unsigned* kin;
+    const unsigned* kout;
+    const unsigned* skey;
+    unsigned* hist;       // 2 nbin_half + 1 words: bin counts, then the scatter's next positions
+    unsigned nbin_half;
     int levels;
     int budget;  // steps (inner nodes + leaves) a trace-launch walk takes before the straggler hand-off
 };
@@ -187,6 +193,11 @@ struct FrameDev {
     float min_energy, scene_ior;
     int flags;
     int band_rows, band_count, band_index;  // band_rows > 0: cyclic row bands (rt.h)
+    // The launch's tile grid and how the big-list kernels deal tiles to the
+    // XCDs (RT_OPT_XCD_DEAL, tile_of_block): tiles_x x tiles_y 8 x 8 tiles;
+    // xcd_w = tiles per stripe (mode 2) or super-tile columns (mode 3);
+    // xcd_m = an XCD's tile slots per tile row (mode 2).
+    int tiles_x, tiles_y, xcd_mode, xcd_w, xcd_m;
     WfDev wf;
 };
 

@@ -69,9 +69,11 @@ __global__ __launch_bounds__(kScanThreads) void rt_scan_blocks(unsigned long lon
 // Pass 3: out[i] = exclusive prefix of in[i] (out may alias in), out[n] =
 // total; both truncated to 32 bits — the caller checks bsum[nb] (64-bit).
 // Thread t owns the 16 consecutive counts [16t, 16t + 16) of its block's tile.
+// zero_in: in (distinct from out) is left all zeros (a counter array that
+// is scanned and then counts again: the wavefront's sort bins).
 __global__ __launch_bounds__(kScanThreads) void rt_scan_apply(const unsigned* in, unsigned n,
                                                               const unsigned long long* __restrict__ bsum,
-                                                              unsigned nb, unsigned* out)
+                                                              unsigned nb, unsigned* out, bool zero_in = false)
 {
     __shared__ unsigned long long sh[kScanThreads];
     const size_t base = (size_t)blockIdx.x * kScanTile + (size_t)threadIdx.x * kScanItems;
@@ -80,6 +82,7 @@ __global__ __launch_bounds__(kScanThreads) void rt_scan_apply(const unsigned* in
     for (int q = 0; q < kScanItems; ++q) {
         v[q] = base + q < n ? in[base + q] : 0u;
         s += v[q];
+        if (zero_in && base + q < n) const_cast<unsigned*>(in)[base + q] = 0u;
     }
     unsigned long long tot;
     unsigned long long run = bsum[blockIdx.x] + block_exscan(s, sh, &tot);
@@ -125,7 +128,8 @@ __global__ __launch_bounds__(kScanSmallThreads) void rt_scan_small_reduce(const 
 }
 __global__ __launch_bounds__(kScanSmallThreads) void rt_scan_small_apply(const unsigned* in, unsigned n,
                                                                          unsigned long long* __restrict__ bsum,
-                                                                         unsigned nb, unsigned* out)
+                                                                         unsigned nb, unsigned* out,
+                                                                         bool zero_in = false)
 {
     __shared__ unsigned ws[kScanSmallThreads / 64];
     __shared__ unsigned long long pre;
@@ -136,6 +140,7 @@ __global__ __launch_bounds__(kScanSmallThreads) void rt_scan_small_apply(const u
     for (int c = 0; c < 4; ++c) {
         const unsigned i = base + (unsigned)c * 64u;
         v[c] = i < n ? in[i] : 0u;
+        if (zero_in && i < n) const_cast<unsigned*>(in)[i] = 0u;
     }
     if (w == 0) {  // this block's prefix; block 0: the total
         const unsigned long long x = (unsigned)lane < nb ? bsum[lane] : 0ull;
@@ -184,13 +189,15 @@ inline size_t scan_scratch(size_t n)
 
 // Exclusive scan of in[0..n) into out[0..n], out[n] = total, on stream st;
 // bsum (scan_scratch(n) u64) receives the 64-bit total at bsum[nb].  n >= 1.
+// zero_in: in (then distinct from out) is left all zeros.
 inline hipError_t scan_u32(const unsigned* in, unsigned n, unsigned* out, unsigned long long* bsum, hipStream_t st,
-                           unsigned long long** total_dev)
+                           unsigned long long** total_dev, bool zero_in = false)
 {
     if (n <= kScanSmallMax) {
         const unsigned nb = (n + kScanSmallTile - 1) / kScanSmallTile;
         hipLaunchKernelGGL(rt_scan_small_reduce, dim3(nb), dim3(kScanSmallThreads), 0, st, in, n, bsum);
-        hipLaunchKernelGGL(rt_scan_small_apply, dim3(nb), dim3(kScanSmallThreads), 0, st, in, n, bsum, nb, out);
+        hipLaunchKernelGGL(rt_scan_small_apply, dim3(nb), dim3(kScanSmallThreads), 0, st, in, n, bsum, nb, out,
+                           zero_in);
         if (total_dev) *total_dev = bsum + nb;
         return hipGetLastError();
     }
@@ -198,7 +205,7 @@ inline hipError_t scan_u32(const unsigned* in, unsigned n, unsigned* out, unsign
     hipLaunchKernelGGL(rt_scan_reduce, dim3(nb), dim3(kScanThreads), 0, st, in, n, bsum);
     hipLaunchKernelGGL(rt_scan_blocks, dim3(1), dim3(kScanThreads), 0, st, bsum, nb);
     hipLaunchKernelGGL(rt_scan_apply, dim3(nb), dim3(kScanThreads), 0, st, in, n, (const unsigned long long*)bsum, nb,
-                       out);
+                       out, zero_in);
     if (total_dev) *total_dev = bsum + nb;
     return hipGetLastError();
 }

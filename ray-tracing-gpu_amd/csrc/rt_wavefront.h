@@ -35,6 +35,46 @@ __device__ __forceinline__ unsigned lane_rank(unsigned long long m)
     return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
 }
 
+__device__ __forceinline__ void wave_bins_count(bool on, unsigned key, unsigned* __restrict__ hist)
+{
+    const int lane = (int)(threadIdx.x & 63);
+    unsigned cnt = 0u;
+    unsigned long long left = __ballot(on);
+    while (left) {
+        const int lead = (int)__builtin_ctzll(left);
+        const unsigned k0 = (unsigned)__builtin_amdgcn_readlane((int)key, lead);
+        const unsigned long long same = __ballot(on & (key == k0)) & left;
+        if (lane == lead) cnt = (unsigned)__popcll(same);
+        left &= ~same;
+    }
+    if (cnt > 0u) atomicAdd(&hist[key], cnt);  // every bin's first lane, one instruction
+}
+// The wave's bins are found first (each lane: its bin's first lane and its
+// rank there; the first lane: the bin's count), then every bin's first lane
+// claims the bin's positions in ONE atomic instruction, and every lane
+// takes its first lane's.
+__device__ __forceinline__ unsigned wave_bins_place(bool on, unsigned key, unsigned* __restrict__ next)
+{
+    const int lane = (int)(threadIdx.x & 63);
+    unsigned cnt = 0u, rank = 0u;
+    int lead_of = lane;
+    unsigned long long left = __ballot(on);
+    while (left) {
+        const int lead = (int)__builtin_ctzll(left);
+        const unsigned k0 = (unsigned)__builtin_amdgcn_readlane((int)key, lead);
+        const unsigned long long same = __ballot(on & (key == k0)) & left;
+        if (lane == lead) cnt = (unsigned)__popcll(same);
+        if ((same >> lane) & 1ull) {
+            lead_of = lead;
+            rank = lane_rank(same);
+        }
+        left &= ~same;
+    }
+    unsigned mine = 0u;
+    if (cnt > 0u) mine = atomicAdd(&next[key], cnt);
+    return (unsigned)__shfl((int)mine, lead_of) + rank;
+}
+
 // A segmented queue as the consumer sees it: the prefix sums of its
 // kWfSeg segment counts (wave-uniform: scalar loads of the counters the
 // previous launch left) and the slot of compacted index x.
@@ -101,7 +141,7 @@ __device__ __forceinline__ bool wf_children(const FrameDev& F, int L, bool act, 
         const Vec3 Dr = reflect(D, N);
         q[2 * (size_t)cR] = make_float4(P.x, P.y, P.z, 0.0f);
         q[2 * (size_t)cR + 1] = make_float4(Dr.x, Dr.y, Dr.z, er);
-        if (F.wf.kin) F.wf.kin[cR] = ((unsigned long long)(2u * (unsigned)surf) << 32) | (unsigned)cR;
+        if (F.wf.kin) F.wf.kin[cR] = F.wf.skey[surf];
     }
     if (doT) {
         cT = (int)(base + (unsigned)__popcll(bR) + lane_rank(bT));
@@ -118,7 +158,12 @@ __device__ __forceinline__ bool wf_children(const FrameDev& F, int L, bool act, 
         const Vec3 Dt = refract(D, n, ratio);
         q[2 * (size_t)cT] = make_float4(P.x, P.y, P.z, rior_t);
         q[2 * (size_t)cT + 1] = make_float4(Dt.x, Dt.y, Dt.z, et);
-        if (F.wf.kin) F.wf.kin[cT] = ((unsigned long long)(2u * (unsigned)surf + 1u) << 32) | (unsigned)cT;
+        if (F.wf.kin) F.wf.kin[cT] = F.wf.skey[surf] + F.wf.nbin_half;
+    }
+    if (F.wf.kin) {  // the coherence sort's bin counts (rt_wf_sort_place)
+        const unsigned kb = (doR | doT) ? F.wf.skey[surf] : 0u;
+        if (bR) wave_bins_count(doR, kb, F.wf.hist);
+        if (bT) wave_bins_count(doT, kb + F.wf.nbin_half, F.wf.hist);
     }
     if (doR | doT) {
         float4* nd = F.wf.node[L] + 2 * (size_t)self;
@@ -127,6 +172,61 @@ __device__ __forceinline__ bool wf_children(const FrameDev& F, int L, bool act, 
         F.wf.plist[L][pbase + lane_rank(bP)] = self;
     }
     return doR | doT;
+}
+
+// The coherence sort of a level's live rays by bin (WfDev::kin), a counting
+// sort whose work follows the rays, not the queue's capacity: the producers
+// (the level-0 kernel, the shade launches) count each appended ray into
+// hist[bin] as they write its bin (wf_children); before the level's trace
+// the host scans the counts into each bin's first position (zeroing them
+// for the next level), and rt_wf_sort_place claims positions and writes the
+// level's slots to kout in bin order.  Both use one atomic per distinct bin
+// of a wave (wave_bins_*: rays of one parent triangle sit together in a
+// wave).  The order inside a bin is the atomics' — every ray is
+// independent, so the image does not depend on it.
+// KEY 0: the ray's parent bin (kin, counted by its producer); KEY 1 (the
+// hit sort before a level's shade, RT_OPT_WF_SORT 2 / 3): its hit surface's
+// bin — so the shading, its light-buffer cells, and the children it appends
+// (whose parent is that surface) stay together — and for a miss one of
+// kWfMissBins bins by its 64-ray chunk of the trace's order (one bin for
+// every miss serialised all waves' atomics on one address).
+// order: the level's slots in the trace's order (null: queue order).
+constexpr unsigned kWfMissBins = 256;
+template <int KEY>
+__device__ __forceinline__ unsigned wf_sort_key(const FrameDev& F, unsigned slot, unsigned x)
+{
+    if constexpr (KEY == 0) return F.wf.kin[slot];
+    const int idx = __float_as_int(F.wf.hit[slot].x);
+    return idx >= 0 ? F.wf.skey[idx] : F.wf.nbin_half + ((x >> 6) & (kWfMissBins - 1u));
+}
+
+__global__ __launch_bounds__(64) void rt_wf_hit_count(const FrameDev F, int L, const unsigned* __restrict__ order,
+                                                      unsigned* __restrict__ hist)
+{
+    const WfQueue Q = wf_queue(F.wf.count, wf_rays(L, 0), F.wf.seg[L]);
+    const unsigned n = Q.pre[kWfSeg];
+    for (unsigned base = blockIdx.x * 64u; base < n; base += gridDim.x * 64u) {
+        const unsigned x = base + (threadIdx.x & 63u);
+        const bool valid = x < n;
+        const unsigned slot = valid ? (order ? order[x] : wf_slot(Q, x)) : 0u;
+        wave_bins_count(valid, valid ? wf_sort_key<1>(F, slot, x) : 0u, hist);
+    }
+}
+
+template <int KEY>
+__global__ __launch_bounds__(64) void rt_wf_sort_place(const FrameDev F, int L, const unsigned* __restrict__ order,
+                                                       unsigned* __restrict__ next, unsigned* __restrict__ kout)
+{
+    const WfQueue Q = wf_queue(F.wf.count, wf_rays(L, 0), F.wf.seg[L]);
+    const unsigned n = Q.pre[kWfSeg];
+    for (unsigned base = blockIdx.x * 64u; base < n; base += gridDim.x * 64u) {
+        const unsigned x = base + (threadIdx.x & 63u);
+        const bool valid = x < n;
+        const unsigned slot = valid ? (order ? order[x] : wf_slot(Q, x)) : 0u;
+        const unsigned k = valid ? wf_sort_key<KEY>(F, slot, x) : 0u;
+        const unsigned pos = wave_bins_place(valid, k, next);
+        if (valid) kout[pos] = slot;
+    }
 }
 
 // Bounce level L >= 1 runs as two launches over the level's queue (a
@@ -199,7 +299,7 @@ __global__ __launch_bounds__(64) void rt_wf_trace(const SceneDev S, const FrameD
             more = b + (unsigned)__popcll(fm) < n;
             const unsigned x = b + lane_rank(fm);
             if (!busy && x < n) {
-                slot = F.wf.kout ? (unsigned)F.wf.kout[x] : wf_slot(Q, x);
+                slot = F.wf.kout ? F.wf.kout[x] : wf_slot(Q, x);
                 const float4 r0 = q[2 * (size_t)slot], r1 = q[2 * (size_t)slot + 1];
                 O = make3(r0.x, r0.y, r0.z);
                 D = make3(r1.x, r1.y, r1.z);
@@ -372,7 +472,7 @@ __global__ __launch_bounds__(64, RT_WF_SHADE_EU) void rt_wf_shade(const SceneDev
     for (unsigned base = blockIdx.x * 64u; base < n; base += gridDim.x * 64u) {
         const unsigned x = base + (threadIdx.x & 63u);
         if (x < n) {
-            const unsigned i = F.wf.kout ? (unsigned)F.wf.kout[x] : wf_slot(Q, x);
+            const unsigned i = F.wf.kout ? F.wf.kout[x] : wf_slot(Q, x);
             const float2 h = F.wf.hit[i];
             const int idx = __float_as_int(h.x);
             Color res = bg;

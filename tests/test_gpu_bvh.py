@@ -413,3 +413,45 @@ def test_negative_min_energy_spawns_both_children(tmp_path, oracle):
 
     path = synth.write_heightfield(str(tmp_path / "hf_neg.dat"), cols=12, rows=6, reflect=0.5)
     _three_ways(path, 1920, 1080, 3, -1.0, oracle)
+
+
+@pytest.mark.parametrize("sort", [0, 2, 3])
+def test_wavefront_sort_orders_render_the_same(hfr, hfr_golden, sort):
+    """RT_OPT_WF_SORT (the counting sorts of each level's live rays by parent
+    bin and by hit bin) only changes which wave takes which ray: the
+    reflective heightfield at 1920 x 1080 d3 and d6 against the reference's
+    windows, bit for bit, and the refracting mesh against the default."""
+    ctx, get = hfr
+    ctx.set_option("wf_sort", sort)
+    try:
+        for d in (3, 6):
+            full = ctx.render_float(get(1920, 1080, d).frame)
+            for win, want, k in _groups(hfr_golden)[(1920, 1080, d)]:
+                r0, r1, c0, c1 = win
+                assert bits_equal(full[r0:r1, c0:c1], want), k
+    finally:
+        ctx.set_option("wf_sort", 1)
+
+
+def test_refractive_mesh_sort_orders(tmp_path):
+    from rt_amd import synth
+
+    lines, k = [], 0
+    for line in synth.heightfield_dat(cols=40, rows=20, reflect=0.3).split("\n"):
+        lines.append(line)
+        if line.startswith("        reflect:"):
+            if k % 2 == 0:
+                lines.append("        refract: 0.4 1.5")
+            k += 1
+    path = tmp_path / "hf_refr.dat"
+    path.write_text("\n".join(lines))
+    s = rt_amd.Scene(str(path), 1920, 1080, 4)
+    imgs = []
+    for sort in (0, 1, 2, 3):
+        c = rt_amd.Context(0, wf_sort=sort)
+        c.upload(s)
+        imgs.append(c.render_float(s.frame))
+        assert c.stats().kernel.startswith("wavefront")
+        c.close()
+    for im in imgs[1:]:
+        assert bits_equal(im, imgs[0])

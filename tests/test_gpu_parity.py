@@ -132,6 +132,43 @@ def test_heightfield_without_plane_silhouette(ctx, tmp_path):
     assert mixed >= 5
 
 
+@pytest.mark.parametrize("mode,stripe", [(0, 0), (2, 0), (2, 3), (2, 4), (3, 0)])
+def test_xcd_deal_modes_render_the_same(golden_images, c3_column, heightfield_path, mode, stripe):
+    """RT_OPT_XCD_DEAL: the big-list kernels' tile-to-XCD dealing (padded
+    grids in modes 2 and 3) only moves tiles between workgroups: C3 at full
+    size against the reference's windows, a slab off the tile grid, a band
+    set and the reflective mesh's wavefront level 0 — all equal to mode 1
+    (stripes of 3 and 4 tiles: 240 tile columns are not a multiple of 24)."""
+    from rt_amd import synth
+
+    a, b = rt_amd.Context(0, xcd_deal=1), rt_amd.Context(0, xcd_deal=mode, xcd_stripe=stripe)
+    s = rt_amd.Scene(heightfield_path, 1920, 1080, 1)
+    for c in (a, b):
+        c.upload(s)
+    full = b.render_float(s.frame)
+    for k, want in _hf_windows(golden_images, c3_column):
+        r0, r1, c0, c1 = map(int, k.rsplit("_win_", 1)[1].split("_"))
+        check(full[r0:r1, c0:c1], want, 0)
+    frames = []
+    f = s.frame.copy()
+    f.row_begin, f.row_end = 203, 1077
+    frames.append(f)
+    f = s.frame.copy()
+    f.band_rows, f.band_count, f.band_index = 16, 3, 2
+    frames.append(f)
+    f = s.frame.copy()
+    f.width, f.height, f.row_end = 1000, 1000, 1000  # tiles not a multiple of 8 either way
+    f.inv_w, f.inv_h = 1.0 / 1000, 1.0 / 1000
+    frames.append(f)
+    for f in frames:
+        assert bits_equal(b.render_float(f), a.render_float(f))
+    hf = synth.write_heightfield("/tmp/rt_amd_xcd_hfr.dat", cols=60, rows=30, reflect=0.5)
+    s2 = rt_amd.Scene(hf, 1920, 1080, 3)
+    for c in (a, b):
+        c.upload(s2)
+    assert bits_equal(b.render_float(s2.frame), a.render_float(s2.frame))
+
+
 @pytest.mark.parametrize("near,far", [(1.5, [64.0]), (1.5, [1.6]), (1.05, [1.1, 1.3, 2.0, 4.0]),
                                       (1.02, [1.05, 1.1, 1.2, 1.4, 1.8, 2.5, 4.0, 8.0]), (1.25, [])])
 def test_heightfield_far_buffer(golden_images, c3_column, heightfield_path, near, far):
