@@ -2298,8 +2298,10 @@ static int wf_branch(const rt_ctx* c, const rt_frame* f)
 // straggler launch: workgroups (one wave, one straggling ray at a time, its
 // kWfStragCap-entry LDS stack) per CU: 4 / 8 / 16 waves of 16 / 16 / 8 KB,
 // c3r 3.359 / 3.273 / 3.249 ms, c5r 21.13 / 19.80 / 19.19
-// (profiles/r05/sorder/ab_straggle*.log)
-#define RT_WF_STRAG_WAVES 16
+// (profiles/r05/sorder/ab_straggle*.log); round 6, with the sorted levels:
+// 32 waves of 4 KB against 16 of 8 KB, c3r 2.862 / 2.887, c5r 17.65 / 17.77
+// (profiles/r06/knobs/)
+#define RT_WF_STRAG_WAVES 32
 #endif
 #ifndef RT_WF_SHADE_WAVES
 #define RT_WF_SHADE_WAVES 24  // shade launch: workgroups (one wave each) per CU (= its occupancy)
@@ -2514,10 +2516,12 @@ static int wf_levels(rt_ctx* c, const SceneDev& S, const FrameDev& F, int levels
             // children, appended in that order, then sit by parent bin)
             const unsigned hb = c->nbin_half + kWfMissBins;
             unsigned *hist2 = W.hist + W.hcap, *next = W.hist + 2 * W.hcap;
-            hipLaunchKernelGGL(rt_wf_hit_count, dim3(gq), dim3(64), 0, st, F, L, (const unsigned*)Fl.wf.kout, hist2);
+            // (both passes read the rays in queue order: consecutive slots,
+            // coalesced hit records — the order inside a bin does not matter)
+            hipLaunchKernelGGL(rt_wf_hit_count, dim3(gq), dim3(64), 0, st, F, L, (const unsigned*)nullptr, hist2);
             HIP_TRY(c, hipGetLastError());
             HIP_TRY(c, scan_u32(hist2, hb, next, W.bsum, st, nullptr, true));
-            hipLaunchKernelGGL(rt_wf_sort_place<1>, dim3(gq), dim3(64), 0, st, F, L, (const unsigned*)Fl.wf.kout, next,
+            hipLaunchKernelGGL(rt_wf_sort_place<1>, dim3(gq), dim3(64), 0, st, F, L, (const unsigned*)nullptr, next,
                                W.kout2);
             HIP_TRY(c, hipGetLastError());
             Fs.wf.kout = W.kout2;

@@ -221,6 +221,12 @@ static int render_rccl(std::vector<rt_ctx*>& ctx, std::vector<rt_frame>& part,
                 return fail("hipStreamWaitEvent", RT_E_HIP, "");
         }
         (void)hipSetDevice(devs[0]);
+        // the root's gather stream starts timing once EVERY rank's slab is
+        // rendered (its receives wait for them anyway), so the reported
+        // gather time is the exchange, not the slowest rank's render
+        for (int r = 1; r < n; ++r)
+            if (!img[r].empty() && hipStreamWaitEvent((hipStream_t)G.stream(g, 0), ev_r[2 * r + b], 0) != hipSuccess)
+                return fail("hipStreamWaitEvent", RT_E_HIP, "");
         (void)hipEventRecord(t_g0[k], (hipStream_t)G.stream(g, 0));
         if ((rc = G.chunks(g, (int32_t)ch[b].size(), ch[b].data(), full)))
             return fail("rt_gather_chunks", rc, G.error(g));

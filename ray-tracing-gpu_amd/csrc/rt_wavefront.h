@@ -289,6 +289,12 @@ __global__ __launch_bounds__(64) void rt_wf_trace(const SceneDev S, const FrameD
     Vec3 O = make3(0.f, 0.f, 0.f), D = O, inv = O;
     float bt = -1.0f;
     int bi = -1, node = kDone, leaf = 0, sp = 0, steps = 0;
+#define WF_PUSH(x)            \
+    do {                      \
+        stk[64 * sp] = (x);   \
+        ++sp;                 \
+    } while (0)
+#define WF_POP(dst) (dst) = sp > 0 ? stk[64 * --sp] : kDone
     for (;;) {
         const unsigned long long fm = __ballot(!busy);
         if (more && fm && (__popcll(fm) >= kWfRefill || !__any(busy))) {
@@ -365,17 +371,16 @@ __global__ __launch_bounds__(64) void rt_wf_trace(const SceneDev S, const FrameD
                 const bool h1 = bvh_box(b0, b1, O, inv, have, bt, t1);
                 if (h0 & h1) {
                     const bool near0 = !(t1 < t0);
-                    stk[64 * sp] = near0 ? r1 : r0;
-                    ++sp;
+                    WF_PUSH(near0 ? r1 : r0);
                     node = near0 ? r0 : r1;
                 } else if (h0 | h1) {
                     node = h0 ? r0 : r1;
                 } else {
-                    node = sp > 0 ? stk[64 * --sp] : kDone;
+                    WF_POP(node);
                 }
                 if ((node < 0) & (leaf == 0)) {  // postpone the first leaf, walk on
                     leaf = node;
-                    node = sp > 0 ? stk[64 * --sp] : kDone;
+                    WF_POP(node);
                 }
                 if (__all(leaf != 0)) break;
             }
@@ -398,7 +403,7 @@ __global__ __launch_bounds__(64) void rt_wf_trace(const SceneDev S, const FrameD
                     leaf = 0;
                     if ((node < 0) & (node != kDone)) {  // the leaf that ended the inner loop
                         leaf = node;
-                        node = sp > 0 ? stk[64 * --sp] : kDone;
+                        WF_POP(node);
                     }
                     ++steps;
                 }
@@ -419,12 +424,14 @@ __global__ __launch_bounds__(64) void rt_wf_trace(const SceneDev S, const FrameD
         if (fin | str) busy = false;
     }
     if (COUNT && (F.flags & RT_FLAG_STATS)) wf_tally<COUNT>(cnt, stats);
+#undef WF_PUSH
+#undef WF_POP
 }
 
 // The straggling walks of level L, one ray per wave (bvh_walk_wave: the
 // wave's LDS stack of kWfStragCap references).
 #ifndef RT_WF_STRAG_CAP
-#define RT_WF_STRAG_CAP 2048
+#define RT_WF_STRAG_CAP 1024
 #endif
 constexpr int kWfStragCap = RT_WF_STRAG_CAP;
 template <bool COUNT>
