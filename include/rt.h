@@ -273,6 +273,10 @@ enum {
                                    never changes an image */
     RT_OPT_XCD_STRIPE = 17,     /* launch (ABI 8): RT_OPT_XCD_DEAL 2's stripe width in tiles,
                                    stripe s on XCD s % 8; 0 (default) one stripe per XCD */
+    RT_OPT_LB_UNROLL = 18,      /* launch (ABI 8): depth-0 frames of more than 1,024 triangles
+                                   under 4 Mpx of output rows walk the light buffer's
+                                   per-lane lists two entries per round: 1 (default) / 0;
+                                   never changes an image */
     RT_OPT_LAUNCH_CAMERA = 12   /* launch (ABI 6): depth-0 frames of scenes of 1-20
                                    triangles with light-buffer shadows take their camera
                                    records with the kernel launch — per-triangle camera

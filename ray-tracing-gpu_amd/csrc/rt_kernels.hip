@@ -801,6 +801,7 @@ struct rt_ctx {
     int opt_wf_sort = 1;        // RT_OPT_WF_SORT
     int opt_xcd_deal = 1;       // RT_OPT_XCD_DEAL
     int opt_xcd_stripe = 0;     // RT_OPT_XCD_STRIPE
+    bool opt_lb_unroll = true;  // RT_OPT_LB_UNROLL
     float kr_max = 0.0f, kt_max = 0.0f;  // max Kr, max Kt over surfaces
     bool uploaded = false;
     rt_stats last{};
@@ -988,6 +989,7 @@ RT_EXPORT int rt_set_option(rt_ctx* c, int32_t opt, double v)
         if (v != 0 && v != 1 && v != 2 && v != 3) return RT_E_ARG;
         c->opt_xcd_deal = (int)v;
         return RT_OK;
+    case RT_OPT_LB_UNROLL: c->opt_lb_unroll = v != 0; return RT_OK;
     case RT_OPT_XCD_STRIPE:
         if (v < 0 || v > 4096 || v != std::floor(v)) return RT_E_ARG;
         c->opt_xcd_stripe = (int)v;
@@ -1019,6 +1021,7 @@ RT_EXPORT int rt_get_option(rt_ctx* c, int32_t opt, double* v)
     case RT_OPT_WF_SORT: *v = c->opt_wf_sort; return RT_OK;
     case RT_OPT_XCD_DEAL: *v = c->opt_xcd_deal; return RT_OK;
     case RT_OPT_XCD_STRIPE: *v = c->opt_xcd_stripe; return RT_OK;
+    case RT_OPT_LB_UNROLL: *v = c->opt_lb_unroll ? 1 : 0; return RT_OK;
     default: return RT_E_ARG;
     }
 }
@@ -1962,15 +1965,22 @@ static KernelPick kpick(unsigned lds)
 // LDS after the staging window.
 // chain: no refracted ray can pass its gate (reflect-only scenes): the
 // bounce kernels keep the chain in registers (WAVE bit 1024).
+// small: a frame under 4 Mpx of output rows — the big-list kernel walks the
+// light buffer's per-lane lists two entries per round (WAVE bit 2048,
+// rt_shade.h lb_slot: its 8 x 8 tiles see more cells there than the staged
+// walk takes; C3 -6%, and no gain at C5 for the registers it holds,
+// profiles/r06/lbwalk/).
 template <bool COUNT>
 static KernelPick pick_kernel(int depth, int n_tri, int n_lights, bool lbuf, bool cbuf, int bvh_depth = 0,
-                              bool chain = false)
+                              bool chain = false, bool small = false)
 {
     const bool bvh = bvh_depth > 0;
     const unsigned win = (unsigned)kLdsWaveBytes;
     if (depth == 0 && n_tri > 0 && lbuf) {  // light-buffer shadows, one light per pass
-        if (n_tri > kClusterMinTriangles)
+        if (n_tri > kClusterMinTriangles) {
+            if (small) return cbuf ? kpick<0, 1, 2062, COUNT>(win) : kpick<0, 1, 2054, COUNT>(win);
             return cbuf ? kpick<0, 1, 14, COUNT>(win) : kpick<0, 1, 6, COUNT>(win);
+        }
         return cbuf ? kpick<0, 1, 13, COUNT>(0) : kpick<0, 1, 5, COUNT>(0);
     }
     if (depth == 0 && n_tri > kClusterMinTriangles)
@@ -2585,11 +2595,12 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
         wf = ok;
     }
     const bool count = (f->flags & RT_FLAG_STATS) != 0;
+    const bool small = (double)f->width * rows < 4e6 && c->opt_lb_unroll;
     const KernelPick kp = wf ? (count ? pick_wf0<true>(c->n_tri, cbuf) : pick_wf0<false>(c->n_tri, cbuf))
                              : (count ? pick_kernel<true>(depth, c->n_tri, c->n_lights, lbuf, cbuf,
-                                                          bvh ? c->bvh_depth : 0, reflect_chain(c, f))
+                                                          bvh ? c->bvh_depth : 0, reflect_chain(c, f), small)
                                       : pick_kernel<false>(depth, c->n_tri, c->n_lights, lbuf, cbuf,
-                                                           bvh ? c->bvh_depth : 0, reflect_chain(c, f)));
+                                                           bvh ? c->bvh_depth : 0, reflect_chain(c, f), small));
     if (!kp.k) {
         c->err = "reachable bounce depth " + std::to_string(depth) + " exceeds the compiled stack (32)";
         return RT_E_UNSUPPORTED;

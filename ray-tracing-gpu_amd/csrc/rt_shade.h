@@ -538,7 +538,7 @@ __device__ __forceinline__ bool lb_walk_lds(const SceneDev& S, bool use, int cel
 // those lanes (the covered ones).
 // BIG (the big-list kernel): multi-cell waves walk staged in LDS, and lanes
 // beyond a level's dcov take the next level of the ladder.
-template <bool BIG>
+template <bool BIG, bool UNROLL = false>
 __device__ __forceinline__ bool lb_slot(const SceneDev& S, int slot, const Vec3 P, const Vec3 L, float dist, bool cand,
                                         bool& occ, Counters& cnt)
 {
@@ -595,34 +595,89 @@ __device__ __forceinline__ bool lb_slot(const SceneDev& S, int slot, const Vec3 
     if (BIG && !one_cell && bu && lb_walk_lds(S, use, cell, e, end, P, L, dist, occ, cnt))
         end = e;  // walked: skip the global walk below
     bool have = e < end;
-    for (;;) {
-        const bool act = have & !occ;
-        if (!__any(act)) break;
-        RT_EV(cnt, 3);
-        bool go = false;
-        float4 c0 = make_float4(0.f, 0.f, 0.f, 0.f), c1 = c0;
-        float2 c2 = make_float2(0.f, 0.f);
-        if (act) {
-            lb_cell_entry(S.lb_ent, e, c0, c1, c2);
-            if (!(c0.w < dist)) {
-                have = false;  // this and every later entry lie beyond P (dmin)
-            } else {
-                go = true;
-                ++e;
-                have = e < end;
+    if constexpr (UNROLL) {
+        // The per-lane walk two entries per round (WAVE bit 2048: the
+        // big-list depth-0 kernel on frames under 4 Mpx, whose 8 x 8 tiles
+        // see more cells than the LDS-staged walk takes): the two loads
+        // issue together, so a lit point's long list (every entry nearer
+        // than the light) waits one load latency per two entries.  Entries
+        // are taken in list order while nearer than P (dmin < dist), as one
+        // at a time; an entry past an occluding one is not tested.
+        // (profiles/r06/lbwalk/: C3 -6%; on other kernels the extra
+        // registers cost occupancy, so only there.)
+        for (;;) {
+            const bool act = have & !occ;
+            if (!__any(act)) break;
+            RT_EV(cnt, 3);
+            constexpr int K = 2;
+            float4 c0[K], c1[K];
+            float2 c2[K];
+            bool go[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                c0[k] = c1[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+                c2[k] = make_float2(0.f, 0.f);
+                go[k] = false;
+                if (act & (e + (unsigned)k < end)) lb_cell_entry(S.lb_ent, e + (unsigned)k, c0[k], c1[k], c2[k]);
+            }
+            if (act) {
+                bool open = true;
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    go[k] = open & (e < end) & (c0[k].w < dist);
+                    e += go[k] ? 1u : 0u;
+                    open = go[k];
+                }
+                have = open & (e < end);
+            }
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const bool g = go[k] & !occ;
+                if (__any(g)) {
+                    ++cnt.tri;
+                    RT_EV(cnt, 4);
+                    if (g) {
+                        const Vec3 e1 = make3(c1[k].x, c1[k].y, c1[k].z), e2 = make3(c1[k].w, c2[k].x, c2[k].y);
+                        const TriU u = tri_u(make3(c0[k].x, c0[k].y, c0[k].z), e1, e2, P, L);
+                        if (__any(u.ok)) {
+                            float t;
+                            const bool ok = tri_vt(u, e1, e2, L, t);
+                            occ |= ok & (t > kEps) & (t < dist);
+                        }
+                    }
+                }
             }
         }
-        if (__any(go)) {
-            ++cnt.tri;
-            RT_EV(cnt, 4);
-            RT_EVN(cnt, 7, (unsigned)__popcll(__ballot(go)));  // lanes doing a test (RT_PROF)
-            if (go) {
-                const Vec3 e1 = make3(c1.x, c1.y, c1.z), e2 = make3(c1.w, c2.x, c2.y);
-                const TriU u = tri_u(make3(c0.x, c0.y, c0.z), e1, e2, P, L);
-                if (__any(u.ok)) {  // v and t only where some lane's u is in [0, 1]
-                    float t;
-                    const bool ok = tri_vt(u, e1, e2, L, t);
-                    occ |= ok & (t > kEps) & (t < dist);
+    } else {
+        for (;;) {
+            const bool act = have & !occ;
+            if (!__any(act)) break;
+            RT_EV(cnt, 3);
+            bool go = false;
+            float4 c0 = make_float4(0.f, 0.f, 0.f, 0.f), c1 = c0;
+            float2 c2 = make_float2(0.f, 0.f);
+            if (act) {
+                lb_cell_entry(S.lb_ent, e, c0, c1, c2);
+                if (!(c0.w < dist)) {
+                    have = false;  // this and every later entry lie beyond P (dmin)
+                } else {
+                    go = true;
+                    ++e;
+                    have = e < end;
+                }
+            }
+            if (__any(go)) {
+                ++cnt.tri;
+                RT_EV(cnt, 4);
+                RT_EVN(cnt, 7, (unsigned)__popcll(__ballot(go)));  // lanes doing a test (RT_PROF)
+                if (go) {
+                    const Vec3 e1 = make3(c1.x, c1.y, c1.z), e2 = make3(c1.w, c2.x, c2.y);
+                    const TriU u = tri_u(make3(c0.x, c0.y, c0.z), e1, e2, P, L);
+                    if (__any(u.ok)) {  // v and t only where some lane's u is in [0, 1]
+                        float t;
+                        const bool ok = tri_vt(u, e1, e2, L, t);
+                        occ |= ok & (t > kEps) & (t < dist);
+                    }
                 }
             }
         }
@@ -658,7 +713,7 @@ __device__ __forceinline__ bool lb_slot(const SceneDev& S, int slot, const Vec3 
 // within the light's buffer distance walk it (lb_slot); with far buffers
 // (big lists, S.lb_R levels) the lanes beyond walk the next level's; lanes
 // no buffer covers take the per-lane loop over every triangle.
-template <bool BIG>
+template <bool BIG, bool UNROLL = false>
 __device__ __forceinline__ void shadow_opaque_lb(const SceneDev& S, int l, const Vec3 P, const Vec3 L, float dist,
                                                  bool& occ, Counters& cnt)
 {
@@ -670,11 +725,11 @@ __device__ __forceinline__ void shadow_opaque_lb(const SceneDev& S, int l, const
     {
     const float mx = fmaxf(fabsf(L.x), fmaxf(fabsf(L.y), fabsf(L.z)));
     const bool cand = !occ & (mx >= 0.5f);  // a direction the lookup takes
-    bool use = lb_slot<BIG>(S, l, P, L, dist, cand, occ, cnt);
+    bool use = lb_slot<BIG, UNROLL>(S, l, P, L, dist, cand, occ, cnt);
     if constexpr (BIG) {  // big lists: lanes beyond a buffer take the next
         for (int lv = 1; lv < S.lb_R; ++lv) {
             if (!__any(cand & !use & !occ)) break;
-            use |= lb_slot<BIG>(S, lv * S.n_lights + l, P, L, dist, cand & !use, occ, cnt);
+            use |= lb_slot<BIG, UNROLL>(S, lv * S.n_lights + l, P, L, dist, cand & !use, occ, cnt);
         }
     }
     const float slack = dist * 1e-6f;
@@ -773,7 +828,7 @@ __device__ __forceinline__ Color shade_local(const SceneDev& S, const Mat& m, co
             cnt.shadow += gate;
             bool occ = !gate;
             RT_MARK(cnt, 2);
-            shadow_opaque_lb<((WAVE) & 2) != 0>(S, li, P, L, dist, occ, cnt);
+            shadow_opaque_lb<((WAVE) & 2) != 0, ((WAVE) & 2048) != 0>(S, li, P, L, dist, occ, cnt);
             RT_MARK(cnt, 7);
             if (gate) {
                 Color F{0.0f, 0.0f, 0.0f};

@@ -132,6 +132,31 @@ def test_heightfield_without_plane_silhouette(ctx, tmp_path):
     assert mixed >= 5
 
 
+def test_small_big_list_frames_walk_two_entries_per_round(golden_images, c3_column, heightfield_path):
+    """RT_OPT_LB_UNROLL: under 4 Mpx the big-list kernel walks the light
+    buffer's per-lane lists two entries per round (WAVE bit 2048): C3 against
+    the reference's windows, the same bits as the one-entry walk, and the
+    kernel label names the variant that ran."""
+    a, b = rt_amd.Context(0), rt_amd.Context(0, lb_unroll=0)
+    s = rt_amd.Scene(heightfield_path, 1920, 1080, 1)
+    for c in (a, b):
+        c.upload(s)
+    full = a.render_float(s.frame)
+    assert a.stats().kernel == "rt_trace_kernel<0,1,2062>", a.stats().kernel
+    assert bits_equal(full, b.render_float(s.frame))
+    assert b.stats().kernel == "rt_trace_kernel<0,1,14>", b.stats().kernel
+    for k, want in _hf_windows(golden_images, c3_column):
+        r0, r1, c0, c1 = map(int, k.rsplit("_win_", 1)[1].split("_"))
+        check(full[r0:r1, c0:c1], want, 0)
+    f = s.frame.copy()
+    f.cam_pos[0] += 3.0  # a new camera: the per-wave path's variant (no camera buffer yet)
+    torch = pytest.importorskip("torch")
+    o = torch.empty((1080, 1920, 3), dtype=torch.float32, device="cuda")
+    a.render_async(f, 0, o.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert bits_equal(o.cpu().numpy(), b.render_float(f))
+
+
 @pytest.mark.parametrize("mode,stripe", [(0, 0), (2, 0), (2, 3), (2, 4), (3, 0)])
 def test_xcd_deal_modes_render_the_same(golden_images, c3_column, heightfield_path, mode, stripe):
     """RT_OPT_XCD_DEAL: the big-list kernels' tile-to-XCD dealing (padded
