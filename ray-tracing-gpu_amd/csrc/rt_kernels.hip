@@ -2470,13 +2470,17 @@ static int wf_ensure(rt_ctx* c, const rt_frame* f, int rows, int levels, bool ca
 
 // Level 0 of a wavefront frame: the depth-0 kernel with WAVE bit 512.
 template <bool COUNT>
-static KernelPick pick_wf0(int n_tri, bool cbuf)
+static KernelPick pick_wf0(int n_tri, bool cbuf, bool small = false)
 {
     const unsigned win = (unsigned)kLdsWaveBytes;
+    if (n_tri > kClusterMinTriangles && small)  // (the two-entry light-buffer walk, pick_kernel)
+        return cbuf ? kpick<0, 1, 2574, COUNT>(win) : kpick<0, 1, 2566, COUNT>(win);
     if (n_tri > kClusterMinTriangles)
         return cbuf ? kpick<0, 1, 526, COUNT>(win) : kpick<0, 1, 518, COUNT>(win);
     return cbuf ? kpick<0, 1, 525, COUNT>(0) : kpick<0, 1, 517, COUNT>(0);
 }
+
+static bool W_px_small(const rt_ctx* c) { return (double)c->wf.px < 4e6; }
 
 // The bounce levels and folds of a wavefront frame, after level 0 on st:
 // per level a trace launch (the BVH walk; LDS = its stack) and a shade
@@ -2487,7 +2491,10 @@ static int wf_levels(rt_ctx* c, const SceneDev& S, const FrameDev& F, int levels
     const bool big = c->n_tri > kClusterMinTriangles;
     const void* kt = count ? (const void*)&rt_wf_trace<true> : (const void*)&rt_wf_trace<false>;
     const void* kg = count ? (const void*)&rt_wf_straggle<true> : (const void*)&rt_wf_straggle<false>;
-    const void* ks = big ? (count ? (const void*)&rt_wf_shade<6, true> : (const void*)&rt_wf_shade<6, false>)
+    // (frames under 4 Mpx: the two-entry light-buffer walk, pick_kernel)
+    const bool small = c->opt_lb_unroll && W_px_small(c);
+    const void* ks = big ? (small ? (count ? (const void*)&rt_wf_shade<2054, true> : (const void*)&rt_wf_shade<2054, false>)
+                                  : (count ? (const void*)&rt_wf_shade<6, true> : (const void*)&rt_wf_shade<6, false>))
                          : (count ? (const void*)&rt_wf_shade<5, true> : (const void*)&rt_wf_shade<5, false>);
     const unsigned lds_t = (unsigned)((size_t)c->bvh_depth * 64 * sizeof(int));
     const unsigned lds_s = big ? (unsigned)kLdsWaveBytes : 0u;
@@ -2596,7 +2603,7 @@ static int launch(rt_ctx* c, const rt_frame* f, unsigned* rgba_dev, float* rgb_d
     }
     const bool count = (f->flags & RT_FLAG_STATS) != 0;
     const bool small = (double)f->width * rows < 4e6 && c->opt_lb_unroll;
-    const KernelPick kp = wf ? (count ? pick_wf0<true>(c->n_tri, cbuf) : pick_wf0<false>(c->n_tri, cbuf))
+    const KernelPick kp = wf ? (count ? pick_wf0<true>(c->n_tri, cbuf, small) : pick_wf0<false>(c->n_tri, cbuf, small))
                              : (count ? pick_kernel<true>(depth, c->n_tri, c->n_lights, lbuf, cbuf,
                                                           bvh ? c->bvh_depth : 0, reflect_chain(c, f), small)
                                       : pick_kernel<false>(depth, c->n_tri, c->n_lights, lbuf, cbuf,
