@@ -263,8 +263,9 @@ enum {
                                    live rays by counting sorts on the device: bit 0 by
                                    their parent surface's bin (BVH leaf order) and branch
                                    before the BVH walk, bit 1 by their hit surface's bin
-                                   before the shading; 0 queue order; default 1; never
-                                   changes an image */
+                                   before the shading (with bit 2: by the hit point's
+                                   light-buffer cell seen from light 0 instead); 0 queue
+                                   order; default 1; never changes an image */
     RT_OPT_XCD_DEAL = 16,       /* launch (ABI 8): how the big-list kernels (more than
                                    1,024 triangles) deal 8 x 8 tiles to the 8 XCDs: 1
                                    (default) runs of 8 along a tile row, 2 column stripes

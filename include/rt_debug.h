@@ -39,7 +39,8 @@ int rt_debug_cb_verify(rt_ctx*, unsigned long long* out3);
 
 /* The last rt_upload_scene's host wall time by part (ms): out[0] records +
  * device copies, out[1] cone / cluster prepasses, out[2] light buffer,
- * out[3] total, out[4..8] the light-buffer build's phases. */
+ * out[3] total, out[4..8] the light-buffer build's phases, out[9] (n >= 10) light
+ * 0's first light buffer's resolution R (6 R^2 cells; 0 without one). */
 int rt_debug_upload_info(rt_ctx*, double* out, int n);
 
 /* The builds' device prefix sum on host counts (n >= 1), in place like its

@@ -703,6 +703,7 @@ struct rt_ctx {
     float4* d_lb_meta = nullptr;
     bool lb_ready = false;
     int lb_levels = 0;  // buffers per light: slot = level * n_lights + light
+    int lb_r0 = 0;      // light 0's first buffer's resolution (cells per face edge)
     size_t lb_entries = 0;
     double lb_build_ms = 0.0;
     float cam_key[3] = {0.f, 0.f, 0.f};
@@ -792,7 +793,7 @@ struct rt_ctx {
         unsigned *kin = nullptr, *kout = nullptr, *kout2 = nullptr, *hist = nullptr;
         unsigned long long* bsum = nullptr;
         size_t kcap = 0, hcap = 0;
-        int sort = 0;  // this frame's RT_OPT_WF_SORT: bit 0 parent sort, bit 1 hit sort
+        int sort = 0;  // this frame's RT_OPT_WF_SORT: bit 0 parent sort, bit 1 hit sort (bit 2: by light cell)
         hipEvent_t ev = nullptr;  // after the last wavefront frame
         hipStream_t last = nullptr;
         bool pending = false;
@@ -982,7 +983,7 @@ RT_EXPORT int rt_set_option(rt_ctx* c, int32_t opt, double v)
     case RT_OPT_BVH: c->opt_bvh = v != 0; return RT_OK;
     case RT_OPT_WAVEFRONT: c->opt_wavefront = v != 0; return RT_OK;
     case RT_OPT_WF_SORT:
-        if (v != 0 && v != 1 && v != 2 && v != 3) return RT_E_ARG;
+        if (v < 0 || v > 7 || v != std::floor(v)) return RT_E_ARG;
         c->opt_wf_sort = (int)v;
         return RT_OK;
     case RT_OPT_XCD_DEAL:
@@ -1465,6 +1466,7 @@ static int lb_build(rt_ctx* c, int ntr, int n_opaque, const std::vector<const fl
             std::memcpy(&m0.y, &db, 4);
             std::memcpy(&m0.z, &nd, 4);
             std::memcpy(&m0.w, &b.R, 4);
+            if (j == 0) c->lb_r0 = b.R;
             meta[2 * j] = m0;
             meta[2 * j + 1] = m1;
         }
@@ -1637,6 +1639,7 @@ RT_EXPORT int rt_upload_scene(rt_ctx* c, const rt_scene_flat* s)
     c->d_lb_ent = c->d_lb_dcap = c->d_lb_meta = nullptr;
     c->lb_ready = false;
     c->lb_levels = 0;
+    c->lb_r0 = 0;
     c->lb_entries = 0;
     hipFree(c->d_uni);
     c->d_uni = nullptr;
@@ -2313,6 +2316,9 @@ static int wf_branch(const rt_ctx* c, const rt_frame* f)
 // (profiles/r06/knobs/)
 #define RT_WF_STRAG_WAVES 32
 #endif
+#ifndef RT_WF_FOLD_BLOCKS
+#define RT_WF_FOLD_BLOCKS 64  // fold launch: 256-thread blocks per CU (4: c5r +0.5%, profiles/r06/knobs2/)
+#endif
 #ifndef RT_WF_SHADE_WAVES
 #define RT_WF_SHADE_WAVES 24  // shade launch: workgroups (one wave each) per CU (= its occupancy)
 #endif
@@ -2442,7 +2448,9 @@ static int wf_ensure(rt_ctx* c, const rt_frame* f, int rows, int levels, bool ca
             W.kcap = w.most;
         }
         // (the hit sort's bins: nbin_half + kWfMissBins)
-        const size_t bins = std::max(2 * (size_t)c->nbin_half, (size_t)c->nbin_half + kWfMissBins);
+        size_t bins = std::max(2 * (size_t)c->nbin_half, (size_t)c->nbin_half + kWfMissBins);
+        if ((c->opt_wf_sort & 4) && c->lb_r0 > 0)  // the light-cell hit sort's bins
+            bins = std::max(bins, 6 * (size_t)c->lb_r0 * (size_t)c->lb_r0 + kWfMissBins);
         if (bins + 1 > W.hcap) {
             free_later(c, W.hist);
             free_later(c, W.bsum);
@@ -2517,7 +2525,7 @@ static int wf_levels(rt_ctx* c, const SceneDev& S, const FrameDev& F, int levels
             const unsigned bins = 2u * c->nbin_half;
             unsigned* next = W.hist + 2 * W.hcap;
             HIP_TRY(c, scan_u32(W.hist, bins, next, W.bsum, st, nullptr, true));
-            hipLaunchKernelGGL(rt_wf_sort_place<0>, dim3(gq), dim3(64), 0, st, F, L, (const unsigned*)nullptr, next,
+            hipLaunchKernelGGL(rt_wf_sort_place<0>, dim3(gq), dim3(64), 0, st, S, F, L, (const unsigned*)nullptr, next,
                                W.kout);
             HIP_TRY(c, hipGetLastError());
             Fl.wf.kout = W.kout;
@@ -2531,15 +2539,27 @@ static int wf_levels(rt_ctx* c, const SceneDev& S, const FrameDev& F, int levels
         if (W.sort & 2) {
             // the level's rays by hit surface's bin for the shading (whose
             // children, appended in that order, then sit by parent bin)
-            const unsigned hb = c->nbin_half + kWfMissBins;
+            // (bit 2: by the hit point's light-buffer cell instead, wf_sort_key<2>)
+            const bool cell = (W.sort & 4) != 0 && c->lb_r0 > 0;
+            const unsigned hb = cell ? 6u * (unsigned)c->lb_r0 * (unsigned)c->lb_r0 + kWfMissBins
+                                     : c->nbin_half + kWfMissBins;
             unsigned *hist2 = W.hist + W.hcap, *next = W.hist + 2 * W.hcap;
             // (both passes read the rays in queue order: consecutive slots,
             // coalesced hit records — the order inside a bin does not matter)
-            hipLaunchKernelGGL(rt_wf_hit_count, dim3(gq), dim3(64), 0, st, F, L, (const unsigned*)nullptr, hist2);
+            if (cell)
+                hipLaunchKernelGGL(rt_wf_hit_count<2>, dim3(gq), dim3(64), 0, st, S, F, L, (const unsigned*)nullptr,
+                                   hist2);
+            else
+                hipLaunchKernelGGL(rt_wf_hit_count<1>, dim3(gq), dim3(64), 0, st, S, F, L, (const unsigned*)nullptr,
+                                   hist2);
             HIP_TRY(c, hipGetLastError());
             HIP_TRY(c, scan_u32(hist2, hb, next, W.bsum, st, nullptr, true));
-            hipLaunchKernelGGL(rt_wf_sort_place<1>, dim3(gq), dim3(64), 0, st, F, L, (const unsigned*)nullptr, next,
-                               W.kout2);
+            if (cell)
+                hipLaunchKernelGGL(rt_wf_sort_place<2>, dim3(gq), dim3(64), 0, st, S, F, L, (const unsigned*)nullptr,
+                                   next, W.kout2);
+            else
+                hipLaunchKernelGGL(rt_wf_sort_place<1>, dim3(gq), dim3(64), 0, st, S, F, L, (const unsigned*)nullptr,
+                                   next, W.kout2);
             HIP_TRY(c, hipGetLastError());
             Fs.wf.kout = W.kout2;
         }
@@ -2547,7 +2567,7 @@ static int wf_levels(rt_ctx* c, const SceneDev& S, const FrameDev& F, int levels
         HIP_TRY(c, hipLaunchKernel(ks, dim3(gs), dim3(64), sargs, lds_s, st));
     }
     for (int L = levels - 1; L >= 0; --L) {
-        const unsigned g = (unsigned)std::min<size_t>((c->wf.pcap[L] + 255) / 256, (size_t)c->n_cu * 4);
+        const unsigned g = (unsigned)std::min<size_t>((c->wf.pcap[L] + 255) / 256, (size_t)c->n_cu * RT_WF_FOLD_BLOCKS);
         hipLaunchKernelGGL(rt_wf_fold, dim3(std::max(1u, g)), dim3(256), 0, st, F, L, rgba, rgbf);
         HIP_TRY(c, hipGetLastError());
     }
@@ -3125,6 +3145,7 @@ RT_EXPORT int rt_debug_upload_info(rt_ctx* c, double* out, int n)
     // light-buffer build phases: cone records to the host, host preparation,
     // supercell counts + scan, supercell lists + cell counts + scan, entries
     for (int i = 0; i < 5 && 4 + i < n; ++i) out[4 + i] = c->lb_parts_ms[i];
+    if (n > 9) out[9] = c->lb_r0;  // light 0's first buffer: cells per face edge (0: none)
     return RT_OK;
 }
 

@@ -192,16 +192,34 @@ __device__ __forceinline__ bool wf_children(const FrameDev& F, int L, bool act, 
 // every miss serialised all waves' atomics on one address).
 // order: the level's slots in the trace's order (null: queue order).
 constexpr unsigned kWfMissBins = 256;
+// KEY 2 (RT_OPT_WF_SORT bit 2 with bit 1): the light-buffer cell of the hit
+// point seen from light 0 (lb_cell of P - light, the direction the shading's
+// lookup takes, at light 0's first buffer's resolution), so a wave's lanes
+// share one cell and walk its list once (lb_slot's one-cell path); misses in
+// kWfMissBins bins after the 6 R^2 cells.  Only the order: the key may be
+// any function of the ray.
 template <int KEY>
-__device__ __forceinline__ unsigned wf_sort_key(const FrameDev& F, unsigned slot, unsigned x)
+__device__ __forceinline__ unsigned wf_sort_key(const SceneDev& S, const FrameDev& F, int L, unsigned slot,
+                                                unsigned x)
 {
     if constexpr (KEY == 0) return F.wf.kin[slot];
-    const int idx = __float_as_int(F.wf.hit[slot].x);
+    const float2 h = F.wf.hit[slot];
+    const int idx = __float_as_int(h.x);
+    if constexpr (KEY == 2) {
+        const int R = __float_as_int(S.lb_meta[0].w);
+        const unsigned ncell = 6u * (unsigned)R * (unsigned)R;
+        if (idx < 0) return ncell + ((x >> 6) & (kWfMissBins - 1u));
+        const float4 r0 = F.wf.ray[L][2 * (size_t)slot], r1 = F.wf.ray[L][2 * (size_t)slot + 1];
+        const Vec3 P = make3(r0.x, r0.y, r0.z) + h.y * make3(r1.x, r1.y, r1.z);
+        const float4 l0 = S.lights[0];
+        return (unsigned)lb_cell(P - make3(l0.x, l0.y, l0.z), R);
+    }
     return idx >= 0 ? F.wf.skey[idx] : F.wf.nbin_half + ((x >> 6) & (kWfMissBins - 1u));
 }
 
-__global__ __launch_bounds__(64) void rt_wf_hit_count(const FrameDev F, int L, const unsigned* __restrict__ order,
-                                                      unsigned* __restrict__ hist)
+template <int KEY>
+__global__ __launch_bounds__(64) void rt_wf_hit_count(const SceneDev S, const FrameDev F, int L,
+                                                      const unsigned* __restrict__ order, unsigned* __restrict__ hist)
 {
     const WfQueue Q = wf_queue(F.wf.count, wf_rays(L, 0), F.wf.seg[L]);
     const unsigned n = Q.pre[kWfSeg];
@@ -209,13 +227,14 @@ __global__ __launch_bounds__(64) void rt_wf_hit_count(const FrameDev F, int L, c
         const unsigned x = base + (threadIdx.x & 63u);
         const bool valid = x < n;
         const unsigned slot = valid ? (order ? order[x] : wf_slot(Q, x)) : 0u;
-        wave_bins_count(valid, valid ? wf_sort_key<1>(F, slot, x) : 0u, hist);
+        wave_bins_count(valid, valid ? wf_sort_key<KEY>(S, F, L, slot, x) : 0u, hist);
     }
 }
 
 template <int KEY>
-__global__ __launch_bounds__(64) void rt_wf_sort_place(const FrameDev F, int L, const unsigned* __restrict__ order,
-                                                       unsigned* __restrict__ next, unsigned* __restrict__ kout)
+__global__ __launch_bounds__(64) void rt_wf_sort_place(const SceneDev S, const FrameDev F, int L,
+                                                       const unsigned* __restrict__ order, unsigned* __restrict__ next,
+                                                       unsigned* __restrict__ kout)
 {
     const WfQueue Q = wf_queue(F.wf.count, wf_rays(L, 0), F.wf.seg[L]);
     const unsigned n = Q.pre[kWfSeg];
@@ -223,7 +242,7 @@ __global__ __launch_bounds__(64) void rt_wf_sort_place(const FrameDev F, int L, 
         const unsigned x = base + (threadIdx.x & 63u);
         const bool valid = x < n;
         const unsigned slot = valid ? (order ? order[x] : wf_slot(Q, x)) : 0u;
-        const unsigned k = valid ? wf_sort_key<KEY>(F, slot, x) : 0u;
+        const unsigned k = valid ? wf_sort_key<KEY>(S, F, L, slot, x) : 0u;
         const unsigned pos = wave_bins_place(valid, k, next);
         if (valid) kout[pos] = slot;
     }

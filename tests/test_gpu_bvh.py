@@ -417,10 +417,11 @@ def test_negative_min_energy_spawns_both_children(tmp_path, oracle):
     _three_ways(path, 1920, 1080, 3, -1.0, oracle)
 
 
-@pytest.mark.parametrize("sort", [0, 2, 3])
+@pytest.mark.parametrize("sort", [0, 2, 3, 6, 7])
 def test_wavefront_sort_orders_render_the_same(hfr, hfr_golden, sort):
     """RT_OPT_WF_SORT (the counting sorts of each level's live rays by parent
-    bin and by hit bin) only changes which wave takes which ray: the
+    bin and by hit bin or, bit 2, the hit's light-buffer cell) only changes
+    which wave takes which ray: the
     reflective heightfield at 1920 x 1080 d3 and d6 against the reference's
     windows, bit for bit, and the refracting mesh against the default."""
     ctx, get = hfr
@@ -449,7 +450,7 @@ def test_refractive_mesh_sort_orders(tmp_path):
     path.write_text("\n".join(lines))
     s = rt_amd.Scene(str(path), 1920, 1080, 4)
     imgs = []
-    for sort in (0, 1, 2, 3):
+    for sort in (0, 1, 2, 3, 7):
         c = rt_amd.Context(0, wf_sort=sort)
         c.upload(s)
         imgs.append(c.render_float(s.frame))
