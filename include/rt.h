@@ -278,6 +278,11 @@ enum {
                                    under 4 Mpx of output rows walk the light buffer's
                                    per-lane lists two entries per round: 1 (default) / 0;
                                    never changes an image */
+    RT_OPT_WF_OVERLAP = 19,     /* launch (ABI 8): wavefront frames finish each level's
+                                   straggling BVH walks and shade their rays on a second
+                                   stream while the level's other rays are shaded (one
+                                   event fork and join per level): 1 (default) / 0;
+                                   never changes an image */
     RT_OPT_LAUNCH_CAMERA = 12   /* launch (ABI 6): depth-0 frames of scenes of 1-20
                                    triangles with light-buffer shadows take their camera
                                    records with the kernel launch — per-triangle camera

@@ -795,11 +795,14 @@ struct rt_ctx {
         size_t kcap = 0, hcap = 0;
         int sort = 0;  // this frame's RT_OPT_WF_SORT: bit 0 parent sort, bit 1 hit sort (bit 2: by light cell)
         hipEvent_t ev = nullptr;  // after the last wavefront frame
+        hipStream_t st2 = nullptr;               // RT_OPT_WF_OVERLAP: the stragglers' stream
+        hipEvent_t ev_t = nullptr, ev_s = nullptr;  // fork (after the trace) / join (after the stragglers' shading)
         hipStream_t last = nullptr;
         bool pending = false;
     } wf;
     int opt_wavefront = 1;      // RT_OPT_WAVEFRONT
     int opt_wf_sort = 1;        // RT_OPT_WF_SORT
+    bool opt_wf_overlap = true; // RT_OPT_WF_OVERLAP
     int opt_xcd_deal = 1;       // RT_OPT_XCD_DEAL
     int opt_xcd_stripe = 0;     // RT_OPT_XCD_STRIPE
     bool opt_lb_unroll = true;  // RT_OPT_LB_UNROLL
@@ -986,6 +989,7 @@ RT_EXPORT int rt_set_option(rt_ctx* c, int32_t opt, double v)
         if (v < 0 || v > 7 || v != std::floor(v)) return RT_E_ARG;
         c->opt_wf_sort = (int)v;
         return RT_OK;
+    case RT_OPT_WF_OVERLAP: c->opt_wf_overlap = v != 0; return RT_OK;
     case RT_OPT_XCD_DEAL:
         if (v != 0 && v != 1 && v != 2 && v != 3) return RT_E_ARG;
         c->opt_xcd_deal = (int)v;
@@ -1020,6 +1024,7 @@ RT_EXPORT int rt_get_option(rt_ctx* c, int32_t opt, double* v)
     case RT_OPT_BVH: *v = c->opt_bvh ? 1 : 0; return RT_OK;
     case RT_OPT_WAVEFRONT: *v = c->opt_wavefront; return RT_OK;
     case RT_OPT_WF_SORT: *v = c->opt_wf_sort; return RT_OK;
+    case RT_OPT_WF_OVERLAP: *v = c->opt_wf_overlap ? 1 : 0; return RT_OK;
     case RT_OPT_XCD_DEAL: *v = c->opt_xcd_deal; return RT_OK;
     case RT_OPT_XCD_STRIPE: *v = c->opt_xcd_stripe; return RT_OK;
     case RT_OPT_LB_UNROLL: *v = c->opt_lb_unroll ? 1 : 0; return RT_OK;
@@ -1103,6 +1108,9 @@ RT_EXPORT void rt_destroy(rt_ctx* c)
     hipFree(c->wf.bsum);
     hipFree(c->d_skey);
     if (c->wf.ev) hipEventDestroy(c->wf.ev);
+    if (c->wf.ev_t) hipEventDestroy(c->wf.ev_t);
+    if (c->wf.ev_s) hipEventDestroy(c->wf.ev_s);
+    if (c->wf.st2) hipStreamDestroy(c->wf.st2);
     for (auto& q : c->tiny_masks) {
         hipFree(q.d);
         if (q.ev) hipEventDestroy(q.ev);
@@ -2341,8 +2349,8 @@ static int wf_branch(const rt_ctx* c, const rt_frame* f)
 // chunks c = s (mod kWfSeg), at most 64 * branch each — then the bytes:
 // counters; level-0 node records (32 B) per pixel and its parent list;
 // per level L >= 1 the rays (32 B), colours (16 B) and, but for the deepest
-// level, node records (32 B) and the parent list; the hit records (8 B) and
-// straggler queue (16 B) of the largest level.
+// level, node records (32 B) and the parent list; the hit records (8 B),
+// straggler queue (16 B) and stragglers' minima (8 B) of the largest level.
 struct WfLayout {
     size_t cap[kWfMaxLevels + 1] = {}, pcap[kWfMaxLevels + 1] = {};
     unsigned seg[kWfMaxLevels + 1] = {}, pseg[kWfMaxLevels + 1] = {};
@@ -2371,7 +2379,7 @@ static WfLayout wf_layout(size_t tiles, size_t px, int levels, int branch)
         tot += a(w.cap[L] * 32) + a(w.cap[L] * 16);
         if (L < levels) tot += a(w.cap[L] * 32) + a(w.pcap[L] * 4);
     }
-    w.bytes = tot + a(w.most * 8) + a(w.most * 16);
+    w.bytes = tot + a(w.most * 8) + a(w.most * 16) + a(w.most * 8);  // hit, strag, hit2
     return w;
 }
 
@@ -2428,6 +2436,7 @@ static int wf_ensure(rt_ctx* c, const rt_frame* f, int rows, int levels, bool ca
     }
     d.hit = (float2*)take(w.most * 8);
     d.strag = (int4*)take(w.most * 16);
+    d.hit2 = (float2*)take(w.most * 8);
     d.levels = levels;
     d.kin = nullptr;
     d.kout = nullptr;
@@ -2504,9 +2513,21 @@ static int wf_levels(rt_ctx* c, const SceneDev& S, const FrameDev& F, int levels
     const void* ks = big ? (small ? (count ? (const void*)&rt_wf_shade<2054, true> : (const void*)&rt_wf_shade<2054, false>)
                                   : (count ? (const void*)&rt_wf_shade<6, true> : (const void*)&rt_wf_shade<6, false>))
                          : (count ? (const void*)&rt_wf_shade<5, true> : (const void*)&rt_wf_shade<5, false>);
+    // (RT_OPT_WF_OVERLAP: the stragglers' walks and shading on a second
+    // stream, beside the level's main shade launch)
+    const void* ks2 =
+        big ? (small ? (count ? (const void*)&rt_wf_shade<2054, true, true> : (const void*)&rt_wf_shade<2054, false, true>)
+                     : (count ? (const void*)&rt_wf_shade<6, true, true> : (const void*)&rt_wf_shade<6, false, true>))
+            : (count ? (const void*)&rt_wf_shade<5, true, true> : (const void*)&rt_wf_shade<5, false, true>);
     const unsigned lds_t = (unsigned)((size_t)c->bvh_depth * 64 * sizeof(int));
     const unsigned lds_s = big ? (unsigned)kLdsWaveBytes : 0u;
     rt_ctx::WfBuf& W = c->wf;
+    const bool ovl = c->opt_wf_overlap;
+    if (ovl) {
+        if (!W.st2) HIP_TRY(c, hipStreamCreateWithFlags(&W.st2, hipStreamNonBlocking));
+        if (!W.ev_t) HIP_TRY(c, hipEventCreateWithFlags(&W.ev_t, hipEventDisableTiming));
+        if (!W.ev_s) HIP_TRY(c, hipEventCreateWithFlags(&W.ev_s, hipEventDisableTiming));
+    }
     for (int L = 1; L <= levels; ++L) {
         // enough waves to fill the chip; each strides over the level's queue
         const size_t waves = (W.cap[L] + 63) / 64;
@@ -2514,6 +2535,7 @@ static int wf_levels(rt_ctx* c, const SceneDev& S, const FrameDev& F, int levels
         const unsigned gs = (unsigned)std::max<size_t>(1, std::min<size_t>(waves, (size_t)c->n_cu * RT_WF_SHADE_WAVES));
         FrameDev Fl = F;
         Fl.wf.budget = W.cap[L] >= (size_t)RT_WF_BUDGET_SPLIT ? RT_WF_BUDGET_BIG : RT_WF_BUDGET_SMALL;
+        if (!ovl) Fl.wf.hit2 = nullptr;
         const unsigned gq = (unsigned)std::max<size_t>(1, std::min<size_t>(waves, (size_t)c->n_cu * 32));
         if (W.dev.kin) {
             // the level's live rays by bin (parent surface in BVH leaf order,
@@ -2533,8 +2555,9 @@ static int wf_levels(rt_ctx* c, const SceneDev& S, const FrameDev& F, int levels
         int Lv = L;
         void* args[] = {(void*)&S, (void*)&Fl, (void*)&Lv, (void*)&stats};
         HIP_TRY(c, hipLaunchKernel(kt, dim3(gt), dim3(64), args, lds_t, st));
-        HIP_TRY(c, hipLaunchKernel(kg, dim3((unsigned)c->n_cu * RT_WF_STRAG_WAVES), dim3(64), args,
-                                   (unsigned)(kWfStragCap * sizeof(int)), st));
+        if (!ovl)
+            HIP_TRY(c, hipLaunchKernel(kg, dim3((unsigned)c->n_cu * RT_WF_STRAG_WAVES), dim3(64), args,
+                                       (unsigned)(kWfStragCap * sizeof(int)), st));
         FrameDev Fs = Fl;
         if (W.sort & 2) {
             // the level's rays by hit surface's bin for the shading (whose
@@ -2564,7 +2587,19 @@ static int wf_levels(rt_ctx* c, const SceneDev& S, const FrameDev& F, int levels
             Fs.wf.kout = W.kout2;
         }
         void* sargs[] = {(void*)&S, (void*)&Fs, (void*)&Lv, (void*)&stats};
+        if (ovl) {
+            // fork: the stragglers finish their walks (into hit2) and are
+            // shaded on st2 while st shades the level's other rays; join
+            // before the next level reads its queue
+            HIP_TRY(c, hipEventRecord(W.ev_t, st));
+            HIP_TRY(c, hipStreamWaitEvent(W.st2, W.ev_t, 0));
+            HIP_TRY(c, hipLaunchKernel(kg, dim3((unsigned)c->n_cu * RT_WF_STRAG_WAVES), dim3(64), args,
+                                       (unsigned)(kWfStragCap * sizeof(int)), W.st2));
+            HIP_TRY(c, hipLaunchKernel(ks2, dim3(gs), dim3(64), sargs, lds_s, W.st2));
+            HIP_TRY(c, hipEventRecord(W.ev_s, W.st2));
+        }
         HIP_TRY(c, hipLaunchKernel(ks, dim3(gs), dim3(64), sargs, lds_s, st));
+        if (ovl) HIP_TRY(c, hipStreamWaitEvent(st, W.ev_s, 0));
     }
     for (int L = levels - 1; L >= 0; --L) {
         const unsigned g = (unsigned)std::min<size_t>((c->wf.pcap[L] + 255) / 256, (size_t)c->n_cu * RT_WF_FOLD_BLOCKS);

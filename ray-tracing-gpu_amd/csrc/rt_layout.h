@@ -155,6 +155,11 @@ struct WfDev {
     unsigned seg[kWfMaxLevels + 1];   // ray slots per segment, level L >= 1
     unsigned pseg[kWfMaxLevels + 1];  // parent slots per segment, level L >= 0
     float2* hit;      // the level being shaded: [file index (int bits), t] per ray slot
+    // RT_OPT_WF_OVERLAP: the straggling walks finish (and their rays are
+    // shaded) on a second stream while the level's other rays are shaded:
+    // the trace leaves kWfPending in hit[slot] for a straggler, and the
+    // straggler kernel writes its minimum here instead; null: into hit.
+    float2* hit2;
     int4* strag;      // the level's straggling walks: [ray slot, partial t (bits), partial index, -]
     unsigned* count;  // counters, kWfCntStride words apart: wf_rays / wf_pars / wf_strag
     // Coherence sort (round 6): a ray being appended writes its bin into

@@ -192,6 +192,7 @@ __device__ __forceinline__ bool wf_children(const FrameDev& F, int L, bool act, 
 // every miss serialised all waves' atomics on one address).
 // order: the level's slots in the trace's order (null: queue order).
 constexpr unsigned kWfMissBins = 256;
+constexpr int kWfPending = -2;  // hit[slot] of a straggler whose minimum goes to hit2 (WfDev::hit2)
 // KEY 2 (RT_OPT_WF_SORT bit 2 with bit 1): the light-buffer cell of the hit
 // point seen from light 0 (lb_cell of P - light, the direction the shading's
 // lookup takes, at light 0's first buffer's resolution), so a wave's lanes
@@ -438,6 +439,7 @@ __global__ __launch_bounds__(64) void rt_wf_trace(const SceneDev S, const FrameD
             if (lane == lead) sb = atomicAdd(&F.wf.count[wf_strag(L)], (unsigned)__popcll(bs));
             sb = (unsigned)__builtin_amdgcn_readlane((int)sb, lead);
             if (str) F.wf.strag[sb + lane_rank(bs)] = make_int4((int)slot, __float_as_int(bt), bi, 0);
+            if (str && F.wf.hit2) F.wf.hit[slot] = make_float2(__int_as_float(kWfPending), bt);
         }
         if (fin) F.wf.hit[slot] = make_float2(__int_as_float(bi), bt);
         if (fin | str) busy = false;
@@ -469,7 +471,7 @@ __global__ __launch_bounds__(64) void rt_wf_straggle(const SceneDev S, const Fra
         float bt = __int_as_float(rec.y);
         int bi = rec.z;
         bvh_walk_wave(S, make3(r0.x, r0.y, r0.z), make3(r1.x, r1.y, r1.z), bt, bi, stk, kWfStragCap, cnt);
-        if ((threadIdx.x & 63) == 0) F.wf.hit[i] = make_float2(__int_as_float(bi), bt);
+        if ((threadIdx.x & 63) == 0) (F.wf.hit2 ? F.wf.hit2 : F.wf.hit)[i] = make_float2(__int_as_float(bi), bt);
     }
     if (COUNT && (F.flags & RT_FLAG_STATS)) {
         // the lanes tally the work they did; the wave's one ray counts once
@@ -486,7 +488,11 @@ __global__ __launch_bounds__(64) void rt_wf_straggle(const SceneDev S, const Fra
 #ifndef RT_WF_SHADE_EU
 #define RT_WF_SHADE_EU 6
 #endif
-template <int WAVE, bool COUNT>
+// STRAG (RT_OPT_WF_OVERLAP, on the second stream after rt_wf_straggle):
+// only the stragglers (hit = kWfPending), with their minima from hit2, in
+// the same order and 64-ray chunks as the main launch — which skips them —
+// so every chunk's children still go to its own queue segment.
+template <int WAVE, bool COUNT, bool STRAG = false>
 __global__ __launch_bounds__(64, RT_WF_SHADE_EU) void rt_wf_shade(const SceneDev S, const FrameDev F, int L,
                                                   StatsDev* __restrict__ stats)
 {
@@ -499,7 +505,14 @@ __global__ __launch_bounds__(64, RT_WF_SHADE_EU) void rt_wf_shade(const SceneDev
         const unsigned x = base + (threadIdx.x & 63u);
         if (x < n) {
             const unsigned i = F.wf.kout ? F.wf.kout[x] : wf_slot(Q, x);
-            const float2 h = F.wf.hit[i];
+            float2 h = F.wf.hit[i];
+            const bool pending = __float_as_int(h.x) == kWfPending;
+            if constexpr (STRAG) {
+                if (!pending) continue;
+                h = F.wf.hit2[i];
+            } else {
+                if (pending) continue;
+            }
             const int idx = __float_as_int(h.x);
             Color res = bg;
             bool parent = false;

@@ -36,7 +36,7 @@ FLAG_STATS = 1
 # rt.h RT_OPT_* (ABI 5): A/B and test switches, none changes an image bit
 OPTIONS = {"light_buffer": 1, "camera_buffer": 2, "union_pretest": 3, "lb_scale": 4, "dcov_near": 5,
            "cb_inline_max_mb": 6, "host_chunk_mb": 7, "cb_capacity": 8, "launch_camera": 12, "bvh": 13, "wavefront": 14,
-           "wf_sort": 15, "xcd_deal": 16, "xcd_stripe": 17, "lb_unroll": 18}
+           "wf_sort": 15, "xcd_deal": 16, "xcd_stripe": 17, "lb_unroll": 18, "wf_overlap": 19}
 _ERRORS = {-1: "RT_E_ARG", -2: "RT_E_IO", -3: "RT_E_PARSE", -4: "RT_E_STATE", -5: "RT_E_HIP",
            -6: "RT_E_UNSUPPORTED"}
 

@@ -162,7 +162,7 @@ def test_option_enum_matches_binding_and_round_trips():
     values = {"light_buffer": 2, "camera_buffer": 2, "union_pretest": 0, "lb_scale": 8, "dcov_near": 1.5,
               "cb_inline_max_mb": 64, "host_chunk_mb": 4, "cb_capacity": 1000, "launch_camera": 0, "bvh": 0, "wavefront": 0,
               "wf_sort": 0, "xcd_deal": 3, "xcd_stripe": 4,
-              "lb_unroll": 0}
+              "lb_unroll": 0, "wf_overlap": 0}
     assert set(values) == set(enum)
     try:
         for name, v in values.items():

@@ -436,6 +436,25 @@ def test_wavefront_sort_orders_render_the_same(hfr, hfr_golden, sort):
         ctx.set_option("wf_sort", 1)
 
 
+def test_straggler_overlap_renders_the_same(hfr, hfr_golden):
+    """RT_OPT_WF_OVERLAP (the stragglers' walks and shading on a second
+    stream beside each level's shade launch) on and off: the same images, and
+    the reference's windows at d3 and d6 with it off."""
+    ctx, get = hfr
+    for d in (3, 6):
+        f = get(1920, 1080, d).frame
+        on = ctx.render_float(f)
+        ctx.set_option("wf_overlap", 0)
+        try:
+            off = ctx.render_float(f)
+        finally:
+            ctx.set_option("wf_overlap", 1)
+        assert bits_equal(on, off), d
+        for win, want, k in _groups(hfr_golden)[(1920, 1080, d)]:
+            r0, r1, c0, c1 = win
+            assert bits_equal(off[r0:r1, c0:c1], want), k
+
+
 def test_refractive_mesh_sort_orders(tmp_path):
     from rt_amd import synth
 
@@ -450,8 +469,8 @@ def test_refractive_mesh_sort_orders(tmp_path):
     path.write_text("\n".join(lines))
     s = rt_amd.Scene(str(path), 1920, 1080, 4)
     imgs = []
-    for sort in (0, 1, 2, 3, 7):
-        c = rt_amd.Context(0, wf_sort=sort)
+    for sort, ovl in ((0, 1), (1, 1), (2, 1), (3, 1), (7, 1), (1, 0), (3, 0)):
+        c = rt_amd.Context(0, wf_sort=sort, wf_overlap=ovl)
         c.upload(s)
         imgs.append(c.render_float(s.frame))
         assert c.stats().kernel.startswith("wavefront")
